@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X retrieval hot path (BASELINE.json configs[1]: 1M synthetic docs, d=1024,
+batch 32, top-k 5, fused similarity + top-k through the C-ABI).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp32|bf16] [--metric cosine|dot]
+    N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+A step = one batch of B queries through the whole device pipeline (fused MFMA similarity + top-k over
+the rank's corpus shard, per-shard merge, RCCL all-gather of candidates when N > 1, final merge), with
+the queries already resident in HBM. The corpus (N_DOCS x d, fixed total: strong scaling) is generated
+on device. Rank 0 prints ONE JSON line.
+
+Also reported: host-inclusive latency (H2D of the queries + pipeline + D2H of results) p50/p99 over
+synchronous batches, and the CPU baseline = the oracle's restatement of the reference SimpleRetriever
+(per-query fp32 matvec + argpartition + argsort) timed on the host cores on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "rag-serving-system_amd"))
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def cpu_baseline(n_docs: int, d: int, batch: int, k: int, batches: int, threads: int) -> dict:
+    """Reference SimpleRetriever algorithm (oracle restatement) on the host: bounded sample."""
+    from threadpoolctl import threadpool_limits
+    from oracle import synth
+    from oracle.retriever_oracle import simple_batch_retrieve
+    corpus = synth.unit_norm_gaussian(4321, n_docs, d)
+    q = synth.unit_norm_gaussian(8765, batch * batches, d)
+    with threadpool_limits(limits=threads):
+        simple_batch_retrieve(corpus, q[:2], [k, k])            # warm
+        t0 = time.perf_counter()
+        for i in range(batches):
+            simple_batch_retrieve(corpus, q[i * batch:(i + 1) * batch], [k] * batch)
+        dt = time.perf_counter() - t0
+    return {"value": round(batch * batches / dt, 3), "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"{batches} batches x {batch} queries, {n_docs} x {d} fp32 unit-norm corpus, k={k}; "
+                      f"oracle restatement of SimpleRetriever.batch_retrieve (retriever.py:131-166), "
+                      f"OpenBLAS limited to {threads} threads"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--docs", type=int, default=1_000_000)
+    ap.add_argument("--dim", type=int, default=1024)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--k", type=int, default=5)
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--metric", default="cosine", choices=["cosine", "dot"])
+    ap.add_argument("--latency-steps", type=int, default=200)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batches", type=int, default=3)
+    ap.add_argument("--traffic-bytes", type=float, default=None,
+                    help="HBM bytes per fused launch from a rocprofv3 --pmc pass (FETCH_SIZE, gfx950-corrected)")
+    args = ap.parse_args()
+
+    from rag_service_amd import Index, get_unique_id
+    from rag_service_amd import _lib
+    from rag_service_amd.dist import (barrier, broadcast_bytes, env_rank_world, init_control_plane,
+                                      max_over_ranks)
+
+    rank, world, local = env_rank_world()
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    dist = init_control_plane(world, rank)
+
+    try:
+        import torch
+        torch.cuda.set_device(local)
+        cuda_sync = torch.cuda.synchronize
+    except Exception:  # torch is plumbing only: timing does not depend on it
+        def cuda_sync():
+            return None
+
+    ix = Index(devices=[local], dtype=args.dtype, metric=args.metric)
+    if world > 1:
+        uid = broadcast_bytes(dist, get_unique_id() if rank == 0 else None)
+        ix.init_dist(world, rank, uid)
+    ix.fill_synthetic(_lib.RR_SYNTH_UNIT_NORM, 1234, args.docs, args.dim)
+    sb, se = ix.shard_range(0)
+    rng = np.random.default_rng(5678)
+    q = rng.standard_normal((args.batch, args.dim)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+
+    # ---- throughput: queries resident in HBM, K back-to-back steps --------------------------------
+    ix.set_queries(q)
+    for _ in range(args.warmup):
+        ix.search_staged(args.k)
+    ix.synchronize()
+    ix.set_timing(True)
+    ix.kernel_time(reset=True)
+    barrier(dist)
+    cuda_sync()
+    ix.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ix.search_staged(args.k)
+    ix.synchronize()
+    cuda_sync()
+    barrier(dist)
+    elapsed = time.perf_counter() - t0
+    kern_ms, launches = ix.kernel_time(reset=True)
+    ix.set_timing(False)
+    elapsed = max_over_ranks(dist, elapsed)
+
+    # ---- latency: host queries in -> host results out, one batch at a time ------------------------
+    lat = []
+    for i in range(args.latency_steps):
+        barrier(dist)
+        t = time.perf_counter()
+        ix.search(q, args.k)
+        lat.append(time.perf_counter() - t)
+    lat_ms = np.array(lat) * 1e3
+    p50 = max_over_ranks(dist, float(np.percentile(lat_ms, 50)))
+    p99 = max_over_ranks(dist, float(np.percentile(lat_ms, 99)))
+
+    # ---- roofline of the fused kernel (rank 0's shard) ---------------------------------------------
+    elem = 4 if args.dtype == "fp32" else 2
+    n_local = se - sb
+    alg_bytes = n_local * args.dim * elem + args.batch * args.dim * 4 + (n_local * 4 if args.metric == "cosine" else 0)
+    avg_kernel_s = (kern_ms / max(launches, 1)) / 1e3
+    achieved = alg_bytes / avg_kernel_s / 1e9 if launches else None
+    traffic = args.traffic_bytes
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline:
+            threads = min(16, os.cpu_count() or 1)
+            cpu = cpu_baseline(args.docs, args.dim, args.batch, args.k, args.cpu_batches, threads)
+        value = args.batch * args.steps / elapsed
+        out = {
+            "metric": "retrieval queries/sec + p99 latency, batch=32, 1M docs d=1024, 1/2/4/8 GPU",
+            "value": round(value, 2),
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (device-generated unit-norm approx-Gaussian rows, seed 1234; unit-norm queries)",
+            "config": {"workload": f"{args.docs} synthetic docs d={args.dim}, batch={args.batch}, top-k={args.k}, "
+                                   f"{args.metric} (CupyRetriever semantics)",
+                       "docs": args.docs, "d": args.dim, "batch": args.batch, "k": args.k,
+                       "metric": args.metric, "corpus_dtype": args.dtype, "parallelism": f"row-shard x{world}"},
+            "p50_ms": round(p50, 4),
+            "p99_ms": round(p99, 4),
+            "latency_note": "host-inclusive per batch: H2D queries + pipeline + D2H results, synchronous",
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                         "traffic": traffic,
+                         "kernel": "fused_score_kernel (similarity + top-k)",
+                         "kernel_avg_us": round(avg_kernel_s * 1e6, 2),
+                         "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    barrier(dist)
+    ix.close()
+
+
+if __name__ == "__main__":
+    main()

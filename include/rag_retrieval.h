@@ -1,0 +1,158 @@
+/*
+ * rag_retrieval.h — C-ABI of the MI355X-native dense-retrieval hot path.
+ *
+ * This library replaces the similarity + top-k core of the reference retrievers
+ * (ngray0/RAG-Serving-System, rag_service/core/retriever.py):
+ *   - CupyRetriever.__init__          retriever.py:566-592  -> rr_create + rr_load
+ *   - CupyRetriever.distance_cosine   retriever.py:594-611  -> fused into rr_search (RR_METRIC_COSINE)
+ *   - CupyRetriever.batch_retrieve    retriever.py:686-799  -> rr_search (per-row argpartition/argsort loop
+ *                                                              :750-769 becomes one fused top-k)
+ *   - SimpleRetriever.retrieve        retriever.py:78-128   -> rr_search (RR_METRIC_DOT, b = 1)
+ *   - SimpleRetriever.batch_retrieve  retriever.py:131-166  -> rr_search (RR_METRIC_DOT)
+ * The Python side (rag_service_amd.core.retriever) keeps the reference's validation, k-clamping,
+ * per-query slicing and document lookup; this ABI only sees validated shapes.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only. Host buffers are caller-owned; device buffers are handle-owned.
+ *   - Every int-returning entry point returns RR_OK (0) on success and a negative RR_E* code otherwise;
+ *     rr_last_error() then returns a thread-local message.
+ *   - One caller thread per handle (the reference calls the retriever from the single BatchProcessor
+ *     thread, batch_processor.py:24,95); no internal locking.
+ *   - Results are sorted by (score descending, global document index ascending). Slots beyond the
+ *     number of documents (k > n) hold score -inf and index -1 (the reference pads with -1,
+ *     retriever.py:767-769).
+ *   - Scores: RR_METRIC_DOT = fp32 dot product (SimpleRetriever, retriever.py:112);
+ *     RR_METRIC_COSINE = clip(dot / (|q|*|d| + 1e-8), -1, 1) in the reference's fp32 operation order
+ *     (retriever.py:600-609).
+ *   - Sharding: the corpus rows are split into contiguous shards, one per device. Shards live either in
+ *     one process (rr_create with n_dev > 1; RCCL communicator from ncclCommInitAll) or one per process
+ *     (rr_init_dist; RCCL communicator from a unique id). Per-shard top-k candidates are exchanged with
+ *     a single ncclAllGather and merged on device; every rank ends with the global result.
+ */
+#ifndef RAG_RETRIEVAL_H
+#define RAG_RETRIEVAL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RR_ABI_VERSION 1
+
+/* error codes */
+#define RR_OK             0
+#define RR_E_INVALID     -1   /* bad argument (shape, k, dtype, metric, null pointer) */
+#define RR_E_HIP         -2   /* HIP runtime error */
+#define RR_E_RCCL        -3   /* RCCL error */
+#define RR_E_STATE       -4   /* call out of order (search before load, ...) */
+#define RR_E_UNSUPPORTED -5   /* valid request outside what this build implements */
+#define RR_E_OOM         -6   /* device allocation failed */
+
+/* corpus storage dtype in HBM */
+#define RR_DTYPE_F32  0       /* fp32 rows, fp32 MFMA (v_mfma_f32_32x32x2_f32) */
+#define RR_DTYPE_BF16 1       /* bf16 rows (RNE from fp32), bf16 MFMA with fp32 accumulate */
+
+/* similarity metric */
+#define RR_METRIC_DOT    0    /* SimpleRetriever: raw dot product          (retriever.py:112)      */
+#define RR_METRIC_COSINE 1    /* CupyRetriever: clipped cosine similarity  (retriever.py:594-611)  */
+
+/* synthetic corpus kinds for rr_fill_synthetic */
+#define RR_SYNTH_EXACT_INT 0  /* x = ((h(seed, row*d+col) mod 255) - 127) * 2^-7 ; exact in bf16 and fp32 */
+#define RR_SYNTH_UNIT_NORM 1  /* approx-Gaussian rows (Irwin-Hall of 4 uniforms), L2-normalised in fp32 */
+
+#define RR_UNIQUE_ID_BYTES 128
+
+/* largest k served by the fused single-pass kernel; larger k uses the full-score sort path */
+#define RR_FUSED_KMAX 32
+
+typedef struct rr_handle rr_handle;
+
+/* ---- lifecycle ---------------------------------------------------------------------------------- */
+
+/* Create a handle over n_dev local devices (HIP ordinals). devices == NULL means {0}.
+ * Replaces CupyRetriever.__init__'s device setup (retriever.py:580-586). */
+int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** out);
+
+/* Release every device buffer, stream and communicator the handle owns. NULL is a no-op. */
+void rr_destroy(rr_handle* h);
+
+/* Thread-local description of the last failure on this thread ("" if none). */
+const char* rr_last_error(void);
+
+/* ABI version (RR_ABI_VERSION). */
+int rr_abi_version(void);
+
+/* ---- multi-process sharding (one process per GPU) ---------------------------------------------- */
+
+/* Fill out[RR_UNIQUE_ID_BYTES] with an RCCL unique id (call on rank 0, broadcast out-of-band). */
+int rr_get_unique_id(char* out);
+
+/* Join a world of `world` processes as `rank`; this process's single local device holds global
+ * shard `rank`. Must precede rr_load / rr_load_shard / rr_fill_synthetic. */
+int rr_init_dist(rr_handle* h, int world, int rank, const char* unique_id);
+
+/* ---- corpus ------------------------------------------------------------------------------------ */
+
+/* Load the whole corpus (row-major fp32, n x d) from host memory. In a multi-process world every
+ * rank passes the full matrix and keeps only its shard. Converts to bf16 (RNE) for RR_DTYPE_BF16
+ * and precomputes per-row L2 norms for RR_METRIC_COSINE. (retriever.py:576-582)  */
+int rr_load(rr_handle* h, const float* host_corpus, int64_t n, int32_t d);
+
+/* Load only this handle's shard(s): host_rows holds rows [row_begin, row_begin + n_rows) of a
+ * corpus of n_total rows. The rows must cover exactly the local shards' ranges. */
+int rr_load_rows(rr_handle* h, const float* host_rows, int64_t row_begin, int64_t n_rows,
+                 int64_t n_total, int32_t d);
+
+/* Generate a deterministic synthetic corpus of n_total x d directly in HBM (each shard generates its
+ * own rows from the global row index, so results do not depend on the shard count). */
+int rr_fill_synthetic(rr_handle* h, int kind, uint64_t seed, int64_t n_total, int32_t d);
+
+/* Shape of the loaded corpus and of this handle's local shards. */
+int rr_info(const rr_handle* h, int64_t* n_total, int32_t* d, int32_t* n_local_shards,
+            int32_t* world_shards);
+
+/* Range [begin, end) of global rows held by local shard `i`. */
+int rr_shard_range(const rr_handle* h, int i, int64_t* begin, int64_t* end);
+
+/* Copy rows [row_begin, row_begin + n_rows) of the device-resident corpus back to host as fp32
+ * (bf16 corpora are widened). The rows must lie in local shards. Test/diagnostic use. */
+int rr_read_rows(const rr_handle* h, int64_t row_begin, int64_t n_rows, float* host_out);
+
+/* ---- search ------------------------------------------------------------------------------------ */
+
+/* Synchronous batched search: host queries (b x d fp32, row-major) -> host results
+ * out_scores[b*k] (fp32) and out_idx[b*k] (int64 global row index), each row sorted.
+ * 1 <= k; k > n is allowed (tail padded with -inf / -1). Replaces batch_retrieve's device part
+ * (retriever.py:734-773). */
+int rr_search(rr_handle* h, const float* host_q, int32_t b, int32_t d, int32_t k,
+              float* out_scores, int64_t* out_idx);
+
+/* Split form of rr_search for serving pipelines and benchmarks:
+ *   rr_set_queries   : H2D copy of b x d queries into every local shard's query buffer
+ *   rr_search_staged : enqueue the device pipeline on the staged queries (async; results stay in HBM)
+ *   rr_synchronize   : wait for all local shard streams
+ *   rr_fetch_results : D2H of the last search's results (synchronises first)           */
+int rr_set_queries(rr_handle* h, const float* host_q, int32_t b, int32_t d);
+int rr_search_staged(rr_handle* h, int32_t k);
+int rr_synchronize(rr_handle* h);
+int rr_fetch_results(rr_handle* h, float* out_scores, int64_t* out_idx);
+
+/* Queries already on local device 0 (e.g. a torch tensor from the embedding model): device-to-device
+ * copy into every local shard's query buffer (skips the reference's .cpu().numpy() round trip,
+ * batch_processor.py:92). dev_q is a device pointer on the handle's first local device. */
+int rr_set_queries_device(rr_handle* h, const float* dev_q, int32_t b, int32_t d);
+
+/* ---- timing (benchmarks) ----------------------------------------------------------------------- */
+
+/* Enable/disable HIP-event timing of the fused similarity+top-k kernel on local shard 0's stream. */
+int rr_set_timing(rr_handle* h, int enable);
+
+/* Sum (ms) and count of timed fused-kernel launches since the last reset; resets when reset != 0. */
+int rr_kernel_time(rr_handle* h, double* total_ms, int64_t* launches, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RAG_RETRIEVAL_H */

@@ -1,0 +1,642 @@
+// rr_api.cpp — C-ABI host side of the MI355X retrieval hot path (see include/rag_retrieval.h).
+//
+// Owns the device state the reference keeps in CupyRetriever (retriever.py:566-592): the corpus in
+// HBM (here row-sharded over devices), plus what the reference recomputes on every call and we keep
+// resident: per-row norms (retriever.py:603) and the query/candidate work buffers. One HIP stream per
+// local shard; shards exchange their top-k candidates with one RCCL all-gather (new: the reference
+// has no collective).
+#include "rag_retrieval.h"
+#include "rr_internal.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                            \
+  do {                                                                                           \
+    hipError_t _e = (expr);                                                                      \
+    if (_e != hipSuccess)                                                                        \
+      return fail(_e == hipErrorOutOfMemory ? RR_E_OOM : RR_E_HIP, "%s failed: %s (%s:%d)", #expr, \
+                  hipGetErrorString(_e), __FILE__, __LINE__);                                    \
+  } while (0)
+
+#define NCCL_TRY(expr)                                                                       \
+  do {                                                                                       \
+    ncclResult_t _r = (expr);                                                                \
+    if (_r != ncclSuccess)                                                                   \
+      return fail(RR_E_RCCL, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(_r), __FILE__, \
+                  __LINE__);                                                                 \
+  } while (0)
+
+struct Shard {
+  int dev = 0;
+  int cus = 256;
+  hipStream_t stream = nullptr;
+  int64_t row_begin = 0, row_end = 0;   // global rows held
+  void* corpus = nullptr;                // [rows][d] fp32 or bf16
+  float* norms = nullptr;                // [round_up(rows, 32)] (pad = 1)
+  float* queries = nullptr;              // [q_cap][d] fp32
+  int q_cap = 0;
+  uint64_t* cand = nullptr;              // [grid][32][32] fused per-workgroup candidates
+  int cand_grid = 0;
+  uint64_t* shard_keys = nullptr;        // [32][k_cap] this shard's top-k (all-gather send buffer)
+  uint64_t* gathered = nullptr;          // [world][32][k_cap] (all-gather receive buffer)
+  float* out_scores = nullptr;           // [q_cap][k_cap]
+  int64_t* out_idx = nullptr;            // [q_cap][k_cap]
+  int k_cap = 0;
+  // k > RR_FUSED_KMAX path
+  uint64_t* full_keys = nullptr;         // [32][max(rows, world*k)]
+  uint64_t* sorted = nullptr;
+  size_t full_cap = 0;                   // elements
+  void* sort_temp = nullptr;
+  size_t sort_temp_bytes = 0;
+  ncclComm_t comm = nullptr;
+  std::vector<hipEvent_t> ev;            // timing event pairs (local shard 0 only)
+  size_t ev_used = 0;
+
+  int64_t rows() const { return row_end - row_begin; }
+};
+
+}  // namespace
+
+struct rr_handle {
+  int dtype = RR_DTYPE_F32;
+  int metric = RR_METRIC_COSINE;
+  int32_t d = 0;
+  int64_t n_total = 0;
+  int world = 1;        // global shard count
+  int shard_base = 0;   // global index of local shard 0
+  bool dist = false;
+  bool loaded = false;
+  std::vector<Shard> shards;
+  int32_t cur_b = 0;    // last staged batch
+  int32_t last_k = 0;   // k of the last search
+  bool timing = false;
+  double t_ms = 0.0;
+  int64_t t_count = 0;
+};
+
+namespace {
+
+size_t elem_bytes(int dtype) { return dtype == RR_DTYPE_BF16 ? 2 : 4; }
+
+void shard_range(int64_t n, int world, int g, int64_t* b, int64_t* e) {
+  const int64_t per = (n + world - 1) / world;
+  *b = std::min<int64_t>(n, (int64_t)g * per);
+  *e = std::min<int64_t>(n, *b + per);
+}
+
+template <class T>
+int dmalloc(T** p, size_t bytes) {
+  if (*p) {
+    hipFree(*p);
+    *p = nullptr;
+  }
+  if (bytes == 0) bytes = 16;
+  HIP_TRY(hipMalloc((void**)p, bytes));
+  return RR_OK;
+}
+
+int free_shard(Shard& s) {
+  hipSetDevice(s.dev);
+  void* ptrs[] = {s.corpus, s.norms, s.queries, s.cand, s.shard_keys, s.gathered, s.out_scores, s.out_idx,
+                  s.full_keys, s.sorted, s.sort_temp};
+  for (void* p : ptrs)
+    if (p) hipFree(p);
+  for (hipEvent_t e : s.ev) hipEventDestroy(e);
+  s.ev.clear();
+  if (s.comm) ncclCommDestroy(s.comm);
+  if (s.stream) hipStreamDestroy(s.stream);
+  s = Shard();
+  return RR_OK;
+}
+
+// Allocate the shard's corpus storage for the current range (and norms when cosine).
+int alloc_corpus(rr_handle* h, Shard& s) {
+  HIP_TRY(hipSetDevice(s.dev));
+  const int64_t rows = s.rows();
+  if (int rc = dmalloc(&s.corpus, (size_t)std::max<int64_t>(rows, 1) * h->d * elem_bytes(h->dtype))) return rc;
+  const int64_t npad = (rows + rr::kTileDocs - 1) / rr::kTileDocs * rr::kTileDocs + rr::kTileDocs;
+  if (int rc = dmalloc(&s.norms, (size_t)npad * sizeof(float))) return rc;
+  // pad norms with 1.0 so padded tiles divide by something finite
+  std::vector<float> ones((size_t)npad, 1.0f);
+  HIP_TRY(hipMemcpy(s.norms, ones.data(), ones.size() * sizeof(float), hipMemcpyHostToDevice));
+  return RR_OK;
+}
+
+int finish_corpus(rr_handle* h, Shard& s) {
+  HIP_TRY(hipSetDevice(s.dev));
+  if (h->metric == RR_METRIC_COSINE && s.rows() > 0)
+    HIP_TRY(rr::launch_row_norms(h->dtype, s.corpus, s.rows(), h->d, s.norms, s.stream));
+  HIP_TRY(hipStreamSynchronize(s.stream));
+  return RR_OK;
+}
+
+// Copy host fp32 rows [src rows] into shard storage at local row offset `dst_row`.
+int upload_rows(rr_handle* h, Shard& s, const float* src, int64_t dst_row, int64_t nrows) {
+  HIP_TRY(hipSetDevice(s.dev));
+  const int d = h->d;
+  if (h->dtype == RR_DTYPE_F32) {
+    HIP_TRY(hipMemcpy((float*)s.corpus + dst_row * d, src, (size_t)nrows * d * 4, hipMemcpyHostToDevice));
+    return RR_OK;
+  }
+  // bf16: stage fp32 chunks on device, convert with RNE
+  const int64_t chunk_rows = std::max<int64_t>(1, (64ll << 20) / (d * 4));
+  float* tmp = nullptr;
+  HIP_TRY(hipMalloc((void**)&tmp, (size_t)std::min(chunk_rows, nrows) * d * 4));
+  for (int64_t r0 = 0; r0 < nrows; r0 += chunk_rows) {
+    const int64_t nr = std::min(chunk_rows, nrows - r0);
+    hipError_t e = hipMemcpy(tmp, src + r0 * d, (size_t)nr * d * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = rr::launch_f32_to_bf16(tmp, (uint16_t*)s.corpus + (dst_row + r0) * d, nr * d, s.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+    if (e != hipSuccess) {
+      hipFree(tmp);
+      return fail(RR_E_HIP, "bf16 upload failed: %s", hipGetErrorString(e));
+    }
+  }
+  hipFree(tmp);
+  return RR_OK;
+}
+
+int check_shape(const rr_handle* h, int64_t n, int32_t d) {
+  if (n <= 0) return fail(RR_E_INVALID, "corpus must have at least one row (n=%lld)", (long long)n);
+  if (n >= 0xFFFFFFFFll) return fail(RR_E_UNSUPPORTED, "n=%lld exceeds the 32-bit index range", (long long)n);
+  const int mult = h->dtype == RR_DTYPE_F32 ? 64 : 128;
+  if (d <= 0 || d % mult != 0)
+    return fail(RR_E_UNSUPPORTED, "d=%d must be a positive multiple of %d for this dtype", d, mult);
+  if (rr::fused_lds_bytes(d, 32, h->dtype) > 160 * 1024)
+    return fail(RR_E_UNSUPPORTED, "d=%d too large for the LDS-resident query image", d);
+  return RR_OK;
+}
+
+int prepare_ranges(rr_handle* h, int64_t n, int32_t d) {
+  if (int rc = check_shape(h, n, d)) return rc;
+  h->n_total = n;
+  h->d = d;
+  for (size_t i = 0; i < h->shards.size(); ++i) {
+    Shard& s = h->shards[i];
+    shard_range(n, h->world, h->shard_base + (int)i, &s.row_begin, &s.row_end);
+    if (int rc = alloc_corpus(h, s)) return rc;
+  }
+  return RR_OK;
+}
+
+// Work buffers sized for (b queries, k results).
+int ensure_buffers(rr_handle* h, int b, int k) {
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    if (b > s.q_cap || k > s.k_cap) {
+      const int qc = std::max(b, s.q_cap), kc = std::max(k, s.k_cap);
+      if (b > s.q_cap) {
+        if (int rc = dmalloc(&s.queries, (size_t)((qc + 31) / 32 * 32) * h->d * 4)) return rc;
+        HIP_TRY(hipMemset(s.queries, 0, (size_t)((qc + 31) / 32 * 32) * h->d * 4));
+      }
+      if (int rc = dmalloc(&s.out_scores, (size_t)qc * kc * 4)) return rc;
+      if (int rc = dmalloc(&s.out_idx, (size_t)qc * kc * 8)) return rc;
+      const int kk = std::max(kc, RR_FUSED_KMAX);
+      if (int rc = dmalloc(&s.shard_keys, (size_t)rr::kQSlots * kk * 8)) return rc;
+      if (int rc = dmalloc(&s.gathered, (size_t)h->world * rr::kQSlots * kk * 8)) return rc;
+      s.q_cap = qc;
+      s.k_cap = kc;
+    }
+    if (!s.cand) {
+      s.cand_grid = s.cus;
+      if (int rc = dmalloc(&s.cand, (size_t)s.cand_grid * rr::kQSlots * RR_FUSED_KMAX * 8)) return rc;
+    }
+    if (k > RR_FUSED_KMAX) {
+      const size_t need = (size_t)rr::kQSlots * std::max<int64_t>(s.rows(), (int64_t)h->world * k);
+      if (need > s.full_cap) {
+        if (int rc = dmalloc(&s.full_keys, need * 8)) return rc;
+        if (int rc = dmalloc(&s.sorted, need * 8)) return rc;
+        s.full_cap = need;
+        size_t tb = 0;
+        HIP_TRY(rr::segmented_sort_desc(nullptr, &tb, s.full_keys, s.sorted, rr::kQSlots,
+                                        (int64_t)(need / rr::kQSlots), s.stream));
+        if (tb > s.sort_temp_bytes) {
+          if (int rc = dmalloc(&s.sort_temp, tb)) return rc;
+          s.sort_temp_bytes = tb;
+        }
+      }
+    }
+  }
+  return RR_OK;
+}
+
+int fused_grid(const Shard& s) {
+  const int64_t ntiles = (s.rows() + rr::kTileDocs - 1) / rr::kTileDocs;
+  const int64_t want = (ntiles + rr::kWaves - 1) / rr::kWaves;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(s.cand_grid, want));
+}
+
+int next_event_pair(Shard& s, hipEvent_t* a, hipEvent_t* b) {
+  while (s.ev.size() < 2 * (s.ev_used + 1)) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreate(&e));
+    s.ev.push_back(e);
+  }
+  *a = s.ev[2 * s.ev_used];
+  *b = s.ev[2 * s.ev_used + 1];
+  ++s.ev_used;
+  return RR_OK;
+}
+
+int collect_timing(rr_handle* h) {
+  if (h->shards.empty()) return RR_OK;
+  Shard& s = h->shards[0];
+  for (size_t i = 0; i < s.ev_used; ++i) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, s.ev[2 * i], s.ev[2 * i + 1]));
+    h->t_ms += ms;
+    h->t_count += 1;
+  }
+  s.ev_used = 0;
+  return RR_OK;
+}
+
+// Enqueue the device pipeline for query block [q0, q0 + bb) on every local shard.
+int enqueue_block(rr_handle* h, int q0, int bb, int k) {
+  const int d = h->d;
+  const int kt = rr::fused_kt(k);
+  const bool multi = h->world > 1;
+  for (size_t si = 0; si < h->shards.size(); ++si) {
+    Shard& s = h->shards[si];
+    HIP_TRY(hipSetDevice(s.dev));
+    const float* qb = s.queries + (size_t)q0 * d;
+    float* osc = s.out_scores + (size_t)q0 * k;
+    int64_t* oix = s.out_idx + (size_t)q0 * k;
+    const uint32_t base = (uint32_t)s.row_begin;
+    if (kt) {
+      const int grid = fused_grid(s);
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      const bool timed = h->timing && si == 0;
+      if (timed) {
+        if (int rc = next_event_pair(s, &e0, &e1)) return rc;
+        HIP_TRY(hipEventRecord(e0, s.stream));
+      }
+      if (s.rows() > 0) {
+        HIP_TRY(rr::launch_fused(h->dtype, h->metric, kt, grid, s.corpus, s.norms, qb, s.rows(), d, bb, base,
+                                 s.cand, s.stream));
+      } else {
+        HIP_TRY(hipMemsetAsync(s.cand, 0, (size_t)rr::kQSlots * kt * 8, s.stream));
+      }
+      if (timed) HIP_TRY(hipEventRecord(e1, s.stream));
+      if (!multi) {
+        HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, nullptr, osc, oix, s.stream));
+      } else {
+        HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, s.shard_keys, nullptr, nullptr, s.stream));
+      }
+    } else {
+      // k > RR_FUSED_KMAX: all keys of this shard, segmented radix sort, keep the first k.
+      const int64_t rows = s.rows();
+      HIP_TRY(hipMemsetAsync(s.shard_keys, 0, (size_t)rr::kQSlots * k * 8, s.stream));
+      if (rows > 0) {
+        const int grid = fused_grid(s);
+        HIP_TRY(rr::launch_full_keys(h->dtype, h->metric, grid, s.corpus, s.norms, qb, rows, d, bb, base,
+                                     s.full_keys, s.stream));
+        size_t tb = s.sort_temp_bytes;
+        HIP_TRY(rr::segmented_sort_desc(s.sort_temp, &tb, s.full_keys, s.sorted, bb, rows, s.stream));
+        HIP_TRY(rr::launch_take_prefix(s.sorted, bb, rows, k, s.shard_keys, s.stream));
+      }
+      if (!multi) HIP_TRY(rr::launch_decode(s.shard_keys, bb, k, osc, oix, s.stream));
+    }
+  }
+  if (!multi) return RR_OK;
+
+  // ---- exchange: one all-gather of every shard's [32][kk] candidate keys ---------------------------
+  const int kk = kt ? kt : k;
+  NCCL_TRY(ncclGroupStart());
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    NCCL_TRY(ncclAllGather(s.shard_keys, s.gathered, (size_t)rr::kQSlots * kk, ncclUint64, s.comm, s.stream));
+  }
+  NCCL_TRY(ncclGroupEnd());
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    float* osc = s.out_scores + (size_t)q0 * k;
+    int64_t* oix = s.out_idx + (size_t)q0 * k;
+    if (kt) {
+      HIP_TRY(rr::launch_merge(kt, s.gathered, h->world, kt, bb, k, nullptr, osc, oix, s.stream));
+    } else {
+      const int64_t seg = (int64_t)h->world * k;
+      HIP_TRY(rr::launch_regroup(s.gathered, h->world, k, bb, s.full_keys, s.stream));
+      size_t tb = s.sort_temp_bytes;
+      HIP_TRY(rr::segmented_sort_desc(s.sort_temp, &tb, s.full_keys, s.sorted, bb, seg, s.stream));
+      HIP_TRY(rr::launch_take_prefix(s.sorted, bb, seg, k, s.shard_keys, s.stream));
+      HIP_TRY(rr::launch_decode(s.shard_keys, bb, k, osc, oix, s.stream));
+    }
+  }
+  return RR_OK;
+}
+
+}  // namespace
+
+// =================================================================================================
+// C-ABI
+// =================================================================================================
+extern "C" {
+
+const char* rr_last_error(void) { return g_err.c_str(); }
+
+int rr_abi_version(void) { return RR_ABI_VERSION; }
+
+int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** out) {
+  g_err.clear();
+  if (!out) return fail(RR_E_INVALID, "out is null");
+  *out = nullptr;
+  if (dtype != RR_DTYPE_F32 && dtype != RR_DTYPE_BF16) return fail(RR_E_INVALID, "bad dtype %d", dtype);
+  if (metric != RR_METRIC_DOT && metric != RR_METRIC_COSINE) return fail(RR_E_INVALID, "bad metric %d", metric);
+  int def = 0;
+  if (!devices) {
+    devices = &def;
+    n_dev = 1;
+  }
+  if (n_dev < 1) return fail(RR_E_INVALID, "n_dev=%d", n_dev);
+  int ndev_avail = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev_avail));
+  rr_handle* h = new rr_handle();
+  h->dtype = dtype;
+  h->metric = metric;
+  h->world = n_dev;
+  h->shards.resize(n_dev);
+  for (int i = 0; i < n_dev; ++i) {
+    Shard& s = h->shards[i];
+    if (devices[i] < 0 || devices[i] >= ndev_avail) {
+      rr_destroy(h);
+      return fail(RR_E_INVALID, "device %d not available (%d devices)", devices[i], ndev_avail);
+    }
+    s.dev = devices[i];
+    hipError_t e = hipSetDevice(s.dev);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&s.cus, hipDeviceAttributeMultiprocessorCount, s.dev);
+    if (e != hipSuccess) {
+      rr_destroy(h);
+      return fail(RR_E_HIP, "device %d setup failed: %s", devices[i], hipGetErrorString(e));
+    }
+  }
+  if (n_dev > 1) {
+    std::vector<ncclComm_t> comms(n_dev);
+    std::vector<int> devs(devices, devices + n_dev);
+    ncclResult_t r = ncclCommInitAll(comms.data(), n_dev, devs.data());
+    if (r != ncclSuccess) {
+      rr_destroy(h);
+      return fail(RR_E_RCCL, "ncclCommInitAll failed: %s", ncclGetErrorString(r));
+    }
+    for (int i = 0; i < n_dev; ++i) h->shards[i].comm = comms[i];
+  }
+  *out = h;
+  return RR_OK;
+}
+
+void rr_destroy(rr_handle* h) {
+  if (!h) return;
+  for (Shard& s : h->shards) free_shard(s);
+  delete h;
+}
+
+int rr_get_unique_id(char* out) {
+  if (!out) return fail(RR_E_INVALID, "out is null");
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  memcpy(out, id.internal, RR_UNIQUE_ID_BYTES);
+  return RR_OK;
+}
+
+int rr_init_dist(rr_handle* h, int world, int rank, const char* unique_id) {
+  if (!h || !unique_id) return fail(RR_E_INVALID, "null argument");
+  if (h->shards.size() != 1) return fail(RR_E_UNSUPPORTED, "multi-process mode needs exactly one local device");
+  if (h->loaded) return fail(RR_E_STATE, "rr_init_dist must precede loading the corpus");
+  if (world < 1 || rank < 0 || rank >= world) return fail(RR_E_INVALID, "bad world/rank %d/%d", world, rank);
+  h->world = world;
+  h->shard_base = rank;
+  h->dist = true;
+  if (world > 1) {
+    Shard& s = h->shards[0];
+    HIP_TRY(hipSetDevice(s.dev));
+    ncclUniqueId id;
+    memcpy(id.internal, unique_id, RR_UNIQUE_ID_BYTES);
+    NCCL_TRY(ncclCommInitRank(&s.comm, world, id, rank));
+  }
+  return RR_OK;
+}
+
+int rr_load(rr_handle* h, const float* host_corpus, int64_t n, int32_t d) {
+  if (!h || !host_corpus) return fail(RR_E_INVALID, "null argument");
+  if (int rc = prepare_ranges(h, n, d)) return rc;
+  for (Shard& s : h->shards) {
+    if (s.rows() > 0)
+      if (int rc = upload_rows(h, s, host_corpus + s.row_begin * (int64_t)d, 0, s.rows())) return rc;
+    if (int rc = finish_corpus(h, s)) return rc;
+  }
+  h->loaded = true;
+  return RR_OK;
+}
+
+int rr_load_rows(rr_handle* h, const float* host_rows, int64_t row_begin, int64_t n_rows, int64_t n_total,
+                 int32_t d) {
+  if (!h || !host_rows) return fail(RR_E_INVALID, "null argument");
+  if (int rc = prepare_ranges(h, n_total, d)) return rc;
+  for (Shard& s : h->shards) {
+    if (s.row_begin < row_begin || s.row_end > row_begin + n_rows)
+      return fail(RR_E_INVALID, "rows [%lld,%lld) do not cover shard [%lld,%lld)", (long long)row_begin,
+                  (long long)(row_begin + n_rows), (long long)s.row_begin, (long long)s.row_end);
+    if (s.rows() > 0)
+      if (int rc = upload_rows(h, s, host_rows + (s.row_begin - row_begin) * (int64_t)d, 0, s.rows())) return rc;
+    if (int rc = finish_corpus(h, s)) return rc;
+  }
+  h->loaded = true;
+  return RR_OK;
+}
+
+int rr_fill_synthetic(rr_handle* h, int kind, uint64_t seed, int64_t n_total, int32_t d) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  if (kind != RR_SYNTH_EXACT_INT && kind != RR_SYNTH_UNIT_NORM) return fail(RR_E_INVALID, "bad kind %d", kind);
+  if (int rc = prepare_ranges(h, n_total, d)) return rc;
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    const int64_t rows = s.rows();
+    if (rows > 0) {
+      if (h->dtype == RR_DTYPE_F32) {
+        HIP_TRY(rr::launch_synth(kind, seed, s.row_begin, rows, d, (float*)s.corpus, s.stream));
+      } else {
+        const int64_t chunk_rows = std::max<int64_t>(1, (256ll << 20) / (d * 4));
+        float* tmp = nullptr;
+        HIP_TRY(hipMalloc((void**)&tmp, (size_t)std::min(chunk_rows, rows) * d * 4));
+        for (int64_t r0 = 0; r0 < rows; r0 += chunk_rows) {
+          const int64_t nr = std::min(chunk_rows, rows - r0);
+          hipError_t e = rr::launch_synth(kind, seed, s.row_begin + r0, nr, d, tmp, s.stream);
+          if (e == hipSuccess) e = rr::launch_f32_to_bf16(tmp, (uint16_t*)s.corpus + r0 * d, nr * d, s.stream);
+          if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+          if (e != hipSuccess) {
+            hipFree(tmp);
+            return fail(RR_E_HIP, "synthetic bf16 fill failed: %s", hipGetErrorString(e));
+          }
+        }
+        hipFree(tmp);
+      }
+    }
+    if (int rc = finish_corpus(h, s)) return rc;
+  }
+  h->loaded = true;
+  return RR_OK;
+}
+
+int rr_info(const rr_handle* h, int64_t* n_total, int32_t* d, int32_t* n_local_shards, int32_t* world_shards) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  if (n_total) *n_total = h->n_total;
+  if (d) *d = h->d;
+  if (n_local_shards) *n_local_shards = (int32_t)h->shards.size();
+  if (world_shards) *world_shards = h->world;
+  return RR_OK;
+}
+
+int rr_shard_range(const rr_handle* h, int i, int64_t* begin, int64_t* end) {
+  if (!h || i < 0 || i >= (int)h->shards.size()) return fail(RR_E_INVALID, "bad shard %d", i);
+  if (begin) *begin = h->shards[i].row_begin;
+  if (end) *end = h->shards[i].row_end;
+  return RR_OK;
+}
+
+int rr_read_rows(const rr_handle* h, int64_t row_begin, int64_t n_rows, float* host_out) {
+  if (!h || !host_out) return fail(RR_E_INVALID, "null argument");
+  if (!h->loaded) return fail(RR_E_STATE, "no corpus loaded");
+  const int d = h->d;
+  int64_t done = 0;
+  while (done < n_rows) {
+    const int64_t row = row_begin + done;
+    const Shard* sp = nullptr;
+    for (const Shard& s : h->shards)
+      if (row >= s.row_begin && row < s.row_end) sp = &s;
+    if (!sp) return fail(RR_E_INVALID, "row %lld is not held locally", (long long)row);
+    const int64_t nr = std::min(n_rows - done, sp->row_end - row);
+    const int64_t lr = row - sp->row_begin;
+    HIP_TRY(hipSetDevice(sp->dev));
+    if (h->dtype == RR_DTYPE_F32) {
+      HIP_TRY(hipMemcpy(host_out + done * d, (const float*)sp->corpus + lr * d, (size_t)nr * d * 4,
+                        hipMemcpyDeviceToHost));
+    } else {
+      float* tmp = nullptr;
+      HIP_TRY(hipMalloc((void**)&tmp, (size_t)nr * d * 4));
+      hipError_t e = rr::launch_bf16_to_f32((const uint16_t*)sp->corpus + lr * d, tmp, nr * d, sp->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(sp->stream);
+      if (e == hipSuccess) e = hipMemcpy(host_out + done * d, tmp, (size_t)nr * d * 4, hipMemcpyDeviceToHost);
+      hipFree(tmp);
+      if (e != hipSuccess) return fail(RR_E_HIP, "read_rows failed: %s", hipGetErrorString(e));
+    }
+    done += nr;
+  }
+  return RR_OK;
+}
+
+int rr_set_queries(rr_handle* h, const float* host_q, int32_t b, int32_t d) {
+  if (!h || (!host_q && b > 0)) return fail(RR_E_INVALID, "null argument");
+  if (!h->loaded) return fail(RR_E_STATE, "no corpus loaded");
+  if (d != h->d) return fail(RR_E_INVALID, "query dim %d != corpus dim %d", d, h->d);
+  if (b < 1) return fail(RR_E_INVALID, "b=%d", b);
+  if (int rc = ensure_buffers(h, b, 1)) return rc;
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    HIP_TRY(hipMemcpyAsync(s.queries, host_q, (size_t)b * d * 4, hipMemcpyHostToDevice, s.stream));
+  }
+  h->cur_b = b;
+  return RR_OK;
+}
+
+int rr_set_queries_device(rr_handle* h, const float* dev_q, int32_t b, int32_t d) {
+  if (!h || !dev_q) return fail(RR_E_INVALID, "null argument");
+  if (!h->loaded) return fail(RR_E_STATE, "no corpus loaded");
+  if (d != h->d) return fail(RR_E_INVALID, "query dim %d != corpus dim %d", d, h->d);
+  if (b < 1) return fail(RR_E_INVALID, "b=%d", b);
+  if (int rc = ensure_buffers(h, b, 1)) return rc;
+  const int src_dev = h->shards[0].dev;
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    if (s.dev == src_dev)
+      HIP_TRY(hipMemcpyAsync(s.queries, dev_q, (size_t)b * d * 4, hipMemcpyDeviceToDevice, s.stream));
+    else
+      HIP_TRY(hipMemcpyPeerAsync(s.queries, s.dev, dev_q, src_dev, (size_t)b * d * 4, s.stream));
+  }
+  h->cur_b = b;
+  return RR_OK;
+}
+
+int rr_search_staged(rr_handle* h, int32_t k) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  if (!h->loaded || h->cur_b < 1) return fail(RR_E_STATE, "no queries staged");
+  if (k < 1) return fail(RR_E_INVALID, "k=%d must be >= 1", k);
+  const int b = h->cur_b;
+  if (int rc = ensure_buffers(h, b, k)) return rc;
+  for (int q0 = 0; q0 < b; q0 += rr::kQSlots) {
+    const int bb = std::min(rr::kQSlots, b - q0);
+    if (int rc = enqueue_block(h, q0, bb, k)) return rc;
+  }
+  h->last_k = k;
+  return RR_OK;
+}
+
+int rr_synchronize(rr_handle* h) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    HIP_TRY(hipStreamSynchronize(s.stream));
+  }
+  return collect_timing(h);
+}
+
+int rr_fetch_results(rr_handle* h, float* out_scores, int64_t* out_idx) {
+  if (!h || !out_scores || !out_idx) return fail(RR_E_INVALID, "null argument");
+  if (h->last_k < 1) return fail(RR_E_STATE, "no search has run");
+  if (int rc = rr_synchronize(h)) return rc;
+  Shard& s = h->shards[0];
+  HIP_TRY(hipSetDevice(s.dev));
+  const size_t cnt = (size_t)h->cur_b * h->last_k;
+  HIP_TRY(hipMemcpy(out_scores, s.out_scores, cnt * 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(out_idx, s.out_idx, cnt * 8, hipMemcpyDeviceToHost));
+  return RR_OK;
+}
+
+int rr_search(rr_handle* h, const float* host_q, int32_t b, int32_t d, int32_t k, float* out_scores,
+              int64_t* out_idx) {
+  if (int rc = rr_set_queries(h, host_q, b, d)) return rc;
+  if (int rc = rr_search_staged(h, k)) return rc;
+  return rr_fetch_results(h, out_scores, out_idx);
+}
+
+int rr_set_timing(rr_handle* h, int enable) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  h->timing = enable != 0;
+  return RR_OK;
+}
+
+int rr_kernel_time(rr_handle* h, double* total_ms, int64_t* launches, int reset) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  if (int rc = rr_synchronize(h)) return rc;
+  if (total_ms) *total_ms = h->t_ms;
+  if (launches) *launches = h->t_count;
+  if (reset) {
+    h->t_ms = 0.0;
+    h->t_count = 0;
+  }
+  return RR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,61 @@
+// rr_internal.h — launchers shared between the C-ABI host code (rr_api.cpp) and the HIP kernels
+// (rr_kernels.hip). Not part of the public ABI (see include/rag_retrieval.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rr {
+
+// Fused kernel geometry: 8 waves per workgroup (2 per SIMD), each wave owns a 32-document tile at a
+// time; 32 query slots per pass (the N dimension of the 32x32 MFMA).
+constexpr int kWaves      = 8;
+constexpr int kThreads    = kWaves * 64;
+constexpr int kQSlots     = 32;
+constexpr int kTileDocs   = 32;
+constexpr int kGroupChunks = 8;   // 16-byte loads per lane kept in flight per pipeline stage
+
+// Smallest fused-kernel list width KT >= k (4, 8, 16, 32); 0 if k > RR_FUSED_KMAX.
+int fused_kt(int k);
+
+// Dynamic LDS bytes the fused kernel needs for (d, KT, dtype).
+size_t fused_lds_bytes(int d, int kt, int dtype);
+
+// Fused similarity + per-workgroup top-KT. queries: [b][d] fp32 (b <= 32) on device.
+// corpus: [n][d] fp32 (dtype 0) or bf16 (dtype 1). norms: [n] (cosine) or nullptr.
+// cand: [grid][32][KT] uint64 keys (see key encoding in rr_kernels.hip).
+hipError_t launch_fused(int dtype, int metric, int kt, int grid, const void* corpus, const float* norms,
+                        const float* queries, int64_t n, int d, int b, uint32_t idx_base,
+                        uint64_t* cand, hipStream_t s);
+
+// Merge nlists candidate lists laid out [nlists][32][in_kt] into the top-kt per query.
+// out_keys [32][kt] (may be null); out_scores/out_idx [b][k_out] (may be null).
+hipError_t launch_merge(int kt, const uint64_t* in, int nlists, int in_kt, int b, int k_out,
+                        uint64_t* out_keys, float* out_scores, int64_t* out_idx, hipStream_t s);
+
+// Full-score path for k > RR_FUSED_KMAX: keys [b][n] for every (query, doc) pair.
+hipError_t launch_full_keys(int dtype, int metric, int grid, const void* corpus, const float* norms,
+                            const float* queries, int64_t n, int d, int b, uint32_t idx_base,
+                            uint64_t* keys, hipStream_t s);
+
+// Segmented descending sort of b segments of `seg` keys each (in -> out); temp from hipcub.
+hipError_t segmented_sort_desc(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out,
+                               int b, int64_t seg, hipStream_t s);
+
+// Gather first k of each sorted segment: out_keys [b][k] (row stride k) from sorted [b][seg].
+hipError_t launch_take_prefix(const uint64_t* sorted, int b, int64_t seg, int k, uint64_t* out_keys,
+                              hipStream_t s);
+
+// gathered [world][32][k] -> per-query segments [b][world*k].
+hipError_t launch_regroup(const uint64_t* gathered, int world, int k, int b, uint64_t* out, hipStream_t s);
+
+// Decode keys [b][k] into scores / indices (-inf / -1 for empty slots).
+hipError_t launch_decode(const uint64_t* keys, int b, int k, float* scores, int64_t* idx, hipStream_t s);
+
+// Corpus preparation.
+hipError_t launch_f32_to_bf16(const float* in, uint16_t* out, int64_t count, hipStream_t s);
+hipError_t launch_row_norms(int dtype, const void* corpus, int64_t n, int d, float* norms, hipStream_t s);
+hipError_t launch_synth(int kind, uint64_t seed, int64_t row_begin, int64_t n_rows, int d, float* out,
+                        hipStream_t s);
+hipError_t launch_bf16_to_f32(const uint16_t* in, float* out, int64_t count, hipStream_t s);
+
+}  // namespace rr

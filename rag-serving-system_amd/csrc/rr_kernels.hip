@@ -1,0 +1,596 @@
+// rr_kernels.hip — hand-written CDNA4 (gfx950, wave64) kernels for the batched dense-retrieval hot path.
+//
+// Reference behaviour being replaced (ngray0/RAG-Serving-System, rag_service/core/retriever.py):
+//   CupyRetriever.distance_cosine  :594-611  (B,N) dot GEMM + norm passes + divide + clip, all materialised
+//   CupyRetriever.batch_retrieve   :742-769  per-row argpartition + argsort loop (B launches)
+//   SimpleRetriever.retrieve       :112-120  fp32 matvec + argpartition + descending argsort
+// Here the whole thing is ONE streaming pass over the corpus: the (B x N) score matrix never reaches
+// HBM. Each wave owns a 32-document tile, computes the 32(doc) x 32(query) score block with MFMA
+// directly from 16-byte-per-lane corpus loads (the corpus is read exactly once, so it is not staged
+// through LDS — only the queries, which every wave re-reads, live in LDS), applies the metric
+// epilogue in registers and folds the 16 scores per lane into a per-lane sorted top-KT list.
+// Lists are merged per workgroup in LDS; a second tiny kernel merges the per-workgroup lists.
+//
+// Score/index keys. A candidate is one uint64: high 32 bits = order-preserving image of the fp32
+// score, low 32 bits = 0xFFFFFFFF - global_index. Unsigned key order == (score desc, index asc), the
+// deterministic tie rule of this implementation (the reference's tie order is implementation
+// defined: numpy introselect / CUB). Key 0 = empty slot.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+#include "rr_internal.h"
+
+namespace rr {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// ------------------------------------------------------------------------------------------------
+// keys
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ord_of(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float float_of_ord(uint32_t o) {
+  const uint32_t u = (o & 0x80000000u) ? (o & 0x7fffffffu) : ~o;
+  return __uint_as_float(u);
+}
+__device__ __forceinline__ uint64_t make_key(float s, uint32_t gidx) {
+  return ((uint64_t)ord_of(s) << 32) | (uint64_t)(0xFFFFFFFFu - gidx);
+}
+__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
+// Per-lane sorted (descending) list of the KT best keys, fully in registers (static indexing only).
+template <int KT>
+struct TopK {
+  uint64_t v[KT];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int i = 0; i < KT; ++i) v[i] = 0;
+  }
+  __device__ __forceinline__ uint64_t last() const { return v[KT - 1]; }
+  // Branch-free insertion of x (caller checked x > last()).
+  __device__ __forceinline__ void insert(uint64_t x) {
+#pragma unroll
+    for (int i = KT - 1; i > 0; --i) {
+      const uint64_t up = v[i - 1];
+      v[i] = (x > up) ? up : umax64(x, v[i]);
+    }
+    v[0] = umax64(x, v[0]);
+  }
+  __device__ __forceinline__ void pop() {
+#pragma unroll
+    for (int i = 0; i < KT - 1; ++i) v[i] = v[i + 1];
+    v[KT - 1] = 0;
+  }
+};
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, off, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), off, 64);
+    x = umax64(x, ((uint64_t)hi << 32) | lo);
+  }
+  return x;
+}
+
+// ------------------------------------------------------------------------------------------------
+// fused similarity + top-k
+// ------------------------------------------------------------------------------------------------
+// DT: 0 = fp32 corpus  (chunk = 8 k-values: lane half h holds k = 8c + 4h + {0..3}; 4 x
+//                       v_mfma_f32_32x32x2_f32, A = doc value, B = query value)
+//     1 = bf16 corpus  (chunk = 16 k-values: lane half h holds k = 16c + 8h + {0..7}; 2 x
+//                       v_mfma_f32_32x32x16_bf16 against the query's bf16 hi and lo parts)
+// The k permutation inside a chunk is applied identically to both operands, so the dot is exact up
+// to fp32 accumulation order (fp32 path: a plain fmaf chain per (doc, query)).
+// LDS image: query operand for (chunk c, half h, query slot q) at 16-byte slot (2c + h) * 32 + q —
+// one wave's ds_read_b128 covers 1 KiB contiguous: conflict-free.
+// MODE 0: per-lane top-KT, merged per workgroup -> cand[blockIdx][32][KT]
+// MODE 1: every key written to keys[q][doc] (the k > RR_FUSED_KMAX path)
+template <int DT, int KT, bool COS, int MODE>
+__global__ __launch_bounds__(kThreads) void fused_score_kernel(
+    const uint4* __restrict__ corpus, const float* __restrict__ norms, const float* __restrict__ queries,
+    int64_t n, int d, int b, uint32_t idx_base, uint64_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int U = kGroupChunks;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+
+  const int d4 = d >> 2;                          // float4 per query row
+  const int nchunk = DT == 0 ? (d >> 3) : (d >> 4);
+  const int ngroup = nchunk / U;
+  const size_t qimg_bytes = (size_t)nchunk * 2 * kQSlots * 16;  // per image
+  float* qnorm = (float*)(smem + (DT == 0 ? qimg_bytes : 2 * qimg_bytes));
+
+  // ---- stage the queries into LDS (zero rows for unused slots) --------------------------------
+  if constexpr (DT == 0) {
+    f32x4* Q4 = (f32x4*)smem;
+    for (int e = tid; e < kQSlots * d4; e += kThreads) {
+      const int q = e / d4, c4 = e - q * d4;   // c4 = 2 * chunk + half
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (q < b) v = ((const f32x4*)queries)[(size_t)q * d4 + c4];
+      Q4[c4 * kQSlots + q] = v;
+    }
+  } else {
+    bf16x8* Qhi = (bf16x8*)smem;
+    bf16x8* Qlo = (bf16x8*)(smem + qimg_bytes);
+    const int d8 = d >> 3;                       // 8-element groups per row = 2 * chunk + half
+    for (int e = tid; e < kQSlots * d8; e += kThreads) {
+      const int q = e / d8, c8 = e - q * d8;
+      bf16x8 hi, lo;
+      if (q < b) {
+        const f32x4* src = (const f32x4*)(queries + (size_t)q * d + c8 * 8);
+        const f32x4 x0 = src[0], x1 = src[1];
+        const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const __bf16 bh = (__bf16)xs[j];
+          hi[j] = bh;
+          lo[j] = (__bf16)(xs[j] - (float)bh);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { hi[j] = (__bf16)0.f; lo[j] = (__bf16)0.f; }
+      }
+      Qhi[c8 * kQSlots + q] = hi;
+      Qlo[c8 * kQSlots + q] = lo;
+    }
+  }
+  if constexpr (COS) {
+    // |q| in fp32 from the original fp32 queries (cp.linalg.norm(X, axis=1), retriever.py:602)
+    for (int q = wid; q < kQSlots; q += kWaves) {
+      float s = 0.f;
+      if (q < b)
+        for (int c = lane; c < d4; c += 64) {
+          const f32x4 v = ((const f32x4*)queries)[(size_t)q * d4 + c];
+          s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
+        }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+      if (lane == 0) qnorm[q] = sqrtf(s);
+    }
+  }
+  __syncthreads();
+
+  const bool qvalid = r < b;
+  const float qn = COS ? qnorm[r] : 0.f;
+  const int64_t ntiles = (n + kTileDocs - 1) / kTileDocs;
+  const int64_t nwave = (int64_t)gridDim.x * kWaves;
+  const int64_t rstride = DT == 0 ? (int64_t)(d >> 2) : (int64_t)(d >> 3);  // uint4 per corpus row
+
+  TopK<KT> tk;
+  tk.init();
+
+  int64_t tile = (int64_t)blockIdx.x * kWaves + wid;
+  if (tile < ntiles) {
+    auto rowp = [&](int64_t t) -> const uint4* {
+      int64_t row = t * kTileDocs + r;
+      row = row < n ? row : n - 1;
+      return corpus + row * rstride + h;
+    };
+    auto compute = [&](const uint4 (&buf)[U], int g, f32x16& acc) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int slot = (2 * (g * U + u) + h) * kQSlots + r;
+        if constexpr (DT == 0) {
+          const f32x4 a = __builtin_bit_cast(f32x4, buf[u]);
+          const f32x4 q = ((const f32x4*)smem)[slot];
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, q.x, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, q.y, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, q.z, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, q.w, acc, 0, 0, 0);
+        } else {
+          const bf16x8 a = __builtin_bit_cast(bf16x8, buf[u]);
+          const bf16x8 qh = ((const bf16x8*)smem)[slot];
+          const bf16x8 ql = ((const bf16x8*)(smem + qimg_bytes))[slot];
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qh, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, ql, acc, 0, 0, 0);
+        }
+      }
+    };
+    // doc norms of the current tile (cosine): lane holds docs 8*gq + 4h + {0..3}, gq = 0..3
+    f32x4 nrm[4];
+    auto load_norms = [&](int64_t t) {
+      if constexpr (COS) {
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) nrm[gq] = *(const f32x4*)(norms + t * kTileDocs + 8 * gq + 4 * h);
+      }
+    };
+    auto epilogue = [&](int64_t t, const f32x16& acc) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int dl = (v & 3) + 8 * (v >> 2) + 4 * h;   // C/D row map of the 32x32 MFMA
+        const int64_t doc = t * kTileDocs + dl;
+        float s = acc[v];
+        if constexpr (COS) {
+          // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
+          const float nd = nrm[v >> 2][v & 3];
+          s = s / (qn * nd + 1e-8f);
+          s = fminf(fmaxf(s, -1.0f), 1.0f);
+        }
+        if constexpr (MODE == 0) {
+          if (qvalid && doc < n) {
+            const uint64_t key = make_key(s, idx_base + (uint32_t)doc);
+            if (key > tk.last()) tk.insert(key);
+          }
+        } else {
+          if (qvalid && doc < n) out[(size_t)r * (size_t)n + (size_t)doc] = make_key(s, idx_base + (uint32_t)doc);
+        }
+      }
+    };
+
+    uint4 bufA[U], bufB[U];
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    const uint4* p = rowp(tile);
+    int g = 0;
+    load_norms(tile);
+#pragma unroll
+    for (int u = 0; u < U; ++u) bufA[u] = p[2 * u];
+
+    // One pipeline step: prefetch the next group (possibly the first group of the wave's next tile)
+    // into `nxt` while the MFMAs consume `cur`. Addresses stay in bounds (the final prefetch re-reads
+    // the current group), so no load sits under a branch.
+    bool more = true;
+    auto step = [&](const uint4 (&cur)[U], uint4 (&nxt)[U]) {
+      int ng = g + 1;
+      int64_t ntile = tile;
+      const uint4* np = p;
+      if (ng == ngroup) {
+        ng = 0;
+        ntile = tile + nwave;
+        np = ntile < ntiles ? rowp(ntile) : p;
+      }
+      more = ntile < ntiles;
+      const uint4* src = more ? np + 2 * U * ng : p + 2 * U * g;
+#pragma unroll
+      for (int u = 0; u < U; ++u) nxt[u] = src[2 * u];
+      // keep the prefetch ahead of the MFMAs (hipcc otherwise sinks the loads below them)
+      __builtin_amdgcn_sched_barrier(0);
+      compute(cur, g, acc);
+      if (g == ngroup - 1) {
+        epilogue(tile, acc);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+        if (more) load_norms(ntile);
+      }
+      tile = ntile;
+      g = ng;
+      p = np;
+    };
+    for (;;) {
+      step(bufA, bufB);
+      if (!more) break;
+      step(bufB, bufA);
+      if (!more) break;
+    }
+  }
+
+  if constexpr (MODE == 0) {
+    // ---- workgroup merge: 16 lists (8 waves x 2 halves) per query slot -> top-KT -----------------
+    __syncthreads();                      // query image no longer needed: reuse LDS
+    uint64_t* L = (uint64_t*)smem;        // [32 q][16 lists][KT]
+    const int list = wid * 2 + h;
+#pragma unroll
+    for (int i = 0; i < KT; ++i) L[((size_t)r * 16 + list) * KT + i] = tk.v[i];
+    __syncthreads();
+    constexpr int IT = (16 * KT) / 64;
+    for (int q = wid; q < kQSlots; q += kWaves) {
+      const uint64_t* src = L + (size_t)q * 16 * KT;
+      uint64_t it[IT];
+#pragma unroll
+      for (int i = 0; i < IT; ++i) it[i] = src[lane + 64 * i];
+      uint64_t* dst = out + ((size_t)blockIdx.x * kQSlots + q) * KT;
+      for (int rnd = 0; rnd < KT; ++rnd) {
+        uint64_t best = 0;
+#pragma unroll
+        for (int i = 0; i < IT; ++i) best = umax64(best, it[i]);
+        best = wave_max_u64(best);
+#pragma unroll
+        for (int i = 0; i < IT; ++i) it[i] = (it[i] == best) ? 0 : it[i];
+        if (lane == 0) dst[rnd] = best;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// merge of candidate lists: in [nlists][32][in_kt] -> top-KT per query slot
+// ------------------------------------------------------------------------------------------------
+template <int KT>
+__global__ __launch_bounds__(256) void merge_kernel(const uint64_t* __restrict__ in, int nlists, int in_kt,
+                                                    int b, int k_out, uint64_t* __restrict__ out_keys,
+                                                    float* __restrict__ out_scores,
+                                                    int64_t* __restrict__ out_idx) {
+  const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ uint64_t wmax[4];
+  __shared__ uint64_t res[KT];
+  TopK<KT> tk;
+  tk.init();
+  const int total = nlists * in_kt;
+  for (int e = tid; e < total; e += 256) {
+    const int l = e / in_kt, i = e - l * in_kt;
+    const uint64_t key = in[((size_t)l * kQSlots + q) * in_kt + i];
+    if (key > tk.last()) tk.insert(key);
+  }
+  for (int rnd = 0; rnd < KT; ++rnd) {
+    const uint64_t head = tk.v[0];
+    const uint64_t m = wave_max_u64(head);
+    if (lane == 0) wmax[wid] = m;
+    __syncthreads();
+    const uint64_t best = umax64(umax64(wmax[0], wmax[1]), umax64(wmax[2], wmax[3]));
+    if (best != 0 && head == best) tk.pop();   // keys are unique: exactly one owner
+    if (tid == 0) res[rnd] = best;
+    __syncthreads();
+  }
+  if (out_keys && tid < KT) out_keys[(size_t)q * KT + tid] = res[tid];
+  if (out_scores && q < b && tid < k_out) {
+    const uint64_t key = res[tid];
+    float s = -INFINITY;
+    int64_t ix = -1;
+    if (key != 0) {
+      s = float_of_ord((uint32_t)(key >> 32));
+      ix = (int64_t)(0xFFFFFFFFu - (uint32_t)key);
+    }
+    out_scores[(size_t)q * k_out + tid] = s;
+    out_idx[(size_t)q * k_out + tid] = ix;
+  }
+}
+
+__global__ void decode_kernel(const uint64_t* __restrict__ keys, int64_t count, float* __restrict__ scores,
+                              int64_t* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const uint64_t key = keys[i];
+  float s = -INFINITY;
+  int64_t ix = -1;
+  if (key != 0) {
+    s = float_of_ord((uint32_t)(key >> 32));
+    ix = (int64_t)(0xFFFFFFFFu - (uint32_t)key);
+  }
+  scores[i] = s;
+  idx[i] = ix;
+}
+
+// sorted [b][seg] -> out [32 slots][k] (rows >= b untouched)
+__global__ void take_prefix_kernel(const uint64_t* __restrict__ sorted, int64_t seg, int k,
+                                   uint64_t* __restrict__ out) {
+  const int q = blockIdx.y;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gridDim.x * blockDim.x)
+    out[(size_t)q * k + i] = i < seg ? sorted[(size_t)q * seg + i] : 0;
+}
+
+// gathered [world][32][k] -> per-query segments [b][world*k] (k > RR_FUSED_KMAX cross-shard merge)
+__global__ void regroup_kernel(const uint64_t* __restrict__ in, int world, int k, uint64_t* __restrict__ out) {
+  const int q = blockIdx.y;
+  const int total = world * k;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int g = i / k, j = i - g * k;
+    out[(size_t)q * total + i] = in[((size_t)g * kQSlots + q) * k + j];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// corpus preparation
+// ------------------------------------------------------------------------------------------------
+__global__ void f32_to_bf16_kernel(const float* __restrict__ in, __bf16* __restrict__ out, int64_t count) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 3 < count) {
+    const f32x4 v = *(const f32x4*)(in + i);
+    out[i] = (__bf16)v.x; out[i + 1] = (__bf16)v.y; out[i + 2] = (__bf16)v.z; out[i + 3] = (__bf16)v.w;
+  } else {
+    for (int64_t j = i; j < count; ++j) out[j] = (__bf16)in[j];
+  }
+}
+
+__global__ void bf16_to_f32_kernel(const __bf16* __restrict__ in, float* __restrict__ out, int64_t count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) out[i] = (float)in[i];
+}
+
+// One wave per row: |row|_2 in fp32 (the reference recomputes cp.linalg.norm(Y, axis=1) every call,
+// retriever.py:603; here it is computed once at load).
+template <int DT>
+__global__ __launch_bounds__(256) void row_norms_kernel(const void* __restrict__ corpus, int64_t n, int d,
+                                                         float* __restrict__ norms) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  float s = 0.f;
+  if constexpr (DT == 0) {
+    const f32x4* p = (const f32x4*)((const float*)corpus + row * d);
+    for (int c = lane; c < (d >> 2); c += 64) {
+      const f32x4 v = p[c];
+      s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
+    }
+  } else {
+    const __bf16* p = (const __bf16*)corpus + row * d;
+    for (int c = lane; c < d; c += 64) { const float v = (float)p[c]; s = fmaf(v, v, s); }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) norms[row] = sqrtf(s);
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// kind 0: ((h mod 255) - 127) / 128 ; kind 1: Irwin-Hall(4) * sqrt(3) (unnormalised)
+__global__ void synth_kernel(int kind, uint64_t seed, int64_t row_begin, int64_t n_rows, int d,
+                             float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_rows * (int64_t)d) return;
+  const uint64_t gi = (uint64_t)(row_begin * (int64_t)d) + (uint64_t)i;
+  const uint64_t z = splitmix64(seed, gi);
+  float v;
+  if (kind == 0) {
+    v = (float)((int)(z % 255ull) - 127) * 0.0078125f;
+  } else {
+    const float u = (float)(z & 0xFFFF) + (float)((z >> 16) & 0xFFFF) + (float)((z >> 32) & 0xFFFF) +
+                    (float)(z >> 48);
+    v = (u * (1.0f / 65536.0f) - 2.0f) * 1.7320508f;
+  }
+  out[i] = v;
+}
+
+__global__ __launch_bounds__(256) void normalize_rows_kernel(float* __restrict__ x, int64_t n, int d) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  float* p = x + row * d;
+  float s = 0.f;
+  for (int c = lane; c < d; c += 64) s = fmaf(p[c], p[c], s);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+  const float inv = 1.0f / sqrtf(s);
+  for (int c = lane; c < d; c += 64) p[c] = p[c] * inv;
+}
+
+// ------------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------------
+int fused_kt(int k) {
+  if (k <= 4) return 4;
+  if (k <= 8) return 8;
+  if (k <= 16) return 16;
+  if (k <= 32) return 32;
+  return 0;
+}
+
+size_t fused_lds_bytes(int d, int kt, int dtype) {
+  const size_t qimg = (size_t)kQSlots * d * 4;   // fp32 image, or bf16 hi + lo images
+  const size_t merge = (size_t)kQSlots * 16 * (kt > 0 ? kt : 1) * 8;
+  const size_t a = qimg + kQSlots * sizeof(float);
+  (void)dtype;
+  return a > merge ? a : merge;
+}
+
+template <int DT, int KT, bool COS, int MODE>
+static hipError_t launch_fused_t(int grid, const void* corpus, const float* norms, const float* queries,
+                                 int64_t n, int d, int b, uint32_t idx_base, uint64_t* out, hipStream_t s) {
+  const size_t lds = fused_lds_bytes(d, MODE == 0 ? KT : 1, DT);
+  auto kern = fused_score_kernel<DT, KT, COS, MODE>;
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, (const uint4*)corpus, norms, queries, n, d, b,
+                     idx_base, out);
+  return hipGetLastError();
+}
+
+template <int DT, bool COS>
+static hipError_t launch_fused_k(int kt, int grid, const void* corpus, const float* norms, const float* queries,
+                                 int64_t n, int d, int b, uint32_t idx_base, uint64_t* cand, hipStream_t s) {
+  switch (kt) {
+    case 4: return launch_fused_t<DT, 4, COS, 0>(grid, corpus, norms, queries, n, d, b, idx_base, cand, s);
+    case 8: return launch_fused_t<DT, 8, COS, 0>(grid, corpus, norms, queries, n, d, b, idx_base, cand, s);
+    case 16: return launch_fused_t<DT, 16, COS, 0>(grid, corpus, norms, queries, n, d, b, idx_base, cand, s);
+    case 32: return launch_fused_t<DT, 32, COS, 0>(grid, corpus, norms, queries, n, d, b, idx_base, cand, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_fused(int dtype, int metric, int kt, int grid, const void* corpus, const float* norms,
+                        const float* queries, int64_t n, int d, int b, uint32_t idx_base, uint64_t* cand,
+                        hipStream_t s) {
+  if (dtype == 0)
+    return metric ? launch_fused_k<0, true>(kt, grid, corpus, norms, queries, n, d, b, idx_base, cand, s)
+                  : launch_fused_k<0, false>(kt, grid, corpus, norms, queries, n, d, b, idx_base, cand, s);
+  return metric ? launch_fused_k<1, true>(kt, grid, corpus, norms, queries, n, d, b, idx_base, cand, s)
+                : launch_fused_k<1, false>(kt, grid, corpus, norms, queries, n, d, b, idx_base, cand, s);
+}
+
+hipError_t launch_full_keys(int dtype, int metric, int grid, const void* corpus, const float* norms,
+                            const float* queries, int64_t n, int d, int b, uint32_t idx_base, uint64_t* keys,
+                            hipStream_t s) {
+  if (dtype == 0)
+    return metric ? launch_fused_t<0, 4, true, 1>(grid, corpus, norms, queries, n, d, b, idx_base, keys, s)
+                  : launch_fused_t<0, 4, false, 1>(grid, corpus, norms, queries, n, d, b, idx_base, keys, s);
+  return metric ? launch_fused_t<1, 4, true, 1>(grid, corpus, norms, queries, n, d, b, idx_base, keys, s)
+                : launch_fused_t<1, 4, false, 1>(grid, corpus, norms, queries, n, d, b, idx_base, keys, s);
+}
+
+hipError_t launch_merge(int kt, const uint64_t* in, int nlists, int in_kt, int b, int k_out, uint64_t* out_keys,
+                        float* out_scores, int64_t* out_idx, hipStream_t s) {
+  // Rows >= b of out_keys are still produced (from the zero-filled slots) so the buffer is uniform.
+  const int grid = out_keys ? kQSlots : b;
+  switch (kt) {
+    case 4: hipLaunchKernelGGL(merge_kernel<4>, dim3(grid), dim3(256), 0, s, in, nlists, in_kt, b, k_out, out_keys, out_scores, out_idx); break;
+    case 8: hipLaunchKernelGGL(merge_kernel<8>, dim3(grid), dim3(256), 0, s, in, nlists, in_kt, b, k_out, out_keys, out_scores, out_idx); break;
+    case 16: hipLaunchKernelGGL(merge_kernel<16>, dim3(grid), dim3(256), 0, s, in, nlists, in_kt, b, k_out, out_keys, out_scores, out_idx); break;
+    case 32: hipLaunchKernelGGL(merge_kernel<32>, dim3(grid), dim3(256), 0, s, in, nlists, in_kt, b, k_out, out_keys, out_scores, out_idx); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t segmented_sort_desc(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, int b,
+                               int64_t seg, hipStream_t s) {
+  hipcub::CountingInputIterator<int64_t> it0(0);
+  struct Mul {
+    int64_t seg;
+    __host__ __device__ int64_t operator()(int64_t i) const { return i * seg; }
+  };
+  hipcub::TransformInputIterator<int64_t, Mul, hipcub::CountingInputIterator<int64_t>> offs(it0, Mul{seg});
+  return hipcub::DeviceSegmentedRadixSort::SortKeysDescending(temp, *temp_bytes, in, out, (int64_t)b * seg, b,
+                                                              offs, offs + 1, 0, 64, s);
+}
+
+hipError_t launch_take_prefix(const uint64_t* sorted, int b, int64_t seg, int k, uint64_t* out_keys,
+                              hipStream_t s) {
+  const int gx = (k + 255) / 256;
+  hipLaunchKernelGGL(take_prefix_kernel, dim3(gx, b), dim3(256), 0, s, sorted, seg, k, out_keys);
+  return hipGetLastError();
+}
+
+hipError_t launch_regroup(const uint64_t* gathered, int world, int k, int b, uint64_t* out, hipStream_t s) {
+  const int64_t seg = (int64_t)world * k;
+  hipLaunchKernelGGL(regroup_kernel, dim3((unsigned)((seg + 255) / 256), b), dim3(256), 0, s, gathered, world, k, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode(const uint64_t* keys, int b, int k, float* scores, int64_t* idx, hipStream_t s) {
+  const int64_t count = (int64_t)b * k;
+  hipLaunchKernelGGL(decode_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, keys, count, scores, idx);
+  return hipGetLastError();
+}
+
+hipError_t launch_f32_to_bf16(const float* in, uint16_t* out, int64_t count, hipStream_t s) {
+  const int64_t threads = (count + 3) / 4;
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, in,
+                     (__bf16*)out, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_bf16_to_f32(const uint16_t* in, float* out, int64_t count, hipStream_t s) {
+  hipLaunchKernelGGL(bf16_to_f32_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s,
+                     (const __bf16*)in, out, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_row_norms(int dtype, const void* corpus, int64_t n, int d, float* norms, hipStream_t s) {
+  const unsigned grid = (unsigned)((n + 3) / 4);
+  if (dtype == 0) hipLaunchKernelGGL(row_norms_kernel<0>, dim3(grid), dim3(256), 0, s, corpus, n, d, norms);
+  else hipLaunchKernelGGL(row_norms_kernel<1>, dim3(grid), dim3(256), 0, s, corpus, n, d, norms);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth(int kind, uint64_t seed, int64_t row_begin, int64_t n_rows, int d, float* out,
+                        hipStream_t s) {
+  const int64_t count = n_rows * (int64_t)d;
+  hipLaunchKernelGGL(synth_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, kind, seed, row_begin,
+                     n_rows, d, out);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || kind == 0) return e;
+  hipLaunchKernelGGL(normalize_rows_kernel, dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, s, out, n_rows, d);
+  return hipGetLastError();
+}
+
+}  // namespace rr

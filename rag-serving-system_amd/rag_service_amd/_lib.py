@@ -1,0 +1,248 @@
+"""ctypes binding of the C-ABI in include/rag_retrieval.h (librag_retrieval.so, built in-tree).
+
+No PyTorch and no CPU fallback: if the shared library is missing or fails to load, every entry point
+raises ``HipRetrievalUnavailable``. The product path never routes through ``oracle/``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # rag-serving-system_amd/
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_PATH = os.path.join(PKG_ROOT, "librag_retrieval.so")
+HEADER_PATH = os.path.join(REPO_ROOT, "include", "rag_retrieval.h")
+
+# mirrors include/rag_retrieval.h
+RR_OK = 0
+RR_E_INVALID = -1
+RR_E_HIP = -2
+RR_E_RCCL = -3
+RR_E_STATE = -4
+RR_E_UNSUPPORTED = -5
+RR_E_OOM = -6
+RR_DTYPE_F32 = 0
+RR_DTYPE_BF16 = 1
+RR_METRIC_DOT = 0
+RR_METRIC_COSINE = 1
+RR_SYNTH_EXACT_INT = 0
+RR_SYNTH_UNIT_NORM = 1
+RR_UNIQUE_ID_BYTES = 128
+RR_FUSED_KMAX = 32
+RR_ABI_VERSION = 1
+
+DTYPES = {"fp32": RR_DTYPE_F32, "float32": RR_DTYPE_F32, "f32": RR_DTYPE_F32,
+          "bf16": RR_DTYPE_BF16, "bfloat16": RR_DTYPE_BF16}
+METRICS = {"dot": RR_METRIC_DOT, "cosine": RR_METRIC_COSINE}
+
+# Every function the header declares: name -> (restype, argtypes)
+_c_int, _c_i32, _c_i64, _c_u64 = ctypes.c_int, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
+_vp, _fp, _i64p, _ip = ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)
+SIGNATURES = {
+    "rr_create": (_c_int, [_ip, _c_int, _c_int, _c_int, ctypes.POINTER(_vp)]),
+    "rr_destroy": (None, [_vp]),
+    "rr_last_error": (ctypes.c_char_p, []),
+    "rr_abi_version": (_c_int, []),
+    "rr_get_unique_id": (_c_int, [ctypes.c_char_p]),
+    "rr_init_dist": (_c_int, [_vp, _c_int, _c_int, ctypes.c_char_p]),
+    "rr_load": (_c_int, [_vp, _fp, _c_i64, _c_i32]),
+    "rr_load_rows": (_c_int, [_vp, _fp, _c_i64, _c_i64, _c_i64, _c_i32]),
+    "rr_fill_synthetic": (_c_int, [_vp, _c_int, _c_u64, _c_i64, _c_i32]),
+    "rr_info": (_c_int, [_vp, _i64p, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32)]),
+    "rr_shard_range": (_c_int, [_vp, _c_int, _i64p, _i64p]),
+    "rr_read_rows": (_c_int, [_vp, _c_i64, _c_i64, _fp]),
+    "rr_search": (_c_int, [_vp, _fp, _c_i32, _c_i32, _c_i32, _fp, _i64p]),
+    "rr_set_queries": (_c_int, [_vp, _fp, _c_i32, _c_i32]),
+    "rr_search_staged": (_c_int, [_vp, _c_i32]),
+    "rr_synchronize": (_c_int, [_vp]),
+    "rr_fetch_results": (_c_int, [_vp, _fp, _i64p]),
+    "rr_set_queries_device": (_c_int, [_vp, _vp, _c_i32, _c_i32]),
+    "rr_set_timing": (_c_int, [_vp, _c_int]),
+    "rr_kernel_time": (_c_int, [_vp, ctypes.POINTER(ctypes.c_double), _i64p, _c_int]),
+}
+
+
+class HipRetrievalUnavailable(RuntimeError):
+    """The HIP extension is not built or cannot be loaded (there is no CPU fallback)."""
+
+
+class HipRetrievalError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"rr error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def build(force: bool = False) -> str:
+    """Compile librag_retrieval.so for gfx950 with hipcc (in-tree)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-C", PKG_ROOT, "-j4"])
+    return LIB_PATH
+
+
+def load_library(path: Optional[str] = None):
+    """Load (once) and type the shared library. Raises HipRetrievalUnavailable if absent."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise HipRetrievalUnavailable(
+                f"{p} not found: build it with `make -C {PKG_ROOT}` (hipcc --offload-arch=gfx950)")
+        try:
+            lib = ctypes.CDLL(p)
+        except OSError as e:
+            raise HipRetrievalUnavailable(f"cannot load {p}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.rr_abi_version() != RR_ABI_VERSION:
+            raise HipRetrievalUnavailable("ABI version mismatch")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def _check(rc: int) -> None:
+    if rc != RR_OK:
+        msg = load_library().rr_last_error().decode(errors="replace")
+        raise HipRetrievalError(rc, msg)
+
+
+def _fptr(a: np.ndarray):
+    return a.ctypes.data_as(_fp)
+
+
+def _i64ptr(a: np.ndarray):
+    return a.ctypes.data_as(_i64p)
+
+
+def get_unique_id() -> bytes:
+    lib = load_library()
+    buf = ctypes.create_string_buffer(RR_UNIQUE_ID_BYTES)
+    _check(lib.rr_get_unique_id(buf))
+    return buf.raw
+
+
+class Index:
+    """Owning wrapper of one ``rr_handle``: a (possibly sharded) corpus resident in HBM.
+
+    The arithmetic contract is the C-ABI's: results sorted by (score desc, index asc); slots beyond
+    the corpus size hold (-inf, -1).
+    """
+
+    def __init__(self, devices: Optional[Sequence[int]] = None, dtype: str = "fp32", metric: str = "cosine"):
+        self._lib = load_library()
+        if dtype not in DTYPES:
+            raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
+        if metric not in METRICS:
+            raise ValueError(f"metric must be one of {sorted(METRICS)}")
+        self.dtype, self.metric = dtype, metric
+        h = _vp()
+        if devices is None:
+            _check(self._lib.rr_create(None, 1, DTYPES[dtype], METRICS[metric], ctypes.byref(h)))
+        else:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            _check(self._lib.rr_create(arr, len(devices), DTYPES[dtype], METRICS[metric], ctypes.byref(h)))
+        self._h = h
+        self.n = 0
+        self.d = 0
+
+    # -- lifecycle ---------------------------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.rr_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def init_dist(self, world: int, rank: int, unique_id: bytes) -> None:
+        _check(self._lib.rr_init_dist(self._h, world, rank, unique_id))
+
+    # -- corpus ------------------------------------------------------------------------------------
+    def load(self, corpus: np.ndarray) -> None:
+        c = np.ascontiguousarray(corpus, dtype=np.float32)
+        if c.ndim != 2:
+            raise ValueError("corpus must be 2-D")
+        _check(self._lib.rr_load(self._h, _fptr(c), c.shape[0], c.shape[1]))
+        self.n, self.d = c.shape
+
+    def load_rows(self, rows: np.ndarray, row_begin: int, n_total: int) -> None:
+        r = np.ascontiguousarray(rows, dtype=np.float32)
+        _check(self._lib.rr_load_rows(self._h, _fptr(r), row_begin, r.shape[0], n_total, r.shape[1]))
+        self.n, self.d = n_total, r.shape[1]
+
+    def fill_synthetic(self, kind: int, seed: int, n: int, d: int) -> None:
+        _check(self._lib.rr_fill_synthetic(self._h, kind, seed, n, d))
+        self.n, self.d = n, d
+
+    def info(self) -> Tuple[int, int, int, int]:
+        n, d, nl, w = _c_i64(), _c_i32(), _c_i32(), _c_i32()
+        _check(self._lib.rr_info(self._h, ctypes.byref(n), ctypes.byref(d), ctypes.byref(nl), ctypes.byref(w)))
+        return n.value, d.value, nl.value, w.value
+
+    def shard_range(self, i: int = 0) -> Tuple[int, int]:
+        b, e = _c_i64(), _c_i64()
+        _check(self._lib.rr_shard_range(self._h, i, ctypes.byref(b), ctypes.byref(e)))
+        return b.value, e.value
+
+    def read_rows(self, row_begin: int, n_rows: int) -> np.ndarray:
+        out = np.empty((n_rows, self.d), dtype=np.float32)
+        _check(self._lib.rr_read_rows(self._h, row_begin, n_rows, _fptr(out)))
+        return out
+
+    # -- search ------------------------------------------------------------------------------------
+    def search(self, queries: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        if q.ndim != 2:
+            raise ValueError("queries must be 2-D")
+        b = q.shape[0]
+        scores = np.empty((b, k), dtype=np.float32)
+        idx = np.empty((b, k), dtype=np.int64)
+        _check(self._lib.rr_search(self._h, _fptr(q), b, q.shape[1], k, _fptr(scores), _i64ptr(idx)))
+        return scores, idx
+
+    def set_queries(self, queries: np.ndarray) -> None:
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        _check(self._lib.rr_set_queries(self._h, _fptr(q), q.shape[0], q.shape[1]))
+        self._staged_b = q.shape[0]
+
+    def set_queries_device(self, dev_ptr: int, b: int, d: int) -> None:
+        _check(self._lib.rr_set_queries_device(self._h, _vp(dev_ptr), b, d))
+        self._staged_b = b
+
+    def search_staged(self, k: int) -> None:
+        _check(self._lib.rr_search_staged(self._h, k))
+        self._staged_k = k
+
+    def synchronize(self) -> None:
+        _check(self._lib.rr_synchronize(self._h))
+
+    def fetch(self) -> Tuple[np.ndarray, np.ndarray]:
+        b, k = self._staged_b, self._staged_k
+        scores = np.empty((b, k), dtype=np.float32)
+        idx = np.empty((b, k), dtype=np.int64)
+        _check(self._lib.rr_fetch_results(self._h, _fptr(scores), _i64ptr(idx)))
+        return scores, idx
+
+    def set_timing(self, enable: bool) -> None:
+        _check(self._lib.rr_set_timing(self._h, 1 if enable else 0))
+
+    def kernel_time(self, reset: bool = True) -> Tuple[float, int]:
+        ms, cnt = ctypes.c_double(), _c_i64()
+        _check(self._lib.rr_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(cnt), 1 if reset else 0))
+        return ms.value, cnt.value

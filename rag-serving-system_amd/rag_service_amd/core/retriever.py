@@ -1,0 +1,241 @@
+"""Drop-in retrievers backed by the MI355X C-ABI (librag_retrieval.so).
+
+Two classes mirror the reference's two live retrievers (ngray0/RAG-Serving-System,
+rag_service/core/retriever.py), keeping their constructor, method names, argument meaning,
+validation order, k-clamping and "log and return empty lists" error convention:
+
+* ``HipRetriever``        <- ``CupyRetriever``   (retriever.py:564-799): clipped cosine similarity,
+                             strict ``isinstance(k, int)`` check, ``max_k`` batching + per-query slicing.
+                             This is the class ``main.py:52-55`` / ``batch_processor.py:11,21`` use.
+* ``HipSimpleRetriever``  <- ``SimpleRetriever`` (retriever.py:57-166): raw dot product, per-query k
+                             rules of ``retrieve`` applied to every query of a batch.
+
+All arithmetic happens in the HIP kernels; there is no NumPy/CPU fallback. If the extension is missing,
+construction raises ``HipRetrievalUnavailable``.
+
+Deliberate, documented difference: ties between exactly equal scores are broken by ascending document
+index (the reference's order on ties is whatever numpy introselect / CuPy's sort produce).
+"""
+from __future__ import annotations
+
+import logging
+import numbers
+import time
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .._lib import Index
+
+logger = logging.getLogger(__name__)
+
+
+def _is_integral(k) -> bool:
+    return isinstance(k, (numbers.Integral, np.integer))
+
+
+class _HipRetrieverBase:
+    _metric = "cosine"
+
+    def __init__(self, doc_embeddings: np.ndarray, documents: List[str], dtype: str = "fp32",
+                 devices: Optional[Sequence[int]] = None):
+        if doc_embeddings.dtype != np.float32:
+            logger.warning(f"Input doc_embeddings dtype is {doc_embeddings.dtype}, converting to float32.")
+            doc_embeddings = doc_embeddings.astype(np.float32)
+        try:
+            self.index = Index(devices=devices, dtype=dtype, metric=self._metric)
+            self.index.load(doc_embeddings)
+            logger.info(f"Moved document embeddings ({doc_embeddings.shape}) to HBM "
+                        f"({dtype}, {self._metric}, devices={list(devices) if devices else [0]}).")
+        except Exception as e:
+            logger.error(f"Failed to move document embeddings to the GPU: {e}", exc_info=True)
+            raise
+        self.documents = documents
+        self.N_A = int(doc_embeddings.shape[0])
+        self.D = int(doc_embeddings.shape[1])
+        self.dtype = dtype
+
+    # extra (not in the reference): raw device results for tests and benchmarks
+    def search(self, queries: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:
+        """(scores [b,k] fp32, global indices [b,k] int64) sorted by (score desc, index asc)."""
+        return self.index.search(np.atleast_2d(np.asarray(queries, dtype=np.float32)), int(k))
+
+    def _docs(self, idx_row: np.ndarray, k_i: int) -> List[str]:
+        valid = idx_row[idx_row >= 0][:k_i]
+        return [self.documents[int(j)] for j in valid]
+
+    def close(self) -> None:
+        self.index.close()
+
+
+class HipRetriever(_HipRetrieverBase):
+    """Drop-in for ``CupyRetriever`` (retriever.py:564-799): clipped cosine similarity on MI355X."""
+
+    _metric = "cosine"
+
+    def __init__(self, doc_embeddings: np.ndarray, documents: List[str], dtype: str = "fp32",
+                 devices: Optional[Sequence[int]] = None, metric: str = "cosine"):
+        self._metric = metric
+        super().__init__(doc_embeddings, documents, dtype=dtype, devices=devices)
+        logger.info(f"Initialized HipRetriever with {self.N_A} documents (Dim={self.D}).")
+
+    # retriever.py:615-683
+    def retrieve(self, query_emb: np.ndarray, k: int = 2) -> List[str]:
+        start_time = time.time()
+        if not isinstance(query_emb, np.ndarray):
+            logger.error(f"HipRetriever.retrieve expects query_emb as NumPy array, got {type(query_emb)}")
+            return []
+        if query_emb.ndim == 2 and query_emb.shape[0] == 1:
+            query_emb = query_emb.flatten()
+        elif query_emb.ndim != 1:
+            logger.error(f"HipRetriever.retrieve expects a 1D query embedding or (1, dim), got shape {query_emb.shape}")
+            return []
+        if query_emb.shape[0] != self.D:
+            logger.error(f"Query embedding dimension ({query_emb.shape[0]}) does not match document embedding dimension ({self.D})")
+            return []
+        actual_k = min(k, self.N_A)
+        if actual_k <= 0:
+            logger.warning(f"Requested k={k} results in actual_k={actual_k}. Returning empty list.")
+            return []
+        try:
+            if not _is_integral(actual_k):
+                raise TypeError(f"k must be an integer, got {type(k)}")
+            if query_emb.dtype != np.float32:
+                query_emb = query_emb.astype(np.float32)
+            _, idx = self.index.search(query_emb.reshape(1, self.D), int(actual_k))
+            docs = self._docs(idx[0], int(actual_k))
+            logger.debug(f"HipRetriever.retrieve took {time.time() - start_time:.6f}s")
+            return docs
+        except Exception as e:
+            logger.error(f"Error during HipRetriever.retrieve: {e}", exc_info=True)
+            return []
+
+    # retriever.py:686-799
+    def batch_retrieve(self, query_embeddings: np.ndarray, ks: List[int]) -> List[List[str]]:
+        start_time = time.time()
+        batch_size = query_embeddings.shape[0]   # read before the type check, as the reference does (:702)
+
+        if not isinstance(query_embeddings, np.ndarray):
+            logger.error(f"HipRetriever.batch_retrieve expects query_embeddings as NumPy array, got {type(query_embeddings)}")
+            return [[] for _ in ks]
+        if query_embeddings.ndim != 2:
+            logger.error(f"HipRetriever.batch_retrieve expects a 2D query_embeddings array, got {query_embeddings.ndim} dimensions.")
+            return [[] for _ in ks]
+        if batch_size == 0:
+            logger.info("Received empty batch of queries.")
+            return []
+        if not isinstance(ks, list) or batch_size != len(ks):
+            logger.error(f"Batch retrieve size mismatch: {batch_size} embeddings vs {len(ks)} k values.")
+            return [[] for _ in range(batch_size)]
+        if query_embeddings.shape[1] != self.D:
+            logger.error(f"Batch query embedding dimension ({query_embeddings.shape[1]}) does not match document embedding dimension ({self.D})")
+            return [[] for _ in ks]
+        if not all(isinstance(k_val, int) for k_val in ks):
+            logger.error("List ks must contain only integers.")
+            return [[] for _ in ks]
+
+        valid_ks = [k_val for k_val in ks if k_val > 0]
+        if not valid_ks:
+            logger.warning("All k values in ks are non-positive. Returning list of empty lists.")
+            return [[] for _ in ks]
+        max_k = min(max(valid_ks), self.N_A)
+        if max_k <= 0:
+            return [[] for _ in ks]
+
+        try:
+            if query_embeddings.dtype != np.float32:
+                query_embeddings = query_embeddings.astype(np.float32)
+            _, idx = self.index.search(query_embeddings, int(max_k))
+            batch_results = []
+            for i in range(batch_size):
+                k_i = ks[i]
+                if k_i <= 0:
+                    batch_results.append([])
+                    continue
+                batch_results.append(self._docs(idx[i], k_i))
+            logger.debug(f"HipRetriever.batch_retrieve took {time.time() - start_time:.6f}s")
+            return batch_results
+        except Exception as e:
+            logger.error(f"Error during HipRetriever.batch_retrieve: {e}", exc_info=True)
+            return [[] for _ in ks]
+
+
+class HipSimpleRetriever(_HipRetrieverBase):
+    """Drop-in for ``SimpleRetriever`` (retriever.py:57-166): raw dot-product similarity on MI355X."""
+
+    _metric = "dot"
+
+    def __init__(self, doc_embeddings: np.ndarray, documents: List[str], dtype: str = "fp32",
+                 devices: Optional[Sequence[int]] = None):
+        super().__init__(doc_embeddings, documents, dtype=dtype, devices=devices)
+        logger.info(f"Initialized HipSimpleRetriever with {len(self.documents)} documents.")
+
+    # per-query k rules of retrieve (:89-94): None -> invalid, else the clamped k
+    def _effective_k(self, k) -> Optional[int]:
+        if k <= 0:
+            return None
+        if k > self.N_A:
+            k = self.N_A
+        return int(k) if _is_integral(k) else None
+
+    # retriever.py:78-128
+    def retrieve(self, query_emb: np.ndarray, k: int = 2) -> List[str]:
+        if k <= 0:
+            logger.warning(f"Requested k={k} is non-positive. Returning empty list.")
+            return []
+        if k > self.N_A:
+            logger.warning(f"Requested k={k} is larger than the number of documents ({self.N_A}). Returning all documents.")
+            k = self.N_A
+        try:
+            if query_emb.dtype != np.float32:
+                query_emb = query_emb.astype(np.float32)
+            if query_emb.ndim != 1:
+                if query_emb.ndim == 2 and query_emb.shape[0] == 1:
+                    query_emb = query_emb.flatten()
+                else:
+                    logger.error(f"HipSimpleRetriever.retrieve expects a 1D query embedding, got shape {query_emb.shape}")
+                    return []
+            if query_emb.shape[0] != self.D:
+                logger.error(f"Query embedding dimension ({query_emb.shape[0]}) does not match document embedding dimension ({self.D})")
+                return []
+            if not _is_integral(k):
+                raise TypeError(f"k must be an integer, got {type(k)}")
+            _, idx = self.index.search(query_emb.reshape(1, self.D), int(k))
+            return self._docs(idx[0], int(k))
+        except Exception as e:
+            logger.error(f"Unexpected error during HipSimpleRetriever.retrieve: {e}", exc_info=True)
+            return []
+
+    # retriever.py:131-166 — same per-query results as calling retrieve() B times, one device pass
+    def batch_retrieve(self, query_embeddings: np.ndarray, ks: List[int]) -> List[List[str]]:
+        if query_embeddings.ndim != 2:
+            logger.error(f"HipSimpleRetriever.batch_retrieve expects a 2D query_embeddings array, got {query_embeddings.ndim} dimensions.")
+            return [[] for _ in ks]
+        if query_embeddings.shape[0] != len(ks):
+            logger.error(f"Batch retrieve size mismatch: {query_embeddings.shape[0]} embeddings vs {len(ks)} k values.")
+            return [[] for _ in ks]
+        if query_embeddings.shape[1] != self.D:
+            logger.error(f"Batch query embedding dimension ({query_embeddings.shape[1]}) does not match document embedding dimension ({self.D})")
+            return [[] for _ in ks]
+
+        eff = [self._effective_k(k) for k in ks]
+        results: List[List[str]] = [[] for _ in ks]
+        rows = [i for i, e in enumerate(eff) if e is not None]
+        if not rows:
+            return results
+        try:
+            q = query_embeddings[rows]
+            if q.dtype != np.float32:
+                q = q.astype(np.float32)
+            _, idx = self.index.search(q, max(eff[i] for i in rows))
+            for j, i in enumerate(rows):
+                results[i] = self._docs(idx[j], eff[i])
+            return results
+        except Exception as e:
+            logger.error(f"Unexpected error during HipSimpleRetriever.batch_retrieve: {e}", exc_info=True)
+            return [[] for _ in ks]
+
+
+# Names a maintainer can import in place of the reference's classes.
+CupyRetriever = HipRetriever
+SimpleRetriever = HipSimpleRetriever

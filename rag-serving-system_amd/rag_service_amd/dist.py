@@ -1,0 +1,79 @@
+"""One-process-per-GPU coordination for a row-sharded corpus.
+
+The data path (candidate exchange) is RCCL inside librag_retrieval.so (ncclAllGather over xGMI). This
+module is only the control plane around it: rank/world from the torchrun environment, broadcasting the
+RCCL unique id, and reductions of host-side timings. It uses a CPU `gloo` process group so it never
+creates a second GPU communicator.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import Optional, Tuple
+
+import numpy as np
+
+
+def env_rank_world() -> Tuple[int, int, int]:
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def shard_rows(n: int, world: int, g: int) -> Tuple[int, int]:
+    """Rows [begin, end) of global shard g (same formula as rr_api.cpp shard_range)."""
+    per = (n + world - 1) // world
+    b = min(n, g * per)
+    return b, min(n, b + per)
+
+
+def init_control_plane(world: int, rank: int, timeout_s: int = 300):
+    """gloo process group from MASTER_ADDR/PORT (torchrun env); None when world == 1."""
+    if world <= 1:
+        return None
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s))
+    return dist
+
+
+def broadcast_bytes(dist, payload: Optional[bytes], src: int = 0) -> bytes:
+    obj = [payload]
+    dist.broadcast_object_list(obj, src=src)
+    return obj[0]
+
+
+def max_over_ranks(dist, x: float) -> float:
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(dist) -> None:
+    if dist is not None:
+        dist.barrier()
+
+
+def merge_shard_topk(scores: np.ndarray, idx: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:
+    """Host-side merge of per-shard candidates [G, b, kk] -> [b, k] by (score desc, index asc).
+
+    The device pipeline does this merge on the GPU after the all-gather; this host form serves callers
+    that gather candidates themselves and documents the rule (used by the multi-process CPU tests).
+    """
+    G, b, kk = scores.shape
+    s = scores.transpose(1, 0, 2).reshape(b, G * kk)
+    i = idx.transpose(1, 0, 2).reshape(b, G * kk)
+    out_s = np.full((b, k), -np.inf, dtype=np.float32)
+    out_i = np.full((b, k), -1, dtype=np.int64)
+    for r in range(b):
+        valid = i[r] >= 0
+        order = np.lexsort((i[r][valid], -s[r][valid]))[:k]
+        out_s[r, :order.size] = s[r][valid][order]
+        out_i[r, :order.size] = i[r][valid][order]
+    return out_s, out_i

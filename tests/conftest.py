@@ -1,0 +1,52 @@
+"""Shared pytest setup: import paths, the `gpu` marker, fixtures for goldens and the HIP library."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG_DIR = os.path.join(REPO, "rag-serving-system_amd")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+for p in (REPO, PKG_DIR):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels through the C-ABI)")
+    config.addinivalue_line("markers", "big: full-size (1M-row) parity cases")
+
+
+@pytest.fixture(scope="session")
+def golden_data():
+    return dict(np.load(os.path.join(GOLDEN, "golden_data.npz")))
+
+
+@pytest.fixture(scope="session")
+def golden_synth():
+    return dict(np.load(os.path.join(GOLDEN, "golden_synth.npz")))
+
+
+@pytest.fixture(scope="session")
+def golden_edges():
+    with open(os.path.join(GOLDEN, "golden_edge_cases.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def short_facts():
+    return np.load(os.path.join(GOLDEN, "data", "short_facts_embeddings.npy"))
+
+
+@pytest.fixture(scope="session")
+def squad():
+    return np.load(os.path.join(GOLDEN, "data", "squad_embeddings.npy"))
+
+
+@pytest.fixture(scope="session")
+def hip():
+    """The loaded C-ABI library; GPU tests fail loudly (not skip) if it is missing."""
+    from rag_service_amd import _lib
+    return _lib.load_library()

@@ -1,0 +1,297 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference's golden vectors and the oracle.
+
+Golden vectors come from the reference retrievers themselves (tests/golden/make_golden.py). Sizes the
+oracle handles in seconds are compared directly; the 1M-row cases compare against the reference's
+committed outputs, plus size-independent properties (self-retrieval, bf16/fp32 agreement on the
+exact-integer corpus, determinism).
+"""
+import numpy as np
+import pytest
+
+from oracle import synth
+from oracle.retriever_oracle import canonical_topk, exact_scores
+from parity_helpers import check_topk
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def Index(hip):
+    from rag_service_amd import Index as _Index
+    return _Index
+
+
+_cache = {}
+
+
+def get_index(Index, key, corpus, dtype="fp32", metric="cosine"):
+    k = (key, dtype, metric)
+    if k not in _cache:
+        ix = Index(dtype=dtype, metric=metric)
+        ix.load(corpus)
+        _cache[k] = ix
+    return _cache[k]
+
+
+GOLDEN_CASES = [
+    ("sf_self_k1", "sf", "sf_self", 1), ("sf_self_k5", "sf", "sf_self", 5), ("sf_self_k10", "sf", "sf_self", 10),
+    ("sf_rand_k1", "sf", "rand", 1), ("sf_rand_k5", "sf", "rand", 5), ("sf_rand_k10", "sf", "rand", 10),
+    ("sf_rand_k100", "sf", "rand", 100),
+    ("sq_rand_k2", "sq", "rand", 2), ("sq_rand_k5", "sq", "rand", 5), ("sq_rand_k10", "sq", "rand", 10),
+    ("sq_rand_k32", "sq", "rand", 32), ("sq_rand_k40", "sq", "rand", 40),
+    ("sq_self_k5", "sq", "sq_self", 5), ("sq_scaled_k10", "sq", "scaled", 10),
+]
+
+
+def _case_inputs(corpus_key, q_key, short_facts, squad, golden_data):
+    corpus = short_facts if corpus_key == "sf" else squad
+    queries = {"sf_self": short_facts, "sq_self": squad[:64], "rand": golden_data["rand_queries"],
+               "scaled": golden_data["scaled_queries"]}[q_key]
+    return corpus, queries
+
+
+@pytest.mark.parametrize("name,corpus_key,q_key,k", GOLDEN_CASES)
+@pytest.mark.parametrize("flavour", ["simple", "cupy"])
+def test_golden_reference_data(Index, golden_data, short_facts, squad, name, corpus_key, q_key, k, flavour):
+    corpus, queries = _case_inputs(corpus_key, q_key, short_facts, squad, golden_data)
+    metric = "dot" if flavour == "simple" else "cosine"
+    ix = get_index(Index, corpus_key, corpus, "fp32", metric)
+    ref_idx = golden_data[f"{name}_{flavour}_idx"]
+    kk = ref_idx.shape[1]
+    scores, idx = ix.search(queries, kk)
+    exact_rows, near = check_topk(idx, scores, ref_idx, corpus, queries, metric)
+    assert exact_rows + near == queries.shape[0]
+    if float(golden_data[f"{name}_{flavour}_gap"]) > 1e-5:
+        assert near == 0
+
+
+def test_retriever_classes_match_reference(hip, golden_data, squad):
+    from rag_service_amd.core.retriever import HipRetriever, HipSimpleRetriever
+    docs = list(range(squad.shape[0]))
+    q = golden_data["rand_queries"]
+    cupy = HipRetriever(doc_embeddings=squad, documents=docs)
+    simple = HipSimpleRetriever(doc_embeddings=squad, documents=docs)
+    got_c = cupy.batch_retrieve(q, [10] * q.shape[0])
+    got_s = simple.batch_retrieve(q, [10] * q.shape[0])
+    assert got_c == golden_data["sq_rand_k10_cupy_idx"].tolist()
+    assert got_s == golden_data["sq_rand_k10_simple_idx"].tolist()
+    assert cupy.retrieve(q[3], 10) == golden_data["sq_rand_k10_cupy_idx"][3].tolist()
+    assert simple.retrieve(q[3:4], 10) == golden_data["sq_rand_k10_simple_idx"][3].tolist()
+
+
+def test_edge_cases_match_reference(hip, golden_edges, short_facts):
+    from rag_service_amd.core.retriever import HipRetriever, HipSimpleRetriever
+    n, d = short_facts.shape
+    docs = list(range(n))
+    rets = {"cupy": HipRetriever(short_facts, docs), "simple": HipSimpleRetriever(short_facts, docs)}
+    rng = np.random.default_rng(golden_edges["seed"])
+    q4 = rng.standard_normal((4, d)).astype(np.float32)
+    q4 /= np.linalg.norm(q4, axis=1, keepdims=True)
+    c = golden_edges["cases"]
+    batch_inputs = {
+        "mixed_ks": (q4, [3, 0, -1, 7]), "k_gt_n": (q4, [n + 50, 2, n, 1]), "all_nonpositive": (q4, [0, -3, 0, -1]),
+        "float64_queries": (q4.astype(np.float64), [5] * 4), "wrong_dim": (q4[:, :d - 8], [5] * 4),
+        "np_int64_ks": (q4, [np.int64(5)] * 4), "len_mismatch": (q4, [5, 5, 5]), "empty_batch": (q4[:0], []),
+        "one_d_batch": (q4[0], [5]),
+    }
+    for case, (q, ks) in batch_inputs.items():
+        for flav, r in rets.items():
+            assert r.batch_retrieve(q, ks) == c[case][flav], (case, flav)
+    single_inputs = {
+        "retrieve_1d": (q4[0], 3), "retrieve_1xd": (q4[:1], 3), "retrieve_k0": (q4[0], 0),
+        "retrieve_kneg": (q4[0], -2), "retrieve_k_gt_n": (q4[0], n + 3), "retrieve_2xd": (q4[:2], 3),
+        "retrieve_wrong_dim": (q4[0, :d - 8], 3), "retrieve_np_int64_k": (q4[0], np.int64(3)),
+        "retrieve_float_k": (q4[0], 2.5), "retrieve_float64": (q4[0].astype(np.float64), 4),
+    }
+    for case, (q, k) in single_inputs.items():
+        for flav, r in rets.items():
+            assert r.retrieve(q, k) == c[case][flav], (case, flav)
+    with pytest.raises(AttributeError):
+        rets["cupy"].batch_retrieve(q4.tolist(), [5] * 4)
+    assert c["cupy_list_input"] == "AttributeError"
+
+
+# ---- synthetic corpora (64k rows: reference outputs committed; oracle-checkable) ----------------------
+@pytest.fixture(scope="module")
+def f2_small(golden_synth):
+    seed, qseed, _, n = [int(x) for x in golden_synth["meta"]]
+    return synth.exact_int_rows(seed, 0, n, 1024), synth.exact_int_queries(qseed, 32, 1024)
+
+
+@pytest.fixture(scope="module")
+def f3_small(golden_synth):
+    seed, _, qseed, n = [int(x) for x in golden_synth["meta"]]
+    return synth.unit_norm_gaussian(seed, n, 1024), synth.unit_norm_gaussian(qseed, 32, 1024)
+
+
+def test_device_generator_matches_numpy(Index, golden_synth):
+    ix = Index(dtype="fp32", metric="dot")
+    ix.fill_synthetic(0, 1234, 4099, 1024)
+    assert np.array_equal(ix.read_rows(0, 4099), synth.exact_int_rows(1234, 0, 4099, 1024))
+    ix2 = Index(dtype="fp32", metric="dot")
+    ix2.fill_synthetic(1, 77, 300, 1024)
+    ref = synth.irwin_hall_unnormalised(77, 0, 300, 1024)
+    ref /= np.linalg.norm(ref, axis=1, keepdims=True)
+    np.testing.assert_allclose(ix2.read_rows(0, 300), ref, rtol=0, atol=2e-7)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_exact_integer_corpus_bit_exact(Index, golden_synth, f2_small, dtype):
+    """F2: every dot is exact in fp32, so scores must equal the fp64 values bit-for-bit and the order is
+    the canonical (score desc, index asc); where the reference had no ties its order matches too."""
+    corpus, q = f2_small
+    ix = get_index(Index, "f2_small", corpus, dtype, "dot")
+    scores, idx = ix.search(q, 10)
+    val, cidx = canonical_topk(exact_scores(corpus, q, "dot"), 10)
+    assert np.array_equal(scores.astype(np.float64), val)
+    assert np.array_equal(idx, cidx)
+    ref = golden_synth["f2_64k_k10_simple_idx"]
+    ex = exact_scores(corpus, q, "dot")
+    for i in range(q.shape[0]):
+        s = np.sort(ex[i])[::-1][:11]
+        if np.all(np.diff(s) != 0):
+            assert np.array_equal(idx[i], ref[i])
+
+
+@pytest.mark.parametrize("metric,flav", [("dot", "simple"), ("cosine", "cupy")])
+def test_unit_norm_corpus_fp32(Index, golden_synth, f3_small, metric, flav):
+    corpus, q = f3_small
+    ix = get_index(Index, "f3_small", corpus, "fp32", metric)
+    scores, idx = ix.search(q, 10)
+    check_topk(idx, scores, golden_synth[f"f3_64k_k10_{flav}_idx"], corpus, q, metric)
+
+
+@pytest.mark.parametrize("metric,flav", [("dot", "simple"), ("cosine", "cupy")])
+def test_unit_norm_corpus_bf16(Index, golden_synth, f3_small, metric, flav):
+    corpus, q = f3_small
+    ix = get_index(Index, "f3_small", corpus, "bf16", metric)
+    rounded = synth.bf16_round(corpus)
+    assert np.array_equal(ix.read_rows(0, 64), rounded[:64])
+    scores, idx = ix.search(q, 10)
+    check_topk(idx, scores, golden_synth[f"f3bf_64k_k10_{flav}_idx"], rounded, q, metric)
+
+
+# ---- kernel edge cases against the oracle's canonical top-k -----------------------------------------
+SHAPES = [  # (n, d, b, k)
+    (1, 64, 1, 1), (31, 64, 3, 5), (33, 128, 32, 4), (100, 1024, 33, 8), (1000, 1024, 70, 17),
+    (4097, 256, 5, 32), (5000, 128, 2, 33), (777, 64, 9, 64), (50, 128, 4, 80), (20000, 1024, 32, 16),
+]
+
+
+@pytest.mark.parametrize("n,d,b,k", SHAPES)
+@pytest.mark.parametrize("metric", ["dot", "cosine"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_shapes_against_oracle(Index, n, d, b, k, metric, dtype):
+    if dtype == "bf16" and d % 128:
+        pytest.skip("bf16 path needs d % 128 == 0")
+    rng = np.random.default_rng(n * 31 + d + b + k)
+    corpus = rng.standard_normal((n, d)).astype(np.float32) * rng.uniform(0.5, 2, size=(n, 1)).astype(np.float32)
+    q = rng.standard_normal((b, d)).astype(np.float32)
+    if dtype == "bf16":
+        corpus = synth.bf16_round(corpus)
+    ix = Index(dtype=dtype, metric=metric)
+    ix.load(corpus)
+    scores, idx = ix.search(q, k)
+    _, cidx = canonical_topk(exact_scores(corpus, q, metric), k)
+    tol = 1e-3 * (np.sqrt(d) if metric == "dot" else 1.0)
+    check_topk(idx, scores, cidx, corpus, q, metric, near_tie=1e-5 * np.sqrt(d), score_tol=tol)
+    if k > n:
+        assert np.all(idx[:, n:] == -1) and np.all(np.isneginf(scores[:, n:]))
+
+
+def test_staged_api_and_determinism(Index, squad, golden_data):
+    ix = get_index(Index, "sq", squad, "fp32", "cosine")
+    q = golden_data["rand_queries"]
+    ix.set_queries(q)
+    ix.search_staged(10)
+    s1, i1 = ix.fetch()
+    for _ in range(3):
+        ix.search_staged(10)
+    s2, i2 = ix.fetch()
+    assert np.array_equal(i1, i2) and np.array_equal(s1, s2)
+    s3, i3 = ix.search(q, 10)
+    assert np.array_equal(i1, i3)
+
+
+def test_device_pointer_queries(Index, squad, golden_data):
+    torch = pytest.importorskip("torch")
+    ix = get_index(Index, "sq", squad, "fp32", "cosine")
+    q = golden_data["rand_queries"]
+    t = torch.from_numpy(q).to("cuda:0")
+    torch.cuda.synchronize()
+    ix.set_queries_device(t.data_ptr(), q.shape[0], q.shape[1])
+    ix.search_staged(5)
+    s, i = ix.fetch()
+    s2, i2 = ix.search(q, 5)
+    assert np.array_equal(i, i2)
+
+
+def test_kernel_timing(Index, squad, golden_data):
+    ix = get_index(Index, "sq", squad, "fp32", "cosine")
+    ix.set_timing(True)
+    ix.kernel_time(reset=True)
+    ix.search(golden_data["rand_queries"], 5)
+    ms, n = ix.kernel_time(reset=True)
+    ix.set_timing(False)
+    assert n == 1 and ms > 0
+
+
+def test_errors_are_reported(Index, hip):
+    from rag_service_amd import HipRetrievalError
+    ix = Index(dtype="fp32", metric="dot")
+    with pytest.raises(HipRetrievalError):
+        ix.search(np.zeros((1, 64), np.float32), 1)       # no corpus yet
+    with pytest.raises(HipRetrievalError):
+        ix.load(np.zeros((10, 65), np.float32))            # d not a multiple of 64
+    ix.load(np.ones((10, 64), np.float32))
+    with pytest.raises(HipRetrievalError):
+        ix.search(np.zeros((1, 128), np.float32), 1)      # wrong d
+    with pytest.raises(HipRetrievalError):
+        ix.search(np.zeros((1, 64), np.float32), 0)       # k < 1
+
+
+# ---- full size (1M rows) --------------------------------------------------------------------------
+@pytest.mark.big
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_1m_exact_integer_against_reference(Index, golden_synth, dtype):
+    if "f2_1m_k10_simple_idx" not in golden_synth:
+        pytest.skip("1M goldens not generated")
+    q = synth.exact_int_queries(99, 32, 1024)
+    ix = Index(dtype=dtype, metric="dot")
+    ix.fill_synthetic(0, 1234, 1_000_000, 1024)            # bit-identical to synth.exact_int_rows
+    for k in (5, 10):
+        scores, idx = ix.search(q, k)
+        ref = golden_synth[f"f2_1m_k{k}_simple_idx"]
+        ref_s = golden_synth[f"f2_1m_k{k}_simple_score"]
+        # exact integer arithmetic: scores are bit-exact; indices equal the reference wherever it is
+        # tie-free, and otherwise equal the canonical order of the reference's (exact) scores
+        assert np.array_equal(np.sort(scores, axis=1), np.sort(ref_s.astype(np.float32), axis=1))
+        assert np.array_equal(scores.astype(np.float64), ref_s)
+        same = np.all(idx == ref, axis=1)
+        for i in np.where(~same)[0]:
+            assert len(set(ref_s[i])) < k, f"query {i} differs without ties"
+
+
+@pytest.mark.big
+def test_1m_unit_norm_against_reference(Index, golden_synth):
+    if "f3_1m_k10_simple_idx" not in golden_synth:
+        pytest.skip("1M goldens not generated")
+    corpus = synth.unit_norm_gaussian(1234, 1_000_000, 1024)
+    q = synth.unit_norm_gaussian(5678, 32, 1024)
+    for metric, flav in (("dot", "simple"), ("cosine", "cupy")):
+        ix = Index(dtype="fp32", metric=metric)
+        ix.load(corpus)
+        for k in (5, 10):
+            scores, idx = ix.search(q, k)
+            check_topk(idx, scores, golden_synth[f"f3_1m_k{k}_{flav}_idx"], corpus, q, metric)
+        # property: self-retrieval — every corpus row finds itself first
+        rows = np.arange(0, 1_000_000, 31250)[:32]
+        _, sidx = ix.search(corpus[rows], 1)
+        assert np.array_equal(sidx[:, 0], rows)
+        ix.close()
+    bf = synth.bf16_round(corpus)
+    del corpus
+    ix = Index(dtype="bf16", metric="dot")
+    ix.load(bf)
+    scores, idx = ix.search(q, 10)
+    check_topk(idx, scores, golden_synth["f3bf_1m_k10_simple_idx"], bf, q, "dot")
