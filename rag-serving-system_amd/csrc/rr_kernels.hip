@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
+#include <type_traits>
 #include "rr_internal.h"
 
 namespace rr {
@@ -25,6 +26,42 @@ namespace rr {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// 16-byte corpus loads of one pipeline group (U loads at 32-byte stride).
+// LM 0: plain loads, waits placed by hipcc.
+// LM 1: inline-asm global_load_dwordx4, waits counted by hand (wait_group): hipcc does not see these
+//       loads, so it cannot drain the prefetch queue with its own conservative vmcnt(0) at the loop
+//       head. Any vector-memory op hipcc adds only makes a counted wait stricter, never looser.
+// LM 2: as LM 1 with the non-temporal hint (`nt`): the corpus is streamed once per search.
+template <int LM, int U>
+__device__ __forceinline__ void load_group(u32x4 (&dst)[U], const u32x4* src) {
+  if constexpr (LM == 0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) dst[u] = src[2 * u];
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (LM == 1)
+        asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(dst[u]) : "v"(src), "i"(32 * u));
+      else
+        asm volatile("global_load_dwordx4 %0, %1, off offset:%2 nt" : "=v"(dst[u]) : "v"(src), "i"(32 * u));
+    }
+  }
+}
+// Before the MFMAs read dst[u] of the OLDEST group: `younger` groups of U loads were issued after it.
+template <int LM, int U, int N>
+__device__ __forceinline__ void wait_vm(u32x4& v) {
+  if constexpr (LM != 0) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(v) : "i"(N));
+}
 
 // ------------------------------------------------------------------------------------------------
 // keys
@@ -90,9 +127,9 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
 // one wave's ds_read_b128 covers 1 KiB contiguous: conflict-free.
 // MODE 0: per-lane top-KT, merged per workgroup -> cand[blockIdx][32][KT]
 // MODE 1: every key written to keys[q][doc] (the k > RR_FUSED_KMAX path)
-template <int DT, int KT, bool COS, int MODE>
+template <int DT, int KT, bool COS, int MODE, int NB = 2, int LM = 0, int AS = 0>
 __global__ __launch_bounds__(kThreads) void fused_score_kernel(
-    const uint4* __restrict__ corpus, const float* __restrict__ norms, const float* __restrict__ queries,
+    const u32x4* __restrict__ corpus, const float* __restrict__ norms, const float* __restrict__ queries,
     int64_t n, int d, int b, uint32_t idx_base, uint64_t* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int U = kGroupChunks;
@@ -157,23 +194,40 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
 
   const bool qvalid = r < b;
   const float qn = COS ? qnorm[r] : 0.f;
-  const int64_t ntiles = (n + kTileDocs - 1) / kTileDocs;
-  const int64_t nwave = (int64_t)gridDim.x * kWaves;
-  const int64_t rstride = DT == 0 ? (int64_t)(d >> 2) : (int64_t)(d >> 3);  // uint4 per corpus row
+  const int64_t rstride = DT == 0 ? (int64_t)(d >> 2) : (int64_t)(d >> 3);  // 16-byte units per corpus row
 
   TopK<KT> tk;
   tk.init();
 
-  int64_t tile = (int64_t)blockIdx.x * kWaves + wid;
-  if (tile < ntiles) {
-    auto rowp = [&](int64_t t) -> const uint4* {
-      int64_t row = t * kTileDocs + r;
-      row = row < n ? row : n - 1;
+  // Work split over the grid's waves. A wave walks 32-row tiles starting at row `base0`, `bstep`
+  // rows apart, until `limit` (exclusive; also the bound for valid documents).
+  //   AS 0: tiles dealt round-robin over all waves.
+  //   AS 1: each wave owns one contiguous, balanced row range (equal bytes per wave, no tail of
+  //         whole tiles); the last tile of a range is partial and its loads stay inside the range.
+  const int64_t nwave = (int64_t)gridDim.x * kWaves;
+  const int64_t gw = (int64_t)blockIdx.x * kWaves + wid;
+  int64_t base0, limit, bstep;
+  if constexpr (AS == 0) {
+    base0 = gw * kTileDocs;
+    limit = n;
+    bstep = nwave * kTileDocs;
+  } else {
+    const int64_t per = n / nwave, rem = n % nwave;
+    base0 = gw * per + (gw < rem ? gw : rem);
+    limit = base0 + per + (gw < rem ? 1 : 0);
+    bstep = kTileDocs;
+  }
+  if (base0 < limit) {
+    auto rowp = [&](int64_t base) -> const u32x4* {
+      int64_t row = base + r;
+      row = row < limit ? row : limit - 1;
       return corpus + row * rstride + h;
     };
-    auto compute = [&](const uint4 (&buf)[U], int g, f32x16& acc) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
+    auto compute = [&](u32x4 (&buf)[U], int g, f32x16& acc) {
+      static_for<0, U>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        // oldest group in flight: (NB-1) younger groups of U loads were issued after it
+        wait_vm<LM, U, (NB - 1) * U + (U - 1 - u)>(buf[u]);
         const int slot = (2 * (g * U + u) + h) * kQSlots + r;
         if constexpr (DT == 0) {
           const f32x4 a = __builtin_bit_cast(f32x4, buf[u]);
@@ -189,85 +243,90 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qh, acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, ql, acc, 0, 0, 0);
         }
-      }
+      });
     };
-    // doc norms of the current tile (cosine): lane holds docs 8*gq + 4h + {0..3}, gq = 0..3
-    f32x4 nrm[4];
-    auto load_norms = [&](int64_t t) {
+    // doc norms of the current tile (cosine), fetched through the SCALAR cache at tile start: 32
+    // wave-uniform floats (s_load, counted on lgkmcnt), so no vector-memory op joins the hand-counted
+    // corpus prefetch queue. Lane half h then picks docs 8*gq + 4h + {0..3}.
+    float sn[kTileDocs];
+    auto load_norms = [&](int64_t base) {
       if constexpr (COS) {
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+        const float* np = norms + (int64_t)(((uint64_t)hi << 32) | lo);
 #pragma unroll
-        for (int gq = 0; gq < 4; ++gq) nrm[gq] = *(const f32x4*)(norms + t * kTileDocs + 8 * gq + 4 * h);
+        for (int i = 0; i < kTileDocs; ++i) sn[i] = np[i];
       }
     };
-    auto epilogue = [&](int64_t t, const f32x16& acc) {
+    auto epilogue = [&](int64_t base, const f32x16& acc) {
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int dl = (v & 3) + 8 * (v >> 2) + 4 * h;   // C/D row map of the 32x32 MFMA
-        const int64_t doc = t * kTileDocs + dl;
+        const int64_t doc = base + dl;
         float s = acc[v];
         if constexpr (COS) {
           // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
-          const float nd = nrm[v >> 2][v & 3];
+          const int j = 8 * (v >> 2) + (v & 3);
+          const float nd = h ? sn[j + 4] : sn[j];
           s = s / (qn * nd + 1e-8f);
           s = fminf(fmaxf(s, -1.0f), 1.0f);
         }
         if constexpr (MODE == 0) {
-          if (qvalid && doc < n) {
+          if (qvalid && doc < limit) {
             const uint64_t key = make_key(s, idx_base + (uint32_t)doc);
             if (key > tk.last()) tk.insert(key);
           }
         } else {
-          if (qvalid && doc < n) out[(size_t)r * (size_t)n + (size_t)doc] = make_key(s, idx_base + (uint32_t)doc);
+          if (qvalid && doc < limit) out[(size_t)r * (size_t)n + (size_t)doc] = make_key(s, idx_base + (uint32_t)doc);
         }
       }
     };
 
-    uint4 bufA[U], bufB[U];
+    // Software pipeline: the load cursor runs NB-1 groups (NB-1 x U x 16 B per lane) ahead of the
+    // compute cursor; both walk this wave's tiles in order, so the prefetch crosses tile boundaries.
+    // Past the wave's last tile the loads re-read a valid address instead of branching around them.
+    u32x4 buf[NB][U];
     f32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    const uint4* p = rowp(tile);
-    int g = 0;
-    load_norms(tile);
-#pragma unroll
-    for (int u = 0; u < U; ++u) bufA[u] = p[2 * u];
-
-    // One pipeline step: prefetch the next group (possibly the first group of the wave's next tile)
-    // into `nxt` while the MFMAs consume `cur`. Addresses stay in bounds (the final prefetch re-reads
-    // the current group), so no load sits under a branch.
-    bool more = true;
-    auto step = [&](const uint4 (&cur)[U], uint4 (&nxt)[U]) {
-      int ng = g + 1;
-      int64_t ntile = tile;
-      const uint4* np = p;
-      if (ng == ngroup) {
-        ng = 0;
-        ntile = tile + nwave;
-        np = ntile < ntiles ? rowp(ntile) : p;
+    int64_t cbase = base0, lrow = base0;
+    int cg = 0, lg = 0;
+    const u32x4* lptr = rowp(base0);
+    const u32x4* const safe = lptr;
+    auto issue = [&](u32x4 (&dst)[U]) {
+      const u32x4* src = lrow < limit ? lptr + 2 * U * lg : safe;
+      load_group<LM, U>(dst, src);
+      if (++lg == ngroup) {
+        lg = 0;
+        lrow += bstep;
+        if (lrow < limit) lptr = rowp(lrow);
       }
-      more = ntile < ntiles;
-      const uint4* src = more ? np + 2 * U * ng : p + 2 * U * g;
-#pragma unroll
-      for (int u = 0; u < U; ++u) nxt[u] = src[2 * u];
-      // keep the prefetch ahead of the MFMAs (hipcc otherwise sinks the loads below them)
-      __builtin_amdgcn_sched_barrier(0);
-      compute(cur, g, acc);
-      if (g == ngroup - 1) {
-        epilogue(tile, acc);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-        if (more) load_norms(ntile);
-      }
-      tile = ntile;
-      g = ng;
-      p = np;
     };
+    auto consume = [&](u32x4 (&src)[U]) -> bool {
+      compute(src, cg, acc);
+      if (++cg < ngroup) return true;
+      epilogue(cbase, acc);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+      cg = 0;
+      cbase += bstep;
+      if (cbase >= limit) return false;
+      load_norms(cbase);
+      return true;
+    };
+    load_norms(base0);
+#pragma unroll
+    for (int s = 0; s < NB - 1; ++s) issue(buf[s]);
     for (;;) {
-      step(bufA, bufB);
-      if (!more) break;
-      step(bufB, bufA);
-      if (!more) break;
+#pragma unroll
+      for (int s = 0; s < NB; ++s) {
+        issue(buf[(s + NB - 1) % NB]);
+        // keep the prefetch ahead of the MFMAs (hipcc otherwise sinks the loads below them)
+        __builtin_amdgcn_sched_barrier(0);
+        if (!consume(buf[s])) goto wave_done;
+      }
     }
+  wave_done:;
   }
 
   if constexpr (MODE == 0) {
@@ -473,14 +532,19 @@ size_t fused_lds_bytes(int d, int kt, int dtype) {
   return a > merge ? a : merge;
 }
 
-template <int DT, int KT, bool COS, int MODE>
-static hipError_t launch_fused_t(int grid, const void* corpus, const float* norms, const float* queries,
-                                 int64_t n, int d, int b, uint32_t idx_base, uint64_t* out, hipStream_t s) {
+// Pipeline depth and load form of the shipped kernel (chosen by tools/kbench.hip A/B runs on MI355X).
+constexpr int kPipeNB = 2;
+constexpr int kLoadMode = 1;
+constexpr int kAssign = 1;
+
+template <int DT, int KT, bool COS, int MODE, int NB = kPipeNB, int LM = kLoadMode, int AS = kAssign>
+hipError_t launch_fused_t(int grid, const void* corpus, const float* norms, const float* queries,
+                          int64_t n, int d, int b, uint32_t idx_base, uint64_t* out, hipStream_t s) {
   const size_t lds = fused_lds_bytes(d, MODE == 0 ? KT : 1, DT);
-  auto kern = fused_score_kernel<DT, KT, COS, MODE>;
+  auto kern = fused_score_kernel<DT, KT, COS, MODE, NB, LM, AS>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, (const uint4*)corpus, norms, queries, n, d, b,
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, (const u32x4*)corpus, norms, queries, n, d, b,
                      idx_base, out);
   return hipGetLastError();
 }

@@ -48,5 +48,12 @@ def squad():
 @pytest.fixture(scope="session")
 def hip():
     """The loaded C-ABI library; GPU tests fail loudly (not skip) if it is missing."""
+    # torch (plumbing for the device-pointer test) ships its own libamdhip64.so.7; let it initialise the
+    # runtime first so that both share one HIP runtime in this process (same SONAME).
+    try:
+        import torch
+        torch.cuda.is_available()
+    except Exception:
+        pass
     from rag_service_amd import _lib
     return _lib.load_library()
