@@ -62,6 +62,32 @@ template <int LM, int U, int N>
 __device__ __forceinline__ void wait_vm(u32x4& v) {
   if constexpr (LM != 0) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(v) : "i"(N));
 }
+// Drain of the corpus pipeline: vmcnt(0) in the first statement, and every buffer named as a
+// read-write operand of that or a later statement, so each in-flight destination stays allocated
+// until the loads have landed.
+#define RR_B8(s, o) "+v"(b[s][o + 0]), "+v"(b[s][o + 1]), "+v"(b[s][o + 2]), "+v"(b[s][o + 3]), \
+                    "+v"(b[s][o + 4]), "+v"(b[s][o + 5]), "+v"(b[s][o + 6]), "+v"(b[s][o + 7])
+#define RR_B4(s, o) "+v"(b[s][o + 0]), "+v"(b[s][o + 1]), "+v"(b[s][o + 2]), "+v"(b[s][o + 3])
+#define RR_KEEP(s)                                                              \
+  if constexpr (U == 4) asm volatile("" : RR_B4(s, 0));                         \
+  else if constexpr (U == 8) asm volatile("" : RR_B8(s, 0));                    \
+  else { asm volatile("" : RR_B8(s, 0)); asm volatile("" : RR_B8(s, 8)); }
+template <int LM, int NB, int U>
+__device__ __forceinline__ void drain_group_loads(u32x4 (&b)[NB][U]) {
+  if constexpr (LM != 0) {
+    static_assert((U == 4 || U == 8 || U == 16) && NB >= 2 && NB <= 4, "drain written for U 4/8/16, NB 2-4");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (the wait above is ordered before these by `volatile`; the operands keep every buffer live up
+    // to here, i.e. past the wait)
+    RR_KEEP(0)
+    RR_KEEP(1)
+    if constexpr (NB > 2) { RR_KEEP(2) }
+    if constexpr (NB > 3) { RR_KEEP(3) }
+  }
+}
+#undef RR_KEEP
+#undef RR_B4
+#undef RR_B8
 
 // ------------------------------------------------------------------------------------------------
 // keys
@@ -127,12 +153,11 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
 // one wave's ds_read_b128 covers 1 KiB contiguous: conflict-free.
 // MODE 0: per-lane top-KT, merged per workgroup -> cand[blockIdx][32][KT]
 // MODE 1: every key written to keys[q][doc] (the k > RR_FUSED_KMAX path)
-template <int DT, int KT, bool COS, int MODE, int NB = 2, int LM = 0, int AS = 0>
+template <int DT, int KT, bool COS, int MODE, int NB = 2, int LM = 0, int AS = 0, int DBG = 0, int U = kGroupChunks>
 __global__ __launch_bounds__(kThreads) void fused_score_kernel(
     const u32x4* __restrict__ corpus, const float* __restrict__ norms, const float* __restrict__ queries,
-    int64_t n, int d, int b, uint32_t idx_base, uint64_t* __restrict__ out) {
+    int64_t n, int d, int b, uint32_t idx_base, uint64_t* __restrict__ out, int seg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int U = kGroupChunks;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
 
@@ -141,12 +166,18 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
   const int ngroup = nchunk / U;
   const size_t qimg_bytes = (size_t)nchunk * 2 * kQSlots * 16;  // per image
   float* qnorm = (float*)(smem + (DT == 0 ? qimg_bytes : 2 * qimg_bytes));
+  // Cosine: each wave keeps the norms of a `seg`-row stretch of its rows in LDS (its own segment of
+  // the region after the query image), refilled when its tiles walk past the end. The refill is
+  // ordinary loads; per refill hipcc drains the vector-memory queue once (a few times per launch).
+  float* const wseg = qnorm + kQSlots + wid * seg;
+  int64_t seg_lo = INT64_MIN / 2;
 
   // ---- stage the queries into LDS (zero rows for unused slots) --------------------------------
   if constexpr (DT == 0) {
     f32x4* Q4 = (f32x4*)smem;
+    // query slot fastest across lanes: consecutive lanes write consecutive 16-byte LDS slots
     for (int e = tid; e < kQSlots * d4; e += kThreads) {
-      const int q = e / d4, c4 = e - q * d4;   // c4 = 2 * chunk + half
+      const int q = e & (kQSlots - 1), c4 = e / kQSlots;   // c4 = 2 * chunk + half
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (q < b) v = ((const f32x4*)queries)[(size_t)q * d4 + c4];
       Q4[c4 * kQSlots + q] = v;
@@ -156,7 +187,7 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
     bf16x8* Qlo = (bf16x8*)(smem + qimg_bytes);
     const int d8 = d >> 3;                       // 8-element groups per row = 2 * chunk + half
     for (int e = tid; e < kQSlots * d8; e += kThreads) {
-      const int q = e / d8, c8 = e - q * d8;
+      const int q = e & (kQSlots - 1), c8 = e / kQSlots;
       bf16x8 hi, lo;
       if (q < b) {
         const f32x4* src = (const f32x4*)(queries + (size_t)q * d + c8 * 8);
@@ -229,7 +260,9 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
         // oldest group in flight: (NB-1) younger groups of U loads were issued after it
         wait_vm<LM, U, (NB - 1) * U + (U - 1 - u)>(buf[u]);
         const int slot = (2 * (g * U + u) + h) * kQSlots + r;
-        if constexpr (DT == 0) {
+        if constexpr (DBG == 1) {   // diagnostic: no MFMA, keep the loaded bytes live
+          acc[u & 15] += __builtin_bit_cast(f32x4, buf[u]).x;
+        } else if constexpr (DT == 0) {
           const f32x4 a = __builtin_bit_cast(f32x4, buf[u]);
           const f32x4 q = ((const f32x4*)smem)[slot];
           acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, q.x, acc, 0, 0, 0);
@@ -245,20 +278,24 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
         }
       });
     };
-    // doc norms of the current tile (cosine), fetched through the SCALAR cache at tile start: 32
-    // wave-uniform floats (s_load, counted on lgkmcnt), so no vector-memory op joins the hand-counted
-    // corpus prefetch queue. Lane half h then picks docs 8*gq + 4h + {0..3}.
-    float sn[kTileDocs];
-    auto load_norms = [&](int64_t base) {
-      if constexpr (COS) {
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
-        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
-        const float* np = norms + (int64_t)(((uint64_t)hi << 32) | lo);
-#pragma unroll
-        for (int i = 0; i < kTileDocs; ++i) sn[i] = np[i];
-      }
-    };
     auto epilogue = [&](int64_t base, const f32x16& acc) {
+      if constexpr (DBG == 2) {   // diagnostic: no epilogue, keep acc live
+        asm volatile("" :: "v"(acc[0]), "v"(acc[15]));
+        return;
+      }
+      if constexpr (COS) {
+        if (base < seg_lo || base + kTileDocs > seg_lo + seg) {   // wave-uniform
+          seg_lo = base;
+#pragma unroll 1
+          for (int i = lane; i < seg; i += 64) {
+            const int64_t row = base + i;
+            wseg[i] = norms[row < limit ? row : limit - 1];
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+      }
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int dl = (v & 3) + 8 * (v >> 2) + 4 * h;   // C/D row map of the 32x32 MFMA
@@ -266,9 +303,8 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
         float s = acc[v];
         if constexpr (COS) {
           // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
-          const int j = 8 * (v >> 2) + (v & 3);
-          const float nd = h ? sn[j + 4] : sn[j];
-          s = s / (qn * nd + 1e-8f);
+          const float nd = wseg[doc - seg_lo];
+          s = s / (qn * nd + 1e-8f);   // IEEE division, as the reference's elementwise kernel
           s = fminf(fmaxf(s, -1.0f), 1.0f);
         }
         if constexpr (MODE == 0) {
@@ -311,10 +347,8 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
       cg = 0;
       cbase += bstep;
       if (cbase >= limit) return false;
-      load_norms(cbase);
       return true;
     };
-    load_norms(base0);
 #pragma unroll
     for (int s = 0; s < NB - 1; ++s) issue(buf[s]);
     for (;;) {
@@ -326,7 +360,11 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
         if (!consume(buf[s])) goto wave_done;
       }
     }
-  wave_done:;
+  wave_done:
+    // The loop leaves prefetches in flight (the dummy loads that keep the hand counts exact). Their
+    // destination registers must stay allocated until they land, or hipcc may hand them to later code
+    // and the late data would overwrite it: one drain that names every buffer as an operand.
+    drain_group_loads<LM, NB, U>(buf);
   }
 
   if constexpr (MODE == 0) {
@@ -360,43 +398,70 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
 // ------------------------------------------------------------------------------------------------
 // merge of candidate lists: in [nlists][32][in_kt] -> top-KT per query slot
 // ------------------------------------------------------------------------------------------------
+// One workgroup per query slot. Every input list is already sorted (descending), so: thread t takes
+// list t (lists beyond 256 are folded in by insertion), each wave extracts its top-KT by KT rounds of a
+// wave-wide max over the lanes' list heads (the winning lane advances its head from LDS; no barrier),
+// and wave 0 merges the 4 per-wave winner lists the same way.
 template <int KT>
-__global__ __launch_bounds__(256) void merge_kernel(const uint64_t* __restrict__ in, int nlists, int in_kt,
-                                                    int b, int k_out, uint64_t* __restrict__ out_keys,
+__global__ __launch_bounds__(256) void merge_kernel(const uint64_t* __restrict__ in, int nlists, int b,
+                                                    int k_out, uint64_t* __restrict__ out_keys,
                                                     float* __restrict__ out_scores,
                                                     int64_t* __restrict__ out_idx) {
   const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  __shared__ uint64_t wmax[4];
-  __shared__ uint64_t res[KT];
+  __shared__ uint64_t L[256][KT];
+  __shared__ uint64_t W[4 * KT];
   TopK<KT> tk;
-  tk.init();
-  const int total = nlists * in_kt;
-  for (int e = tid; e < total; e += 256) {
-    const int l = e / in_kt, i = e - l * in_kt;
-    const uint64_t key = in[((size_t)l * kQSlots + q) * in_kt + i];
-    if (key > tk.last()) tk.insert(key);
+  if (tid < nlists) {
+    const uint64_t* src = in + ((size_t)tid * kQSlots + q) * KT;
+#pragma unroll
+    for (int i = 0; i < KT; ++i) tk.v[i] = src[i];
+  } else {
+    tk.init();
   }
-  for (int rnd = 0; rnd < KT; ++rnd) {
-    const uint64_t head = tk.v[0];
-    const uint64_t m = wave_max_u64(head);
-    if (lane == 0) wmax[wid] = m;
-    __syncthreads();
-    const uint64_t best = umax64(umax64(wmax[0], wmax[1]), umax64(wmax[2], wmax[3]));
-    if (best != 0 && head == best) tk.pop();   // keys are unique: exactly one owner
-    if (tid == 0) res[rnd] = best;
-    __syncthreads();
-  }
-  if (out_keys && tid < KT) out_keys[(size_t)q * KT + tid] = res[tid];
-  if (out_scores && q < b && tid < k_out) {
-    const uint64_t key = res[tid];
-    float s = -INFINITY;
-    int64_t ix = -1;
-    if (key != 0) {
-      s = float_of_ord((uint32_t)(key >> 32));
-      ix = (int64_t)(0xFFFFFFFFu - (uint32_t)key);
+  for (int l = tid + 256; l < nlists; l += 256) {
+    const uint64_t* src = in + ((size_t)l * kQSlots + q) * KT;
+    for (int i = 0; i < KT; ++i) {
+      const uint64_t key = src[i];
+      if (key <= tk.last()) break;            // sorted input: nothing further can enter
+      tk.insert(key);
     }
-    out_scores[(size_t)q * k_out + tid] = s;
-    out_idx[(size_t)q * k_out + tid] = ix;
+  }
+#pragma unroll
+  for (int i = 0; i < KT; ++i) L[tid][i] = tk.v[i];
+  uint64_t head = tk.v[0];
+  int p = 0;
+  for (int rnd = 0; rnd < KT; ++rnd) {
+    const uint64_t m = wave_max_u64(head);
+    if (lane == 0) W[wid * KT + rnd] = m;
+    if (m != 0 && head == m) {                 // keys are unique: exactly one owner advances
+      ++p;
+      head = p < KT ? L[tid][p] : 0;
+    }
+  }
+  __syncthreads();
+  if (wid != 0) return;
+  uint64_t a = lane < 4 * KT ? W[lane] : 0, c = lane + 64 < 4 * KT ? W[lane + 64] : 0;
+  uint64_t mine = 0;
+  for (int rnd = 0; rnd < KT; ++rnd) {
+    const uint64_t m = wave_max_u64(umax64(a, c));
+    if (m != 0) {
+      if (a == m) a = 0;
+      else if (c == m) c = 0;
+    }
+    if (lane == rnd) mine = m;
+  }
+  if (lane < KT) {
+    if (out_keys) out_keys[(size_t)q * KT + lane] = mine;
+    if (out_scores && q < b && lane < k_out) {
+      float sc = -INFINITY;
+      int64_t ix = -1;
+      if (mine != 0) {
+        sc = float_of_ord((uint32_t)(mine >> 32));
+        ix = (int64_t)(0xFFFFFFFFu - (uint32_t)mine);
+      }
+      out_scores[(size_t)q * k_out + lane] = sc;
+      out_idx[(size_t)q * k_out + lane] = ix;
+    }
   }
 }
 
@@ -532,20 +597,34 @@ size_t fused_lds_bytes(int d, int kt, int dtype) {
   return a > merge ? a : merge;
 }
 
+// Rows of the cosine norm window for a launch (0 = scalar-cache path): the largest per-workgroup
+// range under AS 1, if it fits next to the query image.
+// Rows of each wave's cosine norm segment: what fits next to the query image (multiple of 32,
+// capped at 2048 rows = 64 tiles between refills).
+static int norm_segment_rows(int d) {
+  const size_t base = (size_t)kQSlots * d * 4 + kQSlots * sizeof(float);
+  const int64_t rows = (int64_t)((160 * 1024 - base) / 4 / kWaves) / kTileDocs * kTileDocs;
+  return (int)(rows > 2048 ? 2048 : rows);
+}
+
 // Pipeline depth and load form of the shipped kernel (chosen by tools/kbench.hip A/B runs on MI355X).
 constexpr int kPipeNB = 2;
 constexpr int kLoadMode = 1;
 constexpr int kAssign = 1;
 
-template <int DT, int KT, bool COS, int MODE, int NB = kPipeNB, int LM = kLoadMode, int AS = kAssign>
+template <int DT, int KT, bool COS, int MODE, int NB = kPipeNB, int LM = kLoadMode, int AS = kAssign, int DBG = 0,
+          int U = (KT >= 32 ? kGroupChunks / 2 : kGroupChunks)>   // KT 32: fewer buffers, no spills
 hipError_t launch_fused_t(int grid, const void* corpus, const float* norms, const float* queries,
                           int64_t n, int d, int b, uint32_t idx_base, uint64_t* out, hipStream_t s) {
-  const size_t lds = fused_lds_bytes(d, MODE == 0 ? KT : 1, DT);
-  auto kern = fused_score_kernel<DT, KT, COS, MODE, NB, LM, AS>;
+  const int seg = COS ? norm_segment_rows(d) : 0;
+  size_t lds = fused_lds_bytes(d, MODE == 0 ? KT : 1, DT);
+  const size_t lds_seg = (size_t)kQSlots * d * 4 + kQSlots * sizeof(float) + (size_t)seg * kWaves * 4;
+  if (lds_seg > lds) lds = lds_seg;
+  auto kern = fused_score_kernel<DT, KT, COS, MODE, NB, LM, AS, DBG, U>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, (const u32x4*)corpus, norms, queries, n, d, b,
-                     idx_base, out);
+                     idx_base, out, seg);
   return hipGetLastError();
 }
 
@@ -583,13 +662,14 @@ hipError_t launch_full_keys(int dtype, int metric, int grid, const void* corpus,
 
 hipError_t launch_merge(int kt, const uint64_t* in, int nlists, int in_kt, int b, int k_out, uint64_t* out_keys,
                         float* out_scores, int64_t* out_idx, hipStream_t s) {
+  if (in_kt != kt) return hipErrorInvalidValue;   // lists are always produced at the kernel's KT
   // Rows >= b of out_keys are still produced (from the zero-filled slots) so the buffer is uniform.
   const int grid = out_keys ? kQSlots : b;
   switch (kt) {
-    case 4: hipLaunchKernelGGL(merge_kernel<4>, dim3(grid), dim3(256), 0, s, in, nlists, in_kt, b, k_out, out_keys, out_scores, out_idx); break;
-    case 8: hipLaunchKernelGGL(merge_kernel<8>, dim3(grid), dim3(256), 0, s, in, nlists, in_kt, b, k_out, out_keys, out_scores, out_idx); break;
-    case 16: hipLaunchKernelGGL(merge_kernel<16>, dim3(grid), dim3(256), 0, s, in, nlists, in_kt, b, k_out, out_keys, out_scores, out_idx); break;
-    case 32: hipLaunchKernelGGL(merge_kernel<32>, dim3(grid), dim3(256), 0, s, in, nlists, in_kt, b, k_out, out_keys, out_scores, out_idx); break;
+    case 4: hipLaunchKernelGGL(merge_kernel<4>, dim3(grid), dim3(256), 0, s, in, nlists, b, k_out, out_keys, out_scores, out_idx); break;
+    case 8: hipLaunchKernelGGL(merge_kernel<8>, dim3(grid), dim3(256), 0, s, in, nlists, b, k_out, out_keys, out_scores, out_idx); break;
+    case 16: hipLaunchKernelGGL(merge_kernel<16>, dim3(grid), dim3(256), 0, s, in, nlists, b, k_out, out_keys, out_scores, out_idx); break;
+    case 32: hipLaunchKernelGGL(merge_kernel<32>, dim3(grid), dim3(256), 0, s, in, nlists, b, k_out, out_keys, out_scores, out_idx); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -8,6 +8,7 @@ from __future__ import annotations
 import ctypes
 import os
 import subprocess
+import sys
 import threading
 from typing import Optional, Sequence, Tuple
 
@@ -95,6 +96,14 @@ def load_library(path: Optional[str] = None):
         if _lib is not None and path is None:
             return _lib
         p = path or LIB_PATH
+        # If the caller already imported torch (its wheel bundles its own libamdhip64.so.7), let torch
+        # bring up the HIP runtime first so both share one runtime instance in this process.
+        torch = sys.modules.get("torch")
+        if torch is not None:
+            try:
+                torch.cuda.is_available()
+            except Exception:
+                pass
         if not os.path.exists(p):
             raise HipRetrievalUnavailable(
                 f"{p} not found: build it with `make -C {PKG_ROOT}` (hipcc --offload-arch=gfx950)")

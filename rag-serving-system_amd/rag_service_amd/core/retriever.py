@@ -60,6 +60,13 @@ class _HipRetrieverBase:
         """(scores [b,k] fp32, global indices [b,k] int64) sorted by (score desc, index asc)."""
         return self.index.search(np.atleast_2d(np.asarray(queries, dtype=np.float32)), int(k))
 
+    def search_device(self, dev_ptr: int, batch_size: int, dim: int, k: int) -> Tuple[np.ndarray, np.ndarray]:
+        """Like search(), for a (batch_size, dim) row-major fp32 buffer already in HBM on the retriever's
+        first device (device-to-device copy into the C-ABI, rr_set_queries_device)."""
+        self.index.set_queries_device(int(dev_ptr), int(batch_size), int(dim))
+        self.index.search_staged(int(k))
+        return self.index.fetch()
+
     def _docs(self, idx_row: np.ndarray, k_i: int) -> List[str]:
         valid = idx_row[idx_row >= 0][:k_i]
         return [self.documents[int(j)] for j in valid]
@@ -157,6 +164,34 @@ class HipRetriever(_HipRetrieverBase):
             return batch_results
         except Exception as e:
             logger.error(f"Error during HipRetriever.batch_retrieve: {e}", exc_info=True)
+            return [[] for _ in ks]
+
+
+    def batch_retrieve_device(self, dev_ptr: int, batch_size: int, dim: int, ks: List[int]) -> List[List[str]]:
+        """batch_retrieve() for query embeddings that are already on the GPU: a (batch_size, dim) fp32
+        row-major device buffer, fully written (the caller has synchronised its producing stream).
+        Same validation, k rules and results as batch_retrieve; skips the .cpu().numpy() round trip
+        of batch_processor.py:92."""
+        if batch_size == 0:
+            return []
+        if not isinstance(ks, list) or batch_size != len(ks):
+            logger.error(f"Batch retrieve size mismatch: {batch_size} embeddings vs {len(ks)} k values.")
+            return [[] for _ in range(batch_size)]
+        if dim != self.D:
+            logger.error(f"Batch query embedding dimension ({dim}) does not match document embedding dimension ({self.D})")
+            return [[] for _ in ks]
+        if not all(isinstance(k_val, int) for k_val in ks):
+            logger.error("List ks must contain only integers.")
+            return [[] for _ in ks]
+        valid_ks = [k_val for k_val in ks if k_val > 0]
+        if not valid_ks:
+            return [[] for _ in ks]
+        max_k = min(max(valid_ks), self.N_A)
+        try:
+            _, idx = self.search_device(dev_ptr, batch_size, dim, max_k)
+            return [[] if ks[i] <= 0 else self._docs(idx[i], ks[i]) for i in range(batch_size)]
+        except Exception as e:
+            logger.error(f"Error during HipRetriever.batch_retrieve_device: {e}", exc_info=True)
             return [[] for _ in ks]
 
 

@@ -78,3 +78,20 @@ def test_product_path_has_no_oracle_or_fallback():
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(_lib.HipRetrievalUnavailable):
         _lib.load_library(str(tmp_path / "nope.so"))
+
+
+def test_inline_asm_loads_are_hazard_free():
+    """Every fused-kernel instantiation: no compiler instruction writes a VGPR that an in-flight
+    inline-asm corpus load will still land in (tools/check_asm_loads.py; the hazard of
+    cdna_hip_programming.md §5.7 item 1). Needs the gfx950 .s from `make isa`."""
+    pkg = _lib.PKG_ROOT
+    s_file = os.path.join(pkg, "build", "isa", "rr_kernels-hip-amdgcn-amd-amdhsa-gfx950.s")
+    src = os.path.join(pkg, "csrc", "rr_kernels.hip")
+    if not os.path.exists(s_file) or os.path.getmtime(s_file) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-C", pkg, "isa"], stdout=subprocess.DEVNULL)
+    syms = re.findall(r"^(_ZN2rr18fused_score_kernel\w+):", open(s_file).read(), flags=re.M)
+    assert len(syms) >= 16
+    checker = os.path.join(os.path.dirname(pkg), "tools", "check_asm_loads.py")
+    for sym in syms:
+        r = subprocess.run(["python3", checker, s_file, sym], capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout

@@ -1,0 +1,58 @@
+"""Audit a kernel's .s for the inline-asm load hazard of cdna_hip_programming.md §5.7 item 1: no
+compiler instruction may write a VGPR that is the destination of a still-outstanding vector-memory
+load. Linear scan of the listing: a FIFO of outstanding vector-memory ops is pushed by every
+global/buffer load/store and popped by every `s_waitcnt vmcnt(n)` (loads return in order).
+usage: python tools/check_asm_loads.py file.s kernel_symbol"""
+import re
+import sys
+from collections import deque
+
+lines = open(sys.argv[1]).read().split("\n")
+sym = sys.argv[2]
+start = next(i for i, l in enumerate(lines) if l.startswith(sym + ":"))
+end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
+fifo = deque()          # sets of destination VGPRs (empty set for stores)
+bad = []
+n_asm = 0
+inasm = False
+REG = r"v\[?(\d+)(?::(\d+))?\]?"
+for i in range(start, end):
+    l = lines[i]
+    if "ASMSTART" in l:
+        inasm = True
+        continue
+    if "ASMEND" in l:
+        inasm = False
+        continue
+    t = l.strip()
+    m = re.match(r"s_waitcnt\s.*vmcnt\((\d+)\)", t)
+    if m:
+        n = int(m.group(1))
+        while len(fifo) > n:
+            fifo.popleft()
+        continue
+    m = re.match(r"(global|buffer)_(load|store|atomic)\w*\s+" + REG, t)
+    if m:
+        regs = set()
+        if m.group(2) == "load" and "lds" not in t:
+            regs = set(range(int(m.group(3)), int(m.group(4) or m.group(3)) + 1))
+        fifo.append(regs if inasm else set())  # hipcc waits for its own loads
+        n_asm += inasm
+        continue
+    if inasm:
+        continue
+    # any compiler instruction that reads or writes an in-flight destination (incl. spills)
+    if not fifo or t.startswith((";", ".", "s_")) or not t:
+        continue
+    live = set().union(*fifo)
+    touched = set()
+    for a, b in re.findall(r"\bv\[(\d+):(\d+)\]", t):
+        touched.update(range(int(a), int(b) + 1))
+    for a in re.findall(r"\bv(\d+)\b", t):
+        touched.add(int(a))
+    if touched & live:
+        bad.append((i + 1, t))
+print(f"asm vector-memory ops: {n_asm}; compiler writes to in-flight load destinations: {len(bad)}")
+for b in bad[:20]:
+    print("  ", b)
+sys.exit(1 if bad else 0)

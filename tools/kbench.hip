@@ -94,14 +94,16 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&cand, cand_elems * 8));
   std::vector<uint64_t> h_ref32(cand_elems), h_ref16(cand_elems), h_out(cand_elems);
 
+  uint64_t* fin;
+  CK(hipMalloc(&fin, kQSlots * kt * 8));
   unsigned* sink;
   CK(hipMalloc(&sink, (size_t)grid * 4 * 8 * 64 * 4));  // room for the x4 grid
-#define V32(NB, LM, AS) Variant{"fp32 NB=" #NB " LM=" #LM " AS=" #AS, 0, [&](const void* c, uint64_t* o) { \
-    return launch_fused_t<0, 8, true, 0, NB, LM, AS>(grid, c, norms, q, n, d, b, 0, o, s); }, {}}
-#define V16(NB, LM, AS) Variant{"bf16 NB=" #NB " LM=" #LM " AS=" #AS, 1, [&](const void* c, uint64_t* o) { \
-    return launch_fused_t<1, 8, true, 0, NB, LM, AS>(grid, c, norms, q, n, d, b, 0, o, s); }, {}}
-  std::vector<Variant> vs = {V32(2, 0, 0), V32(2, 1, 0), V32(3, 1, 0), V32(2, 1, 1), V32(3, 1, 1), V32(2, 0, 1),
-                             V16(2, 0, 0), V16(2, 1, 0), V16(2, 1, 1), V16(3, 1, 1), V16(2, 0, 1)};
+#define V32(NB, LM, AS, COS, DBG, U) Variant{"fp32 NB=" #NB " LM=" #LM " AS=" #AS " COS=" #COS " DBG=" #DBG " U=" #U, 0, \
+    [&](const void* c, uint64_t* o) { return launch_fused_t<0, 8, COS, 0, NB, LM, AS, DBG, U>(grid, c, norms, q, n, d, b, 0, o, s); }, {}}
+#define V16(NB, LM, AS, COS, DBG, U) Variant{"bf16 NB=" #NB " LM=" #LM " AS=" #AS " COS=" #COS " DBG=" #DBG " U=" #U, 1, \
+    [&](const void* c, uint64_t* o) { return launch_fused_t<1, 8, COS, 0, NB, LM, AS, DBG, U>(grid, c, norms, q, n, d, b, 0, o, s); }, {}}
+  std::vector<Variant> vs = {V32(2, 1, 1, true, 0, 8), V32(2, 1, 1, false, 0, 8), V32(2, 1, 1, true, 1, 8),
+                             V32(2, 1, 1, true, 2, 8), V16(2, 1, 1, true, 0, 8), V16(2, 1, 1, false, 0, 8)};
   std::vector<Variant> streams = {
       Variant{"stream frag U=8 fp32", 0, [&](const void* c, uint64_t*) {
         hipLaunchKernelGGL(stream_frag<8>, dim3(grid), dim3(512), 0, s, (const u32x4*)c, n, d, sink);
@@ -109,6 +111,8 @@ int main(int argc, char** argv) {
       Variant{"stream frag U=16 fp32", 0, [&](const void* c, uint64_t*) {
         hipLaunchKernelGGL(stream_frag<16>, dim3(grid), dim3(512), 0, s, (const u32x4*)c, n, d, sink);
         return hipGetLastError(); }, {}},
+      Variant{"merge_kernel KT=8 (256 lists)", 0, [&](const void*, uint64_t*) {
+        return launch_merge(kt, cand, grid, kt, b, 5, fin, nullptr, nullptr, s); }, {}},
       Variant{"stream lin fp32", 0, [&](const void* c, uint64_t*) {
         hipLaunchKernelGGL(stream_lin, dim3(grid), dim3(512), 0, s, (const u32x4*)c, n * d / 4, sink);
         return hipGetLastError(); }, {}},
@@ -121,8 +125,6 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   // reference outputs (first variant of each dtype) and correctness of the others
   bool have32 = false, have16 = false;
-  uint64_t* fin;
-  CK(hipMalloc(&fin, kQSlots * kt * 8));
   h_out.resize(kQSlots * kt);
   h_ref32.resize(kQSlots * kt);
   h_ref16.resize(kQSlots * kt);
