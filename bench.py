@@ -64,8 +64,9 @@ def main() -> None:
     ap.add_argument("--latency-steps", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batches", type=int, default=3)
-    ap.add_argument("--traffic-bytes", type=float, default=None,
-                    help="HBM bytes per fused launch from a rocprofv3 --pmc pass (FETCH_SIZE, gfx950-corrected)")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the rocprofv3 --pmc FETCH_SIZE child pass that fills roofline.traffic")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     from rag_service_amd import Index, get_unique_id
@@ -135,8 +136,14 @@ def main() -> None:
     alg_bytes = n_local * args.dim * elem + args.batch * args.dim * 4 + (n_local * 4 if args.metric == "cosine" else 0)
     avg_kernel_s = (kern_ms / max(launches, 1)) / 1e3
     achieved = alg_bytes / avg_kernel_s / 1e9 if launches else None
-    traffic = args.traffic_bytes
+    if args.pmc_child:            # only the fused-kernel launches matter to the parent's PMC parse
+        ix.close()
+        return
 
+    traffic, traffic_note = None, "not measured"
+    if rank == 0 and world == 1 and not args.no_pmc:
+        ix.close()                 # free HBM for the child pass
+        traffic, traffic_note = pmc_traffic(args)
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline:
@@ -167,6 +174,7 @@ def main() -> None:
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": traffic,
+                         "traffic_note": traffic_note,
                          "kernel": "fused_score_kernel (similarity + top-k)",
                          "kernel_avg_us": round(avg_kernel_s * 1e6, 2),
                          "alg_bytes_per_launch": alg_bytes},
@@ -175,6 +183,42 @@ def main() -> None:
         print(json.dumps(out), flush=True)
     barrier(dist)
     ix.close()
+
+
+def pmc_traffic(args):
+    """HBM bytes per fused launch from a rocprofv3 --pmc FETCH_SIZE pass over a short run of this same
+    workload, run as a CHILD process (MI355X_MICROARCH.md §HBM: FETCH_SIZE is in KiB and reports half the
+    bytes of a wide coalesced stream on gfx950, so bytes = FETCH_SIZE * 1024 * 2)."""
+    import csv
+    import shutil
+    import statistics
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return None, "rocprofv3 not found"
+    out = tempfile.mkdtemp(prefix="bench_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    cmd = [exe, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", out, "-o", "pmc", "--",
+           sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "3", "--warmup", "1",
+           "--latency-steps", "1", "--no-cpu-baseline", "--docs", str(args.docs), "--dim", str(args.dim),
+           "--batch", str(args.batch), "--k", str(args.k), "--dtype", args.dtype, "--metric", args.metric]
+    try:
+        subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        vals = []
+        for root, _, files in os.walk(out):
+            for f in files:
+                if f.endswith("counter_collection.csv"):
+                    for row in csv.DictReader(open(os.path.join(root, f))):
+                        if "fused_score_kernel" in row["Kernel_Name"] and row["Counter_Name"] == "FETCH_SIZE":
+                            vals.append(float(row["Counter_Value"]))
+        if not vals:
+            return None, "no fused_score_kernel FETCH_SIZE rows"
+        return round(statistics.median(vals) * 1024 * 2), (
+            f"rocprofv3 --pmc FETCH_SIZE child pass, median of {len(vals)} fused launches, x1024 B/KiB x2 (gfx950)")
+    except Exception as e:  # never fail the benchmark on the profiler
+        return None, f"pmc pass failed: {type(e).__name__}"
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
 
 
 if __name__ == "__main__":
