@@ -50,6 +50,38 @@ def cpu_baseline(n_docs: int, d: int, batch: int, k: int, batches: int, threads:
                       f"OpenBLAS limited to {threads} threads"}
 
 
+def algorithmic_bytes(rows: int, d: int, batch: int, dtype: str, metric: str) -> int:
+    """HBM bytes one fused launch must move: the corpus rows once (4 B/element fp32 and fp32-split, 2 B bf16),
+    the per-row factors it reads (norm for cosine, row scale for fp32-split), the fp32 queries once."""
+    elem = 2 if dtype == "bf16" else 4
+    per_row = (4 if metric == "cosine" else 0) + (4 if dtype == "fp32-split" else 0)
+    return rows * (d * elem + per_row) + batch * d * 4
+
+
+def timed_steps(ix, k, steps, warmup, dist, cuda_sync):
+    """W untimed warmup steps, then exactly K steps between barrier + device sync on both sides.
+    Returns (wall seconds, fused-kernel event ms summed, fused launches timed)."""
+    from rag_service_amd.dist import barrier
+    for _ in range(warmup):
+        ix.search_staged(k)
+    ix.synchronize()
+    ix.set_timing(True)
+    ix.kernel_time(reset=True)
+    barrier(dist)
+    cuda_sync()
+    ix.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ix.search_staged(k)
+    ix.synchronize()
+    cuda_sync()
+    barrier(dist)
+    elapsed = time.perf_counter() - t0
+    kern_ms, launches = ix.kernel_time(reset=True)
+    ix.set_timing(False)
+    return elapsed, kern_ms, launches
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -59,7 +91,10 @@ def main() -> None:
     ap.add_argument("--dim", type=int, default=1024)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--k", type=int, default=5)
-    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16", "fp32-split"])
+    ap.add_argument("--variants", default="bf16,fp32-split",
+                    help="other corpus dtypes measured on the same workload (N=1 only; reported beside value)")
+    ap.add_argument("--variant-steps", type=int, default=100)
     ap.add_argument("--metric", default="cosine", choices=["cosine", "dot"])
     ap.add_argument("--latency-steps", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -100,23 +135,7 @@ def main() -> None:
 
     # ---- throughput: queries resident in HBM, K back-to-back steps --------------------------------
     ix.set_queries(q)
-    for _ in range(args.warmup):
-        ix.search_staged(args.k)
-    ix.synchronize()
-    ix.set_timing(True)
-    ix.kernel_time(reset=True)
-    barrier(dist)
-    cuda_sync()
-    ix.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ix.search_staged(args.k)
-    ix.synchronize()
-    cuda_sync()
-    barrier(dist)
-    elapsed = time.perf_counter() - t0
-    kern_ms, launches = ix.kernel_time(reset=True)
-    ix.set_timing(False)
+    elapsed, kern_ms, launches = timed_steps(ix, args.k, args.steps, args.warmup, dist, cuda_sync)
     elapsed = max_over_ranks(dist, elapsed)
 
     # ---- latency: host queries in -> host results out, one batch at a time ------------------------
@@ -129,16 +148,34 @@ def main() -> None:
     lat_ms = np.array(lat) * 1e3
     p50 = max_over_ranks(dist, float(np.percentile(lat_ms, 50)))
     p99 = max_over_ranks(dist, float(np.percentile(lat_ms, 99)))
+    _, head_idx = ix.search(q, args.k)
 
     # ---- roofline of the fused kernel (rank 0's shard) ---------------------------------------------
-    elem = 4 if args.dtype == "fp32" else 2
     n_local = se - sb
-    alg_bytes = n_local * args.dim * elem + args.batch * args.dim * 4 + (n_local * 4 if args.metric == "cosine" else 0)
+    alg_bytes = algorithmic_bytes(n_local, args.dim, args.batch, args.dtype, args.metric)
     avg_kernel_s = (kern_ms / max(launches, 1)) / 1e3
     achieved = alg_bytes / avg_kernel_s / 1e9 if launches else None
     if args.pmc_child:            # only the fused-kernel launches matter to the parent's PMC parse
         ix.close()
         return
+
+    # ---- the other corpus dtypes on the same workload (1 GPU only; reported beside, never `value`) --
+    variants = {}
+    if world == 1 and args.variants:
+        for vd in [v for v in args.variants.split(",") if v and v != args.dtype]:
+            vx = Index(devices=[local], dtype=vd, metric=args.metric)
+            vx.fill_synthetic(_lib.RR_SYNTH_UNIT_NORM, 1234, args.docs, args.dim)
+            vx.set_queries(q)
+            v_el, v_ms, v_n = timed_steps(vx, args.k, args.variant_steps, args.warmup, dist, cuda_sync)
+            _, v_idx = vx.search(q, args.k)
+            vx.close()
+            v_kern = v_ms / max(v_n, 1) / 1e3
+            v_ach = algorithmic_bytes(n_local, args.dim, args.batch, vd, args.metric) / v_kern / 1e9
+            variants[vd] = {"value": round(args.batch * args.variant_steps / v_el, 2), "unit": "queries/s",
+                            "ms_per_step": round(v_el / args.variant_steps * 1e3, 4),
+                            "kernel_avg_us": round(v_kern * 1e6, 2), "achieved_GBps": round(v_ach, 1),
+                            "frac": round(v_ach / HBM_PEAK_GBS, 4), "steps": args.variant_steps,
+                            "index_agreement_with_headline": round(float(np.mean(v_idx == head_idx)), 4)}
 
     traffic, traffic_note = None, "not measured"
     if rank == 0 and world == 1 and not args.no_pmc:
@@ -179,6 +216,11 @@ def main() -> None:
                          "kernel_avg_us": round(avg_kernel_s * 1e6, 2),
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
+            "other_dtypes": variants or None,
+            "dtype_note": {"fp32": "fp32 rows stored exactly, v_mfma_f32_32x32x2_f32 (fmaf chain per score)",
+                           "bf16": "bf16 rows (RNE), bf16 MFMA, fp32 accumulate",
+                           "fp32-split": "fp32 rows as f16 hi+lo with per-row 2^e scale (22-bit significand), "
+                                         "3 f16 MFMAs, fp32 accumulate"},
         }
         print(json.dumps(out), flush=True)
     barrier(dist)
@@ -201,7 +243,8 @@ def pmc_traffic(args):
     cmd = [exe, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", out, "-o", "pmc", "--",
            sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "3", "--warmup", "1",
            "--latency-steps", "1", "--no-cpu-baseline", "--docs", str(args.docs), "--dim", str(args.dim),
-           "--batch", str(args.batch), "--k", str(args.k), "--dtype", args.dtype, "--metric", args.metric]
+           "--batch", str(args.batch), "--k", str(args.k), "--dtype", args.dtype, "--metric", args.metric,
+           "--variants", ""]
     try:
         subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
         vals = []

@@ -49,9 +49,14 @@ extern "C" {
 #define RR_E_UNSUPPORTED -5   /* valid request outside what this build implements */
 #define RR_E_OOM         -6   /* device allocation failed */
 
-/* corpus storage dtype in HBM */
-#define RR_DTYPE_F32  0       /* fp32 rows, fp32 MFMA (v_mfma_f32_32x32x2_f32) */
-#define RR_DTYPE_BF16 1       /* bf16 rows (RNE from fp32), bf16 MFMA with fp32 accumulate */
+/* corpus storage dtype in HBM (4 bytes per element for both fp32 forms, 2 for bf16) */
+#define RR_DTYPE_F32       0  /* fp32 rows stored exactly, v_mfma_f32_32x32x2_f32: every score is an fp32
+                                  fmaf chain (the reference's fp32 GEMM, up to summation order) */
+#define RR_DTYPE_BF16      1  /* bf16 rows (RNE from fp32), bf16 MFMA with fp32 accumulate */
+#define RR_DTYPE_F32_SPLIT 2  /* opt-in: fp32 rows stored as f16 hi + lo with a per-row power-of-two scale,
+                                  x ~ (hi + lo) * 2^-e with a 22-bit significand (|err| <= 2^-22 |x|); scores
+                                  from 3 f16 MFMAs per chunk, fp32 accumulate. Same 4 bytes/element as
+                                  RR_DTYPE_F32 but ~1/10 of its matrix-core work (faster; NOT bit-exact fp32) */
 
 /* similarity metric */
 #define RR_METRIC_DOT    0    /* SimpleRetriever: raw dot product          (retriever.py:112)      */

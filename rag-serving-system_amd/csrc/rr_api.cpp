@@ -53,7 +53,8 @@ struct Shard {
   hipStream_t stream = nullptr;
   int64_t row_begin = 0, row_end = 0;   // global rows held
   void* corpus = nullptr;                // [rows][d] fp32 or bf16
-  float* norms = nullptr;                // [round_up(rows, 32)] (pad = 1)
+  float* norms = nullptr;                // [round_up(rows, 32) + 32] |row| (pad = 1)
+  float* rscale = nullptr;               // [same] split-f16 row scale 2^-e (pad = 1)
   float* queries = nullptr;              // [q_cap][d] fp32
   int q_cap = 0;
   uint64_t* cand = nullptr;              // [grid][32][32] fused per-workgroup candidates
@@ -99,6 +100,15 @@ namespace {
 
 size_t elem_bytes(int dtype) { return dtype == RR_DTYPE_BF16 ? 2 : 4; }
 
+// How each public corpus dtype is stored and multiplied (rr_internal.h KDT_*).
+int kdt_of(int dtype) {
+  switch (dtype) {
+    case RR_DTYPE_BF16: return rr::KDT_BF16;
+    case RR_DTYPE_F32_SPLIT: return rr::KDT_F32_SPLIT;
+    default: return rr::KDT_F32_MFMA;
+  }
+}
+
 void shard_range(int64_t n, int world, int g, int64_t* b, int64_t* e) {
   const int64_t per = (n + world - 1) / world;
   *b = std::min<int64_t>(n, (int64_t)g * per);
@@ -118,7 +128,7 @@ int dmalloc(T** p, size_t bytes) {
 
 int free_shard(Shard& s) {
   hipSetDevice(s.dev);
-  void* ptrs[] = {s.corpus, s.norms, s.queries, s.cand, s.shard_keys, s.gathered, s.out_scores, s.out_idx,
+  void* ptrs[] = {s.corpus, s.norms, s.rscale, s.queries, s.cand, s.shard_keys, s.gathered, s.out_scores, s.out_idx,
                   s.full_keys, s.sorted, s.sort_temp};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -137,41 +147,53 @@ int alloc_corpus(rr_handle* h, Shard& s) {
   if (int rc = dmalloc(&s.corpus, (size_t)std::max<int64_t>(rows, 1) * h->d * elem_bytes(h->dtype))) return rc;
   const int64_t npad = (rows + rr::kTileDocs - 1) / rr::kTileDocs * rr::kTileDocs + rr::kTileDocs;
   if (int rc = dmalloc(&s.norms, (size_t)npad * sizeof(float))) return rc;
-  // pad norms with 1.0 so padded tiles divide by something finite
+  if (int rc = dmalloc(&s.rscale, (size_t)npad * sizeof(float))) return rc;
+  // pad with 1.0 so padded rows divide / scale by something finite
   std::vector<float> ones((size_t)npad, 1.0f);
   HIP_TRY(hipMemcpy(s.norms, ones.data(), ones.size() * sizeof(float), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s.rscale, ones.data(), ones.size() * sizeof(float), hipMemcpyHostToDevice));
   return RR_OK;
 }
 
 int finish_corpus(rr_handle* h, Shard& s) {
   HIP_TRY(hipSetDevice(s.dev));
-  if (h->metric == RR_METRIC_COSINE && s.rows() > 0)
-    HIP_TRY(rr::launch_row_norms(h->dtype, s.corpus, s.rows(), h->d, s.norms, s.stream));
+  // split-f16 rows got their norms (of the fp32 values) during the split
+  if (h->metric == RR_METRIC_COSINE && s.rows() > 0 && kdt_of(h->dtype) != rr::KDT_F32_SPLIT)
+    HIP_TRY(rr::launch_row_norms(h->dtype == RR_DTYPE_BF16 ? 1 : 0, s.corpus, s.rows(), h->d, s.norms, s.stream));
   HIP_TRY(hipStreamSynchronize(s.stream));
   return RR_OK;
 }
 
-// Copy host fp32 rows [src rows] into shard storage at local row offset `dst_row`.
+// Convert `nr` fp32 rows already on the device (tmp) into the shard's storage at local row `dst_row`.
+hipError_t store_rows(rr_handle* h, Shard& s, const float* tmp, int64_t dst_row, int64_t nr) {
+  const int d = h->d;
+  switch (kdt_of(h->dtype)) {
+    case rr::KDT_BF16:
+      return rr::launch_f32_to_bf16(tmp, (uint16_t*)s.corpus + dst_row * d, nr, d, s.stream);
+    case rr::KDT_F32_SPLIT:
+      return rr::launch_split_f32(tmp, nr, d, (float*)s.corpus + dst_row * d, s.norms + dst_row,
+                                  s.rscale + dst_row, s.stream);
+    default:
+      return rr::launch_permute_f32(tmp, (float*)s.corpus + dst_row * d, nr, d, 0, s.stream);
+  }
+}
+
+// Copy host fp32 rows into shard storage at local row offset `dst_row`.
 int upload_rows(rr_handle* h, Shard& s, const float* src, int64_t dst_row, int64_t nrows) {
   HIP_TRY(hipSetDevice(s.dev));
   const int d = h->d;
-  if (h->dtype == RR_DTYPE_F32) {
-    HIP_TRY(hipMemcpy((float*)s.corpus + dst_row * d, src, (size_t)nrows * d * 4, hipMemcpyHostToDevice));
-    return RR_OK;
-  }
-  // bf16: stage fp32 chunks on device, convert with RNE
+  // stage fp32 chunks on device, convert (pair_unit permutation, bf16 RNE, or split-f16 + norms + scales)
   const int64_t chunk_rows = std::max<int64_t>(1, (64ll << 20) / (d * 4));
   float* tmp = nullptr;
   HIP_TRY(hipMalloc((void**)&tmp, (size_t)std::min(chunk_rows, nrows) * d * 4));
   for (int64_t r0 = 0; r0 < nrows; r0 += chunk_rows) {
     const int64_t nr = std::min(chunk_rows, nrows - r0);
     hipError_t e = hipMemcpy(tmp, src + r0 * d, (size_t)nr * d * 4, hipMemcpyHostToDevice);
-    if (e == hipSuccess)
-      e = rr::launch_f32_to_bf16(tmp, (uint16_t*)s.corpus + (dst_row + r0) * d, nr * d, s.stream);
+    if (e == hipSuccess) e = store_rows(h, s, tmp, dst_row + r0, nr);
     if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
     if (e != hipSuccess) {
       hipFree(tmp);
-      return fail(RR_E_HIP, "bf16 upload failed: %s", hipGetErrorString(e));
+      return fail(RR_E_HIP, "corpus upload failed: %s", hipGetErrorString(e));
     }
   }
   hipFree(tmp);
@@ -181,10 +203,10 @@ int upload_rows(rr_handle* h, Shard& s, const float* src, int64_t dst_row, int64
 int check_shape(const rr_handle* h, int64_t n, int32_t d) {
   if (n <= 0) return fail(RR_E_INVALID, "corpus must have at least one row (n=%lld)", (long long)n);
   if (n >= 0xFFFFFFFFll) return fail(RR_E_UNSUPPORTED, "n=%lld exceeds the 32-bit index range", (long long)n);
-  const int mult = h->dtype == RR_DTYPE_F32 ? 64 : 128;
+  const int mult = h->dtype == RR_DTYPE_BF16 ? 128 : 64;
   if (d <= 0 || d % mult != 0)
     return fail(RR_E_UNSUPPORTED, "d=%d must be a positive multiple of %d for this dtype", d, mult);
-  if (rr::fused_lds_bytes(d, 32, h->dtype) > 160 * 1024)
+  if (rr::fused_lds_bytes(d, 32, kdt_of(h->dtype)) > 150 * 1024)
     return fail(RR_E_UNSUPPORTED, "d=%d too large for the LDS-resident query image", d);
   return RR_OK;
 }
@@ -294,8 +316,8 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k) {
         HIP_TRY(hipEventRecord(e0, s.stream));
       }
       if (s.rows() > 0) {
-        HIP_TRY(rr::launch_fused(h->dtype, h->metric, kt, grid, s.corpus, s.norms, qb, s.rows(), d, bb, base,
-                                 s.cand, s.stream));
+        HIP_TRY(rr::launch_fused(kdt_of(h->dtype), h->metric, kt, grid, s.corpus, s.norms, s.rscale, qb, s.rows(),
+                                 d, bb, base, s.cand, s.stream));
       } else {
         HIP_TRY(hipMemsetAsync(s.cand, 0, (size_t)rr::kQSlots * kt * 8, s.stream));
       }
@@ -311,8 +333,8 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k) {
       HIP_TRY(hipMemsetAsync(s.shard_keys, 0, (size_t)rr::kQSlots * k * 8, s.stream));
       if (rows > 0) {
         const int grid = fused_grid(s);
-        HIP_TRY(rr::launch_full_keys(h->dtype, h->metric, grid, s.corpus, s.norms, qb, rows, d, bb, base,
-                                     s.full_keys, s.stream));
+        HIP_TRY(rr::launch_full_keys(kdt_of(h->dtype), h->metric, grid, s.corpus, s.norms, s.rscale, qb, rows, d,
+                                     bb, base, s.full_keys, s.stream));
         size_t tb = s.sort_temp_bytes;
         HIP_TRY(rr::segmented_sort_desc(s.sort_temp, &tb, s.full_keys, s.sorted, bb, rows, s.stream));
         HIP_TRY(rr::launch_take_prefix(s.sorted, bb, rows, k, s.shard_keys, s.stream));
@@ -363,7 +385,8 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   g_err.clear();
   if (!out) return fail(RR_E_INVALID, "out is null");
   *out = nullptr;
-  if (dtype != RR_DTYPE_F32 && dtype != RR_DTYPE_BF16) return fail(RR_E_INVALID, "bad dtype %d", dtype);
+  if (dtype != RR_DTYPE_F32 && dtype != RR_DTYPE_BF16 && dtype != RR_DTYPE_F32_SPLIT)
+    return fail(RR_E_INVALID, "bad dtype %d", dtype);
   if (metric != RR_METRIC_DOT && metric != RR_METRIC_COSINE) return fail(RR_E_INVALID, "bad metric %d", metric);
   int def = 0;
   if (!devices) {
@@ -475,24 +498,21 @@ int rr_fill_synthetic(rr_handle* h, int kind, uint64_t seed, int64_t n_total, in
     HIP_TRY(hipSetDevice(s.dev));
     const int64_t rows = s.rows();
     if (rows > 0) {
-      if (h->dtype == RR_DTYPE_F32) {
-        HIP_TRY(rr::launch_synth(kind, seed, s.row_begin, rows, d, (float*)s.corpus, s.stream));
-      } else {
-        const int64_t chunk_rows = std::max<int64_t>(1, (256ll << 20) / (d * 4));
-        float* tmp = nullptr;
-        HIP_TRY(hipMalloc((void**)&tmp, (size_t)std::min(chunk_rows, rows) * d * 4));
-        for (int64_t r0 = 0; r0 < rows; r0 += chunk_rows) {
-          const int64_t nr = std::min(chunk_rows, rows - r0);
-          hipError_t e = rr::launch_synth(kind, seed, s.row_begin + r0, nr, d, tmp, s.stream);
-          if (e == hipSuccess) e = rr::launch_f32_to_bf16(tmp, (uint16_t*)s.corpus + r0 * d, nr * d, s.stream);
-          if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
-          if (e != hipSuccess) {
-            hipFree(tmp);
-            return fail(RR_E_HIP, "synthetic bf16 fill failed: %s", hipGetErrorString(e));
-          }
+      // generate fp32 rows in chunks, then convert into the storage layout like uploaded rows
+      const int64_t chunk_rows = std::max<int64_t>(1, (256ll << 20) / (d * 4));
+      float* tmp = nullptr;
+      HIP_TRY(hipMalloc((void**)&tmp, (size_t)std::min(chunk_rows, rows) * d * 4));
+      for (int64_t r0 = 0; r0 < rows; r0 += chunk_rows) {
+        const int64_t nr = std::min(chunk_rows, rows - r0);
+        hipError_t e = rr::launch_synth(kind, seed, s.row_begin + r0, nr, d, tmp, s.stream);
+        if (e == hipSuccess) e = store_rows(h, s, tmp, r0, nr);
+        if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+        if (e != hipSuccess) {
+          hipFree(tmp);
+          return fail(RR_E_HIP, "synthetic fill failed: %s", hipGetErrorString(e));
         }
-        hipFree(tmp);
       }
+      hipFree(tmp);
     }
     if (int rc = finish_corpus(h, s)) return rc;
   }
@@ -530,13 +550,16 @@ int rr_read_rows(const rr_handle* h, int64_t row_begin, int64_t n_rows, float* h
     const int64_t nr = std::min(n_rows - done, sp->row_end - row);
     const int64_t lr = row - sp->row_begin;
     HIP_TRY(hipSetDevice(sp->dev));
-    if (h->dtype == RR_DTYPE_F32) {
-      HIP_TRY(hipMemcpy(host_out + done * d, (const float*)sp->corpus + lr * d, (size_t)nr * d * 4,
-                        hipMemcpyDeviceToHost));
-    } else {
+    {
       float* tmp = nullptr;
       HIP_TRY(hipMalloc((void**)&tmp, (size_t)nr * d * 4));
-      hipError_t e = rr::launch_bf16_to_f32((const uint16_t*)sp->corpus + lr * d, tmp, nr * d, sp->stream);
+      const int kdt = kdt_of(h->dtype);
+      hipError_t e =
+          kdt == rr::KDT_BF16
+              ? rr::launch_bf16_to_f32((const uint16_t*)sp->corpus + lr * d, tmp, nr, d, sp->stream)
+          : kdt == rr::KDT_F32_SPLIT
+              ? rr::launch_unsplit_f32((const float*)sp->corpus + lr * d, sp->rscale + lr, nr, d, tmp, sp->stream)
+              : rr::launch_permute_f32((const float*)sp->corpus + lr * d, tmp, nr, d, 1, sp->stream);
       if (e == hipSuccess) e = hipStreamSynchronize(sp->stream);
       if (e == hipSuccess) e = hipMemcpy(host_out + done * d, tmp, (size_t)nr * d * 4, hipMemcpyDeviceToHost);
       hipFree(tmp);

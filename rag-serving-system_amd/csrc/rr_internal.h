@@ -14,17 +14,26 @@ constexpr int kQSlots     = 32;
 constexpr int kTileDocs   = 32;
 constexpr int kGroupChunks = 8;   // 16-byte loads per lane kept in flight per pipeline stage
 
+// Kernel data types (how a corpus dtype is stored and multiplied).
+//   KDT_F32_MFMA : fp32 rows, v_mfma_f32_32x32x2_f32 (a plain fmaf chain per score)
+//   KDT_BF16     : bf16 rows, v_mfma_f32_32x32x16_bf16 against the query's bf16 hi + lo
+//   KDT_F32_SPLIT: fp32 rows stored as f16 hi + lo (per-row power-of-two scale; x = (hi + lo) * 2^-e
+//                  to 2^-22 relative), 3 x v_mfma_f32_32x32x16_f16 per chunk (hi*qhi + hi*qlo + lo*qhi)
+constexpr int KDT_F32_MFMA = 0;
+constexpr int KDT_BF16 = 1;
+constexpr int KDT_F32_SPLIT = 2;
+
 // Smallest fused-kernel list width KT >= k (4, 8, 16, 32); 0 if k > RR_FUSED_KMAX.
 int fused_kt(int k);
 
-// Dynamic LDS bytes the fused kernel needs for (d, KT, dtype).
-size_t fused_lds_bytes(int d, int kt, int dtype);
+// Dynamic LDS bytes the fused kernel needs for (d, KT, kernel dtype), without the per-doc segments.
+size_t fused_lds_bytes(int d, int kt, int kdt);
 
 // Fused similarity + per-workgroup top-KT. queries: [b][d] fp32 (b <= 32) on device.
-// corpus: [n][d] fp32 (dtype 0) or bf16 (dtype 1). norms: [n] (cosine) or nullptr.
-// cand: [grid][32][KT] uint64 keys (see key encoding in rr_kernels.hip).
-hipError_t launch_fused(int dtype, int metric, int kt, int grid, const void* corpus, const float* norms,
-                        const float* queries, int64_t n, int d, int b, uint32_t idx_base,
+// corpus: [n][...] in the kernel dtype's storage. norms: [n] |d| (cosine). rscale: [n] split-f16 row
+// scales. cand: [grid][32][KT] uint64 keys (see key encoding in rr_kernels.hip).
+hipError_t launch_fused(int kdt, int metric, int kt, int grid, const void* corpus, const float* norms,
+                        const float* rscale, const float* queries, int64_t n, int d, int b, uint32_t idx_base,
                         uint64_t* cand, hipStream_t s);
 
 // Merge nlists candidate lists laid out [nlists][32][in_kt] into the top-kt per query.
@@ -33,9 +42,9 @@ hipError_t launch_merge(int kt, const uint64_t* in, int nlists, int in_kt, int b
                         uint64_t* out_keys, float* out_scores, int64_t* out_idx, hipStream_t s);
 
 // Full-score path for k > RR_FUSED_KMAX: keys [b][n] for every (query, doc) pair.
-hipError_t launch_full_keys(int dtype, int metric, int grid, const void* corpus, const float* norms,
-                            const float* queries, int64_t n, int d, int b, uint32_t idx_base,
-                            uint64_t* keys, hipStream_t s);
+hipError_t launch_full_keys(int kdt, int metric, int grid, const void* corpus, const float* norms,
+                            const float* rscale, const float* queries, int64_t n, int d, int b,
+                            uint32_t idx_base, uint64_t* keys, hipStream_t s);
 
 // Segmented descending sort of b segments of `seg` keys each (in -> out); temp from hipcub.
 hipError_t segmented_sort_desc(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out,
@@ -52,10 +61,16 @@ hipError_t launch_regroup(const uint64_t* gathered, int world, int k, int b, uin
 hipError_t launch_decode(const uint64_t* keys, int b, int k, float* scores, int64_t* idx, hipStream_t s);
 
 // Corpus preparation.
-hipError_t launch_f32_to_bf16(const float* in, uint16_t* out, int64_t count, hipStream_t s);
+// fp32 (MFMA) and bf16 rows use the pair_unit layout (rr_kernels.hip); conversions take whole rows.
+hipError_t launch_permute_f32(const float* in, float* out, int64_t nrows, int d, int inverse, hipStream_t s);
+hipError_t launch_f32_to_bf16(const float* in, uint16_t* out, int64_t nrows, int d, hipStream_t s);
 hipError_t launch_row_norms(int dtype, const void* corpus, int64_t n, int d, float* norms, hipStream_t s);
 hipError_t launch_synth(int kind, uint64_t seed, int64_t row_begin, int64_t n_rows, int d, float* out,
                         hipStream_t s);
-hipError_t launch_bf16_to_f32(const uint16_t* in, float* out, int64_t count, hipStream_t s);
+// fp32 rows -> split-f16 storage + |row| (of the fp32 values) + row scales; and back (diagnostics).
+hipError_t launch_split_f32(const float* in, int64_t n, int d, void* out, float* norms, float* rscale,
+                            hipStream_t s);
+hipError_t launch_unsplit_f32(const void* in, const float* rscale, int64_t n, int d, float* out, hipStream_t s);
+hipError_t launch_bf16_to_f32(const uint16_t* in, float* out, int64_t nrows, int d, hipStream_t s);
 
 }  // namespace rr

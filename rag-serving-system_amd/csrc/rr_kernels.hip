@@ -27,6 +27,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 template <int I, int N, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -42,19 +43,30 @@ __device__ __forceinline__ void static_for(F&& f) {
 //       loads, so it cannot drain the prefetch queue with its own conservative vmcnt(0) at the loop
 //       head. Any vector-memory op hipcc adds only makes a counted wait stricter, never looser.
 // LM 2: as LM 1 with the non-temporal hint (`nt`): the corpus is streamed once per search.
-template <int LM, int U>
+// 16-byte unit offset of load u inside a group. Every row layout pairs the two 16-byte pieces a lane
+// consumes back to back: split-f16 rows store a chunk's hi and lo pieces adjacent; fp32 and bf16 rows
+// store chunks 2m and 2m+1 adjacent (pair_unit layout). A lane reads 32 contiguous bytes and the two
+// lane halves 64 contiguous bytes of a row per load pair.
+template <int DT>
+__device__ __forceinline__ constexpr int group_off(int u) { return 4 * (u >> 1) + (u & 1); }
+
+template <int LM, int DT, int U, int u>
+__device__ __forceinline__ void load_one(u32x4 (&dst)[U], const u32x4* src) {
+  constexpr int off = 16 * group_off<DT>(u);
+  if constexpr (LM == 1)
+    asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(dst[u]) : "v"(src), "i"(off));
+  else
+    asm volatile("global_load_dwordx4 %0, %1, off offset:%2 nt" : "=v"(dst[u]) : "v"(src), "i"(off));
+  if constexpr (u + 1 < U) load_one<LM, DT, U, u + 1>(dst, src);
+}
+
+template <int LM, int U, int DT>
 __device__ __forceinline__ void load_group(u32x4 (&dst)[U], const u32x4* src) {
   if constexpr (LM == 0) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) dst[u] = src[2 * u];
+    for (int u = 0; u < U; ++u) dst[u] = src[group_off<DT>(u)];
   } else {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if constexpr (LM == 1)
-        asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(dst[u]) : "v"(src), "i"(32 * u));
-      else
-        asm volatile("global_load_dwordx4 %0, %1, off offset:%2 nt" : "=v"(dst[u]) : "v"(src), "i"(32 * u));
-    }
+    load_one<LM, DT, U, 0>(dst, src);
   }
 }
 // Before the MFMAs read dst[u] of the OLDEST group: `younger` groups of U loads were issued after it.
@@ -155,21 +167,26 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
 // MODE 1: every key written to keys[q][doc] (the k > RR_FUSED_KMAX path)
 template <int DT, int KT, bool COS, int MODE, int NB = 2, int LM = 0, int AS = 0, int DBG = 0, int U = kGroupChunks>
 __global__ __launch_bounds__(kThreads) void fused_score_kernel(
-    const u32x4* __restrict__ corpus, const float* __restrict__ norms, const float* __restrict__ queries,
-    int64_t n, int d, int b, uint32_t idx_base, uint64_t* __restrict__ out, int seg) {
+    const u32x4* __restrict__ corpus, const float* __restrict__ norms, const float* __restrict__ rscale,
+    const float* __restrict__ queries, int64_t n, int d, int b, uint32_t idx_base, uint64_t* __restrict__ out,
+    int seg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
 
   const int d4 = d >> 2;                          // float4 per query row
   const int nchunk = DT == 0 ? (d >> 3) : (d >> 4);
-  const int ngroup = nchunk / U;
+  constexpr int CPG = DT == 2 ? U / 2 : U;         // chunks per pipeline group (split-f16: 2 loads/chunk)
+  const int ngroup = nchunk / CPG;
   const size_t qimg_bytes = (size_t)nchunk * 2 * kQSlots * 16;  // per image
   float* qnorm = (float*)(smem + (DT == 0 ? qimg_bytes : 2 * qimg_bytes));
-  // Cosine: each wave keeps the norms of a `seg`-row stretch of its rows in LDS (its own segment of
-  // the region after the query image), refilled when its tiles walk past the end. The refill is
-  // ordinary loads; per refill hipcc drains the vector-memory queue once (a few times per launch).
-  float* const wseg = qnorm + kQSlots + wid * seg;
+  float* qinv = qnorm + kQSlots;                    // split-f16: 2^-e of each query's scaling
+  // Per-doc factors in LDS: each wave keeps a `seg`-row stretch of its rows (its own segment of the
+  // region after the query image) of |d| (cosine) and, for split-f16, the row scale; refilled when its
+  // tiles walk past the end (ordinary loads: hipcc drains the vector-memory queue once per refill).
+  constexpr bool SEG = COS || DT == 2;
+  constexpr int SW = (COS && DT == 2) ? 2 : 1;      // floats per row in the segment
+  float* const wseg = qinv + kQSlots + wid * seg * SW;
   int64_t seg_lo = INT64_MIN / 2;
 
   // ---- stage the queries into LDS (zero rows for unused slots) --------------------------------
@@ -182,7 +199,7 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
       if (q < b) v = ((const f32x4*)queries)[(size_t)q * d4 + c4];
       Q4[c4 * kQSlots + q] = v;
     }
-  } else {
+  } else if constexpr (DT == 1) {
     bf16x8* Qhi = (bf16x8*)smem;
     bf16x8* Qlo = (bf16x8*)(smem + qimg_bytes);
     const int d8 = d >> 3;                       // 8-element groups per row = 2 * chunk + half
@@ -206,6 +223,51 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
       Qhi[c8 * kQSlots + q] = hi;
       Qlo[c8 * kQSlots + q] = lo;
     }
+  } else {
+    // split-f16: q * 2^e = hi + lo to 2^-22 relative (22-bit significand), hi and lo f16, with 2^e putting the
+    // row's max |q| in [2^14, 2^15) (every f16 part normal down to 2^-18 of the max)
+    int* qexp = (int*)qinv;
+    for (int q = wid; q < kQSlots; q += kWaves) {
+      float m = 0.f;
+      if (q < b)
+        for (int c = lane; c < d4; c += 64) {
+          const f32x4 v = ((const f32x4*)queries)[(size_t)q * d4 + c];
+          m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+      int E = 0;
+      if (m > 0.f) frexpf(m, &E);
+      if (lane == 0) qexp[q] = m > 0.f ? 15 - E : 0;
+    }
+    __syncthreads();
+    f16x8* Qhi = (f16x8*)smem;
+    f16x8* Qlo = (f16x8*)(smem + qimg_bytes);
+    const int d8 = d >> 3;
+    for (int e = tid; e < kQSlots * d8; e += kThreads) {
+      const int q = e & (kQSlots - 1), c8 = e / kQSlots;
+      f16x8 hi, lo;
+      if (q < b) {
+        const int ex = qexp[q];
+        const f32x4* src = (const f32x4*)(queries + (size_t)q * d + c8 * 8);
+        const f32x4 x0 = src[0], x1 = src[1];
+        const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xsj = ldexpf(xs[j], ex);
+          const _Float16 fh = (_Float16)xsj;
+          hi[j] = fh;
+          lo[j] = (_Float16)(xsj - (float)fh);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { hi[j] = (_Float16)0.f; lo[j] = (_Float16)0.f; }
+      }
+      Qhi[c8 * kQSlots + q] = hi;
+      Qlo[c8 * kQSlots + q] = lo;
+    }
+    __syncthreads();                              // qexp read above; now overwrite with 2^-e
+    if (tid < kQSlots) qinv[tid] = ldexpf(1.0f, -qexp[tid]);
   }
   if constexpr (COS) {
     // |q| in fp32 from the original fp32 queries (cp.linalg.norm(X, axis=1), retriever.py:602)
@@ -225,7 +287,8 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
 
   const bool qvalid = r < b;
   const float qn = COS ? qnorm[r] : 0.f;
-  const int64_t rstride = DT == 0 ? (int64_t)(d >> 2) : (int64_t)(d >> 3);  // 16-byte units per corpus row
+  const float qs = DT == 2 ? qinv[r] : 1.f;
+  const int64_t rstride = DT == 1 ? (int64_t)(d >> 3) : (int64_t)(d >> 2);  // 16-byte units per corpus row
 
   TopK<KT> tk;
   tk.init();
@@ -252,48 +315,87 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
     auto rowp = [&](int64_t base) -> const u32x4* {
       int64_t row = base + r;
       row = row < limit ? row : limit - 1;
-      return corpus + row * rstride + h;
+      return corpus + row * rstride + 2 * h;
     };
     auto compute = [&](u32x4 (&buf)[U], int g, f32x16& acc) {
-      static_for<0, U>([&](auto uc) {
-        constexpr int u = decltype(uc)::value;
-        // oldest group in flight: (NB-1) younger groups of U loads were issued after it
-        wait_vm<LM, U, (NB - 1) * U + (U - 1 - u)>(buf[u]);
-        const int slot = (2 * (g * U + u) + h) * kQSlots + r;
-        if constexpr (DBG == 1) {   // diagnostic: no MFMA, keep the loaded bytes live
-          acc[u & 15] += __builtin_bit_cast(f32x4, buf[u]).x;
-        } else if constexpr (DT == 0) {
-          const f32x4 a = __builtin_bit_cast(f32x4, buf[u]);
-          const f32x4 q = ((const f32x4*)smem)[slot];
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, q.x, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, q.y, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, q.z, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, q.w, acc, 0, 0, 0);
-        } else {
-          const bf16x8 a = __builtin_bit_cast(bf16x8, buf[u]);
-          const bf16x8 qh = ((const bf16x8*)smem)[slot];
-          const bf16x8 ql = ((const bf16x8*)(smem + qimg_bytes))[slot];
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qh, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, ql, acc, 0, 0, 0);
-        }
-      });
+      if constexpr (DT == 2) {
+        static_for<0, U / 2>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          // oldest group in flight: (NB-1) younger groups of U loads were issued after it
+          wait_vm<LM, U, (NB - 1) * U + (U - 1 - 2 * j)>(buf[2 * j]);
+          wait_vm<LM, U, (NB - 1) * U + (U - 2 - 2 * j)>(buf[2 * j + 1]);
+          const int slot = (2 * (g * CPG + j) + h) * kQSlots + r;
+          if constexpr (DBG == 1) {
+            acc[j & 15] += __builtin_bit_cast(f32x4, buf[2 * j]).x + __builtin_bit_cast(f32x4, buf[2 * j + 1]).x;
+          } else {
+            const f16x8 ah = __builtin_bit_cast(f16x8, buf[2 * j]);
+            const f16x8 al = __builtin_bit_cast(f16x8, buf[2 * j + 1]);
+            const f16x8 qh = ((const f16x8*)smem)[slot];
+            const f16x8 ql = ((const f16x8*)(smem + qimg_bytes))[slot];
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, qh, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ql, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, qh, acc, 0, 0, 0);
+          }
+        });
+      } else {
+        static_for<0, U>([&](auto uc) {
+          constexpr int u = decltype(uc)::value;
+          wait_vm<LM, U, (NB - 1) * U + (U - 1 - u)>(buf[u]);
+          const int slot = (2 * (g * U + u) + h) * kQSlots + r;
+          if constexpr (DBG == 1) {   // diagnostic: no MFMA, keep the loaded bytes live
+            acc[u & 15] += __builtin_bit_cast(f32x4, buf[u]).x;
+          } else if constexpr (DT == 0) {
+            const f32x4 a = __builtin_bit_cast(f32x4, buf[u]);
+            const f32x4 q = ((const f32x4*)smem)[slot];
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, q.x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, q.y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, q.z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, q.w, acc, 0, 0, 0);
+          } else {
+            const bf16x8 a = __builtin_bit_cast(bf16x8, buf[u]);
+            const bf16x8 qh = ((const bf16x8*)smem)[slot];
+            const bf16x8 ql = ((const bf16x8*)(smem + qimg_bytes))[slot];
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qh, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, ql, acc, 0, 0, 0);
+          }
+        });
+      }
     };
     auto epilogue = [&](int64_t base, const f32x16& acc) {
       if constexpr (DBG == 2) {   // diagnostic: no epilogue, keep acc live
         asm volatile("" :: "v"(acc[0]), "v"(acc[15]));
         return;
       }
-      if constexpr (COS) {
+      if constexpr (SEG) {
         if (base < seg_lo || base + kTileDocs > seg_lo + seg) {   // wave-uniform
           seg_lo = base;
 #pragma unroll 1
           for (int i = lane; i < seg; i += 64) {
-            const int64_t row = base + i;
-            wseg[i] = norms[row < limit ? row : limit - 1];
+            int64_t row = base + i;
+            row = row < limit ? row : limit - 1;
+            if constexpr (COS && DT == 2) {
+              wseg[2 * i] = norms[row];
+              wseg[2 * i + 1] = rscale[row];
+            } else if constexpr (COS) {
+              wseg[i] = norms[row];
+            } else {
+              wseg[i] = rscale[row];
+            }
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+      }
+      // Cosine prefilter (top-k mode): a score whose quick estimate acc * rcp(den) (within 3 ulp of
+      // the exact quotient) is below the lane's current k-th score minus a 2^-20 relative margin cannot
+      // enter the list, so only the few that pass pay the exact IEEE division.
+      float thr = -INFINITY;
+      if constexpr (COS && MODE == 0) {
+        const uint64_t last = tk.last();
+        if (last != 0) {
+          const float t = float_of_ord((uint32_t)(last >> 32));
+          thr = t - fabsf(t) * 0x1p-20f - 0x1p-100f;
         }
       }
 #pragma unroll
@@ -301,19 +403,34 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
         const int dl = (v & 3) + 8 * (v >> 2) + 4 * h;   // C/D row map of the 32x32 MFMA
         const int64_t doc = base + dl;
         float s = acc[v];
+        if constexpr (DT == 2) {   // undo the two exact power-of-two scalings
+          const float rs = COS ? wseg[2 * (doc - seg_lo) + 1] : wseg[doc - seg_lo];
+          s = s * rs * qs;
+        }
+        const bool valid = qvalid && doc < limit;
         if constexpr (COS) {
           // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
-          const float nd = wseg[doc - seg_lo];
-          s = s / (qn * nd + 1e-8f);   // IEEE division, as the reference's elementwise kernel
-          s = fminf(fmaxf(s, -1.0f), 1.0f);
-        }
-        if constexpr (MODE == 0) {
-          if (qvalid && doc < limit) {
+          const float nd = DT == 2 ? wseg[2 * (doc - seg_lo)] : wseg[doc - seg_lo];
+          const float den = qn * nd + 1e-8f;
+          if constexpr (MODE == 0) {
+            if (valid && s * __builtin_amdgcn_rcpf(den) >= thr) {
+              float c = s / den;   // IEEE division, as the reference's elementwise kernel
+              c = fminf(fmaxf(c, -1.0f), 1.0f);
+              const uint64_t key = make_key(c, idx_base + (uint32_t)doc);
+              if (key > tk.last()) tk.insert(key);
+            }
+          } else {
+            float c = s / den;
+            c = fminf(fmaxf(c, -1.0f), 1.0f);
+            if (valid) out[(size_t)r * (size_t)n + (size_t)doc] = make_key(c, idx_base + (uint32_t)doc);
+          }
+        } else if constexpr (MODE == 0) {
+          if (valid) {
             const uint64_t key = make_key(s, idx_base + (uint32_t)doc);
             if (key > tk.last()) tk.insert(key);
           }
         } else {
-          if (qvalid && doc < limit) out[(size_t)r * (size_t)n + (size_t)doc] = make_key(s, idx_base + (uint32_t)doc);
+          if (valid) out[(size_t)r * (size_t)n + (size_t)doc] = make_key(s, idx_base + (uint32_t)doc);
         }
       }
     };
@@ -331,7 +448,7 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
     const u32x4* const safe = lptr;
     auto issue = [&](u32x4 (&dst)[U]) {
       const u32x4* src = lrow < limit ? lptr + 2 * U * lg : safe;
-      load_group<LM, U>(dst, src);
+      load_group<LM, U, DT>(dst, src);
       if (++lg == ngroup) {
         lg = 0;
         lrow += bstep;
@@ -501,19 +618,106 @@ __global__ void regroup_kernel(const uint64_t* __restrict__ in, int world, int k
 // ------------------------------------------------------------------------------------------------
 // corpus preparation
 // ------------------------------------------------------------------------------------------------
-__global__ void f32_to_bf16_kernel(const float* __restrict__ in, __bf16* __restrict__ out, int64_t count) {
-  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (i + 3 < count) {
-    const f32x4 v = *(const f32x4*)(in + i);
-    out[i] = (__bf16)v.x; out[i + 1] = (__bf16)v.y; out[i + 2] = (__bf16)v.z; out[i + 3] = (__bf16)v.w;
-  } else {
-    for (int64_t j = i; j < count; ++j) out[j] = (__bf16)in[j];
+// fp32 and bf16 row storage in 16-byte units: unit g = 2c + h of a row (chunk c, lane half h; fp32:
+// elements 8c + 4h + {0..3}, bf16: 16c + 8h + {0..7}) lives at unit 4(c >> 1) + 2h + (c & 1), so the two
+// chunks a lane loads back to back are adjacent (32 contiguous bytes per lane, 64 per row).
+__device__ __forceinline__ int pair_unit(int g) {
+  const int c = g >> 1, h = g & 1;
+  return 4 * (c >> 1) + 2 * h + (c & 1);
+}
+
+// fp32 rows -> pair_unit layout (one 16-byte unit per thread), and back.
+__global__ void permute_f32_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out, int64_t nrows, int d,
+                                   int inverse) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int upr = d >> 2;
+  if (i >= nrows * upr) return;
+  const int64_t row = i / upr;
+  const int g = (int)(i - row * upr);
+  if (inverse) out[i] = in[row * upr + pair_unit(g)];
+  else out[row * upr + pair_unit(g)] = in[i];
+}
+
+__global__ void f32_to_bf16_kernel(const float* __restrict__ in, u32x4* __restrict__ out, int64_t nrows, int d) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // one 8-element group
+  const int gpr = d >> 3;
+  if (i >= nrows * gpr) return;
+  const int64_t row = i / gpr;
+  const int g = (int)(i - row * gpr);
+  const f32x4 x0 = ((const f32x4*)in)[2 * i], x1 = ((const f32x4*)in)[2 * i + 1];
+  const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (__bf16)xs[j];
+  out[row * gpr + pair_unit(g)] = __builtin_bit_cast(u32x4, v);
+}
+
+__global__ void bf16_to_f32_kernel(const u32x4* __restrict__ in, float* __restrict__ out, int64_t nrows, int d) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int gpr = d >> 3;
+  if (i >= nrows * gpr) return;
+  const int64_t row = i / gpr;
+  const int g = (int)(i - row * gpr);
+  const bf16x8 v = __builtin_bit_cast(bf16x8, in[row * gpr + pair_unit(g)]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[i * 8 + j] = (float)v[j];
+}
+
+// fp32 rows -> split-f16 storage: per 8-element group g of a row, 16 bytes of hi then 16 bytes of lo
+// (byte offset 32 g), where x * 2^e = hi + lo to 2^-22 relative and 2^e puts the row's max |x| in
+// [2^14, 2^15). Also |row|_2 of the ORIGINAL fp32 values and rscale = 2^-e. One wave per row.
+__global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict__ in, int64_t n, int d,
+                                                        u32x4* __restrict__ out, float* __restrict__ norms,
+                                                        float* __restrict__ rscale) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const f32x4* src = (const f32x4*)(in + row * d);
+  float m = 0.f, ss = 0.f;
+  for (int c = lane; c < (d >> 2); c += 64) {
+    const f32x4 v = src[c];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    ss = fmaf(v.x, v.x, ss); ss = fmaf(v.y, v.y, ss); ss = fmaf(v.z, v.z, ss); ss = fmaf(v.w, v.w, ss);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    m = fmaxf(m, __shfl_xor(m, off, 64));
+    ss += __shfl_xor(ss, off, 64);
+  }
+  int E = 0;
+  if (m > 0.f) frexpf(m, &E);
+  const int ex = m > 0.f ? 15 - E : 0;
+  if (lane == 0) {
+    norms[row] = sqrtf(ss);
+    rscale[row] = ldexpf(1.0f, -ex);
+  }
+  u32x4* dst = out + row * (d >> 2);
+  for (int g = lane; g < (d >> 3); g += 64) {
+    const f32x4 x0 = src[2 * g], x1 = src[2 * g + 1];
+    const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    f16x8 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xsj = ldexpf(xs[j], ex);
+      const _Float16 fh = (_Float16)xsj;
+      hi[j] = fh;
+      lo[j] = (_Float16)(xsj - (float)fh);
+    }
+    dst[2 * g] = __builtin_bit_cast(u32x4, hi);
+    dst[2 * g + 1] = __builtin_bit_cast(u32x4, lo);
   }
 }
 
-__global__ void bf16_to_f32_kernel(const __bf16* __restrict__ in, float* __restrict__ out, int64_t count) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < count) out[i] = (float)in[i];
+__global__ void unsplit_f32_kernel(const u32x4* __restrict__ in, const float* __restrict__ rscale, int64_t n,
+                                   int d, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // one 8-element group
+  if (i >= n * (d >> 3)) return;
+  const int64_t row = i / (d >> 3);
+  const f16x8 hi = __builtin_bit_cast(f16x8, in[2 * i]);
+  const f16x8 lo = __builtin_bit_cast(f16x8, in[2 * i + 1]);
+  const float rs = rscale[row];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[i * 8 + j] = ((float)hi[j] + (float)lo[j]) * rs;
 }
 
 // One wave per row: |row|_2 in fp32 (the reference recomputes cp.linalg.norm(Y, axis=1) every call,
@@ -589,21 +793,20 @@ int fused_kt(int k) {
   return 0;
 }
 
-size_t fused_lds_bytes(int d, int kt, int dtype) {
-  const size_t qimg = (size_t)kQSlots * d * 4;   // fp32 image, or bf16 hi + lo images
+// LDS of the query image (fp32: one 4-byte image; bf16 / split-f16: hi + lo 2-byte images) plus the
+// per-query scalars, or of the end-of-kernel merge if larger.
+size_t fused_lds_bytes(int d, int kt, int kdt) {
+  (void)kdt;
+  const size_t qimg = (size_t)kQSlots * d * 4 + 2 * kQSlots * sizeof(float);
   const size_t merge = (size_t)kQSlots * 16 * (kt > 0 ? kt : 1) * 8;
-  const size_t a = qimg + kQSlots * sizeof(float);
-  (void)dtype;
-  return a > merge ? a : merge;
+  return qimg > merge ? qimg : merge;
 }
 
-// Rows of the cosine norm window for a launch (0 = scalar-cache path): the largest per-workgroup
-// range under AS 1, if it fits next to the query image.
-// Rows of each wave's cosine norm segment: what fits next to the query image (multiple of 32,
-// capped at 2048 rows = 64 tiles between refills).
-static int norm_segment_rows(int d) {
-  const size_t base = (size_t)kQSlots * d * 4 + kQSlots * sizeof(float);
-  const int64_t rows = (int64_t)((160 * 1024 - base) / 4 / kWaves) / kTileDocs * kTileDocs;
+// Rows of each wave's per-doc segment (|d| and/or the split-f16 row scale, `sw` floats per row): what
+// fits next to the query image, a multiple of 32, capped at 2048 rows (64 tiles between refills).
+static int segment_rows(int d, int sw) {
+  const size_t base = (size_t)kQSlots * d * 4 + 2 * kQSlots * sizeof(float);
+  const int64_t rows = (int64_t)((160 * 1024 - base) / (4 * sw) / kWaves) / kTileDocs * kTileDocs;
   return (int)(rows > 2048 ? 2048 : rows);
 }
 
@@ -614,50 +817,65 @@ constexpr int kAssign = 1;
 
 template <int DT, int KT, bool COS, int MODE, int NB = kPipeNB, int LM = kLoadMode, int AS = kAssign, int DBG = 0,
           int U = (KT >= 32 ? kGroupChunks / 2 : kGroupChunks)>   // KT 32: fewer buffers, no spills
-hipError_t launch_fused_t(int grid, const void* corpus, const float* norms, const float* queries,
-                          int64_t n, int d, int b, uint32_t idx_base, uint64_t* out, hipStream_t s) {
-  const int seg = COS ? norm_segment_rows(d) : 0;
+hipError_t launch_fused_t(int grid, const void* corpus, const float* norms, const float* rscale,
+                          const float* queries, int64_t n, int d, int b, uint32_t idx_base, uint64_t* out,
+                          hipStream_t s) {
+  constexpr int sw = (COS && DT == 2) ? 2 : 1;
+  const int seg = (COS || DT == 2) ? segment_rows(d, sw) : 0;
   size_t lds = fused_lds_bytes(d, MODE == 0 ? KT : 1, DT);
-  const size_t lds_seg = (size_t)kQSlots * d * 4 + kQSlots * sizeof(float) + (size_t)seg * kWaves * 4;
+  const size_t lds_seg = (size_t)kQSlots * d * 4 + 2 * kQSlots * sizeof(float) + (size_t)seg * sw * kWaves * 4;
   if (lds_seg > lds) lds = lds_seg;
   auto kern = fused_score_kernel<DT, KT, COS, MODE, NB, LM, AS, DBG, U>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, (const u32x4*)corpus, norms, queries, n, d, b,
-                     idx_base, out, seg);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, (const u32x4*)corpus, norms, rscale, queries, n,
+                     d, b, idx_base, out, seg);
   return hipGetLastError();
 }
 
 template <int DT, bool COS>
-static hipError_t launch_fused_k(int kt, int grid, const void* corpus, const float* norms, const float* queries,
-                                 int64_t n, int d, int b, uint32_t idx_base, uint64_t* cand, hipStream_t s) {
+static hipError_t launch_fused_k(int kt, int grid, const void* c, const float* nr, const float* rs,
+                                 const float* q, int64_t n, int d, int b, uint32_t base, uint64_t* o,
+                                 hipStream_t s) {
   switch (kt) {
-    case 4: return launch_fused_t<DT, 4, COS, 0>(grid, corpus, norms, queries, n, d, b, idx_base, cand, s);
-    case 8: return launch_fused_t<DT, 8, COS, 0>(grid, corpus, norms, queries, n, d, b, idx_base, cand, s);
-    case 16: return launch_fused_t<DT, 16, COS, 0>(grid, corpus, norms, queries, n, d, b, idx_base, cand, s);
-    case 32: return launch_fused_t<DT, 32, COS, 0>(grid, corpus, norms, queries, n, d, b, idx_base, cand, s);
+    case 4: return launch_fused_t<DT, 4, COS, 0>(grid, c, nr, rs, q, n, d, b, base, o, s);
+    case 8: return launch_fused_t<DT, 8, COS, 0>(grid, c, nr, rs, q, n, d, b, base, o, s);
+    case 16: return launch_fused_t<DT, 16, COS, 0>(grid, c, nr, rs, q, n, d, b, base, o, s);
+    case 32: return launch_fused_t<DT, 32, COS, 0>(grid, c, nr, rs, q, n, d, b, base, o, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-hipError_t launch_fused(int dtype, int metric, int kt, int grid, const void* corpus, const float* norms,
-                        const float* queries, int64_t n, int d, int b, uint32_t idx_base, uint64_t* cand,
-                        hipStream_t s) {
-  if (dtype == 0)
-    return metric ? launch_fused_k<0, true>(kt, grid, corpus, norms, queries, n, d, b, idx_base, cand, s)
-                  : launch_fused_k<0, false>(kt, grid, corpus, norms, queries, n, d, b, idx_base, cand, s);
-  return metric ? launch_fused_k<1, true>(kt, grid, corpus, norms, queries, n, d, b, idx_base, cand, s)
-                : launch_fused_k<1, false>(kt, grid, corpus, norms, queries, n, d, b, idx_base, cand, s);
+hipError_t launch_fused(int kdt, int metric, int kt, int grid, const void* c, const float* nr, const float* rs,
+                        const float* q, int64_t n, int d, int b, uint32_t base, uint64_t* cand, hipStream_t s) {
+  switch (kdt) {
+    case KDT_F32_MFMA:
+      return metric ? launch_fused_k<0, true>(kt, grid, c, nr, rs, q, n, d, b, base, cand, s)
+                    : launch_fused_k<0, false>(kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+    case KDT_BF16:
+      return metric ? launch_fused_k<1, true>(kt, grid, c, nr, rs, q, n, d, b, base, cand, s)
+                    : launch_fused_k<1, false>(kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+    case KDT_F32_SPLIT:
+      return metric ? launch_fused_k<2, true>(kt, grid, c, nr, rs, q, n, d, b, base, cand, s)
+                    : launch_fused_k<2, false>(kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
-hipError_t launch_full_keys(int dtype, int metric, int grid, const void* corpus, const float* norms,
-                            const float* queries, int64_t n, int d, int b, uint32_t idx_base, uint64_t* keys,
-                            hipStream_t s) {
-  if (dtype == 0)
-    return metric ? launch_fused_t<0, 4, true, 1>(grid, corpus, norms, queries, n, d, b, idx_base, keys, s)
-                  : launch_fused_t<0, 4, false, 1>(grid, corpus, norms, queries, n, d, b, idx_base, keys, s);
-  return metric ? launch_fused_t<1, 4, true, 1>(grid, corpus, norms, queries, n, d, b, idx_base, keys, s)
-                : launch_fused_t<1, 4, false, 1>(grid, corpus, norms, queries, n, d, b, idx_base, keys, s);
+hipError_t launch_full_keys(int kdt, int metric, int grid, const void* c, const float* nr, const float* rs,
+                            const float* q, int64_t n, int d, int b, uint32_t base, uint64_t* keys, hipStream_t s) {
+  switch (kdt) {
+    case KDT_F32_MFMA:
+      return metric ? launch_fused_t<0, 4, true, 1>(grid, c, nr, rs, q, n, d, b, base, keys, s)
+                    : launch_fused_t<0, 4, false, 1>(grid, c, nr, rs, q, n, d, b, base, keys, s);
+    case KDT_BF16:
+      return metric ? launch_fused_t<1, 4, true, 1>(grid, c, nr, rs, q, n, d, b, base, keys, s)
+                    : launch_fused_t<1, 4, false, 1>(grid, c, nr, rs, q, n, d, b, base, keys, s);
+    case KDT_F32_SPLIT:
+      return metric ? launch_fused_t<2, 4, true, 1>(grid, c, nr, rs, q, n, d, b, base, keys, s)
+                    : launch_fused_t<2, 4, false, 1>(grid, c, nr, rs, q, n, d, b, base, keys, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_merge(int kt, const uint64_t* in, int nlists, int in_kt, int b, int k_out, uint64_t* out_keys,
@@ -706,16 +924,38 @@ hipError_t launch_decode(const uint64_t* keys, int b, int k, float* scores, int6
   return hipGetLastError();
 }
 
-hipError_t launch_f32_to_bf16(const float* in, uint16_t* out, int64_t count, hipStream_t s) {
-  const int64_t threads = (count + 3) / 4;
-  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, in,
-                     (__bf16*)out, count);
+hipError_t launch_permute_f32(const float* in, float* out, int64_t nrows, int d, int inverse, hipStream_t s) {
+  const int64_t units = nrows * (d >> 2);
+  hipLaunchKernelGGL(permute_f32_kernel, dim3((unsigned)((units + 255) / 256)), dim3(256), 0, s, (const u32x4*)in,
+                     (u32x4*)out, nrows, d, inverse);
   return hipGetLastError();
 }
 
-hipError_t launch_bf16_to_f32(const uint16_t* in, float* out, int64_t count, hipStream_t s) {
-  hipLaunchKernelGGL(bf16_to_f32_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s,
-                     (const __bf16*)in, out, count);
+hipError_t launch_f32_to_bf16(const float* in, uint16_t* out, int64_t nrows, int d, hipStream_t s) {
+  const int64_t groups = nrows * (d >> 3);
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, in, (u32x4*)out,
+                     nrows, d);
+  return hipGetLastError();
+}
+
+hipError_t launch_bf16_to_f32(const uint16_t* in, float* out, int64_t nrows, int d, hipStream_t s) {
+  const int64_t groups = nrows * (d >> 3);
+  hipLaunchKernelGGL(bf16_to_f32_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s,
+                     (const u32x4*)in, out, nrows, d);
+  return hipGetLastError();
+}
+
+hipError_t launch_split_f32(const float* in, int64_t n, int d, void* out, float* norms, float* rscale,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(split_f32_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, in, n, d, (u32x4*)out, norms,
+                     rscale);
+  return hipGetLastError();
+}
+
+hipError_t launch_unsplit_f32(const void* in, const float* rscale, int64_t n, int d, float* out, hipStream_t s) {
+  const int64_t groups = n * (d >> 3);
+  hipLaunchKernelGGL(unsplit_f32_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, (const u32x4*)in,
+                     rscale, n, d, out);
   return hipGetLastError();
 }
 

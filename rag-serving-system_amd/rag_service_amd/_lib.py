@@ -29,6 +29,7 @@ RR_E_UNSUPPORTED = -5
 RR_E_OOM = -6
 RR_DTYPE_F32 = 0
 RR_DTYPE_BF16 = 1
+RR_DTYPE_F32_SPLIT = 2
 RR_METRIC_DOT = 0
 RR_METRIC_COSINE = 1
 RR_SYNTH_EXACT_INT = 0
@@ -38,7 +39,7 @@ RR_FUSED_KMAX = 32
 RR_ABI_VERSION = 1
 
 DTYPES = {"fp32": RR_DTYPE_F32, "float32": RR_DTYPE_F32, "f32": RR_DTYPE_F32,
-          "bf16": RR_DTYPE_BF16, "bfloat16": RR_DTYPE_BF16}
+          "bf16": RR_DTYPE_BF16, "bfloat16": RR_DTYPE_BF16, "fp32-split": RR_DTYPE_F32_SPLIT}
 METRICS = {"dot": RR_METRIC_DOT, "cosine": RR_METRIC_COSINE}
 
 # Every function the header declares: name -> (restype, argtypes)

@@ -124,6 +124,22 @@ def f3_small(golden_synth):
     return synth.unit_norm_gaussian(seed, n, 1024), synth.unit_norm_gaussian(qseed, 32, 1024)
 
 
+def test_fp32_split_storage_round_trip(Index):
+    """RR_DTYPE_F32_SPLIT keeps x as f16 hi + lo with a per-row power-of-two scale: read-back is within 2^-22
+    relative of every input element (22-bit significand), exact for values with <= 22 significant bits."""
+    rng = np.random.default_rng(5)
+    x = (rng.standard_normal((257, 128)) * rng.uniform(1e-3, 1e3, size=(257, 1))).astype(np.float32)
+    x[3] = 0.0
+    ix = Index(dtype="fp32-split", metric="dot")
+    ix.load(x)
+    y = ix.read_rows(0, 257)
+    bound = 2.0 ** -22 * np.abs(x) + 2.0 ** -30 * np.abs(x).max(axis=1, keepdims=True)   # tiny elements: f16 subnormal lo
+    assert np.all(np.abs(y - x) <= bound)
+    ints = synth.exact_int_rows(3, 0, 64, 128)
+    ix.load(ints)
+    assert np.array_equal(ix.read_rows(0, 64), ints)
+
+
 def test_device_generator_matches_numpy(Index, golden_synth):
     ix = Index(dtype="fp32", metric="dot")
     ix.fill_synthetic(0, 1234, 4099, 1024)
@@ -135,7 +151,7 @@ def test_device_generator_matches_numpy(Index, golden_synth):
     np.testing.assert_allclose(ix2.read_rows(0, 300), ref, rtol=0, atol=2e-7)
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp32-split"])
 def test_exact_integer_corpus_bit_exact(Index, golden_synth, f2_small, dtype):
     """F2: every dot is exact in fp32, so scores must equal the fp64 values bit-for-bit and the order is
     the canonical (score desc, index asc); where the reference had no ties its order matches too."""
@@ -154,9 +170,10 @@ def test_exact_integer_corpus_bit_exact(Index, golden_synth, f2_small, dtype):
 
 
 @pytest.mark.parametrize("metric,flav", [("dot", "simple"), ("cosine", "cupy")])
-def test_unit_norm_corpus_fp32(Index, golden_synth, f3_small, metric, flav):
+@pytest.mark.parametrize("dtype", ["fp32", "fp32-split"])
+def test_unit_norm_corpus_fp32(Index, golden_synth, f3_small, metric, flav, dtype):
     corpus, q = f3_small
-    ix = get_index(Index, "f3_small", corpus, "fp32", metric)
+    ix = get_index(Index, "f3_small", corpus, dtype, metric)
     scores, idx = ix.search(q, 10)
     check_topk(idx, scores, golden_synth[f"f3_64k_k10_{flav}_idx"], corpus, q, metric)
 
@@ -180,7 +197,7 @@ SHAPES = [  # (n, d, b, k)
 
 @pytest.mark.parametrize("n,d,b,k", SHAPES)
 @pytest.mark.parametrize("metric", ["dot", "cosine"])
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp32-split"])
 def test_shapes_against_oracle(Index, n, d, b, k, metric, dtype):
     if dtype == "bf16" and d % 128:
         pytest.skip("bf16 path needs d % 128 == 0")

@@ -86,8 +86,21 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&q, (size_t)b * d * 4));
   CK(launch_synth(1, 1234, 0, n, d, c32, s));
   CK(launch_synth(1, 99, 0, b, d, q, s));
-  CK(launch_f32_to_bf16(c32, c16, (int64_t)n * d, s));
+  CK(launch_f32_to_bf16(c32, c16, n, d, s));
   CK(launch_row_norms(0, c32, n, d, norms, s));
+  float *csplit, *norms2, *rscale;
+  CK(hipMalloc(&csplit, (size_t)n * d * 4));
+  CK(hipMalloc(&norms2, (size_t)(n + 64) * 4));
+  CK(hipMalloc(&rscale, (size_t)(n + 64) * 4));
+  CK(launch_split_f32(c32, n, d, csplit, norms2, rscale, s));
+  {  // the fp32-MFMA kernel reads rows in the pair_unit layout
+    float* cperm;
+    CK(hipMalloc(&cperm, (size_t)n * d * 4));
+    CK(launch_permute_f32(c32, cperm, n, d, 0, s));
+    CK(hipStreamSynchronize(s));
+    CK(hipFree(c32));
+    c32 = cperm;
+  }
   const int grid = cus;
   uint64_t *cand, *ref32, *ref16;
   const size_t cand_elems = (size_t)grid * kQSlots * kt;
@@ -99,11 +112,14 @@ int main(int argc, char** argv) {
   unsigned* sink;
   CK(hipMalloc(&sink, (size_t)grid * 4 * 8 * 64 * 4));  // room for the x4 grid
 #define V32(NB, LM, AS, COS, DBG, U) Variant{"fp32 NB=" #NB " LM=" #LM " AS=" #AS " COS=" #COS " DBG=" #DBG " U=" #U, 0, \
-    [&](const void* c, uint64_t* o) { return launch_fused_t<0, 8, COS, 0, NB, LM, AS, DBG, U>(grid, c, norms, q, n, d, b, 0, o, s); }, {}}
+    [&](const void* c, uint64_t* o) { return launch_fused_t<0, 8, COS, 0, NB, LM, AS, DBG, U>(grid, c, norms, rscale, q, n, d, b, 0, o, s); }, {}}
 #define V16(NB, LM, AS, COS, DBG, U) Variant{"bf16 NB=" #NB " LM=" #LM " AS=" #AS " COS=" #COS " DBG=" #DBG " U=" #U, 1, \
-    [&](const void* c, uint64_t* o) { return launch_fused_t<1, 8, COS, 0, NB, LM, AS, DBG, U>(grid, c, norms, q, n, d, b, 0, o, s); }, {}}
-  std::vector<Variant> vs = {V32(2, 1, 1, true, 0, 8), V32(2, 1, 1, false, 0, 8), V32(2, 1, 1, true, 1, 8),
-                             V32(2, 1, 1, true, 2, 8), V16(2, 1, 1, true, 0, 8), V16(2, 1, 1, false, 0, 8)};
+    [&](const void* c, uint64_t* o) { return launch_fused_t<1, 8, COS, 0, NB, LM, AS, DBG, U>(grid, c, norms, rscale, q, n, d, b, 0, o, s); }, {}}
+#define VS(NB, LM, AS, COS, DBG, U) Variant{"fp32-split NB=" #NB " LM=" #LM " AS=" #AS " COS=" #COS " DBG=" #DBG " U=" #U, 2, \
+    [&](const void* c, uint64_t* o) { return launch_fused_t<2, 8, COS, 0, NB, LM, AS, DBG, U>(grid, c, norms2, rscale, q, n, d, b, 0, o, s); }, {}}
+  std::vector<Variant> vs = {V32(2, 1, 1, true, 0, 8), V32(2, 1, 1, true, 1, 8), V32(3, 1, 1, true, 0, 8), V32(2, 1, 1, true, 0, 4), VS(2, 1, 1, true, 0, 8), VS(2, 1, 1, false, 0, 8),
+                             VS(2, 1, 1, true, 2, 8), V16(2, 1, 1, true, 0, 8), V16(3, 1, 1, true, 0, 8),
+                             V16(2, 1, 1, false, 0, 8), V16(2, 1, 1, true, 1, 8)};
   std::vector<Variant> streams = {
       Variant{"stream frag U=8 fp32", 0, [&](const void* c, uint64_t*) {
         hipLaunchKernelGGL(stream_frag<8>, dim3(grid), dim3(512), 0, s, (const u32x4*)c, n, d, sink);
@@ -130,21 +146,23 @@ int main(int argc, char** argv) {
   h_ref16.resize(kQSlots * kt);
   for (auto& v : vs) {
     CK(hipMemsetAsync(cand, 0, cand_elems * 8, s));
-    CK(v.run(v.dtype ? (const void*)c16 : (const void*)c32, cand));
+    CK(v.run(v.dtype == 1 ? (const void*)c16 : v.dtype == 2 ? (const void*)csplit : (const void*)c32, cand));
     CK(launch_merge(kt, cand, grid, kt, b, kt, fin, nullptr, nullptr, s));
     CK(hipStreamSynchronize(s));
     CK(hipMemcpy(h_out.data(), fin, kQSlots * kt * 8, hipMemcpyDeviceToHost));
-    auto& ref = v.dtype ? h_ref16 : h_ref32;
-    bool& have = v.dtype ? have16 : have32;
+    auto& ref = h_ref32;
+    bool& have = have32;
     if (!have) { ref = h_out; have = true; }
-    const bool same = memcmp(ref.data(), h_out.data(), kQSlots * kt * 8) == 0;
-    printf("{\"variant\": \"%s\", \"bitwise_equal_to_first\": %s}\n", v.name.c_str(), same ? "true" : "false");
+    int same_idx = 0;
+    for (size_t i = 0; i < ref.size(); ++i) same_idx += (uint32_t)ref[i] == (uint32_t)h_out[i];
+    printf("{\"variant\": \"%s\", \"same_index_frac_vs_first\": %.4f, \"bitwise\": %s}\n", v.name.c_str(),
+           same_idx / (double)ref.size(), memcmp(ref.data(), h_out.data(), ref.size() * 8) == 0 ? "true" : "false");
   }
   const size_t nvar = vs.size();
   for (auto& v : streams) vs.push_back(v);
   for (int r = 0; r < rounds; ++r) {
     for (auto& v : vs) {
-      const void* c = v.dtype ? (const void*)c16 : (const void*)c32;
+      const void* c = v.dtype == 1 ? (const void*)c16 : v.dtype == 2 ? (const void*)csplit : (const void*)c32;
       CK(v.run(c, cand));   // warm
       CK(hipEventRecord(e0, s));
       for (int i = 0; i < reps; ++i) CK(v.run(c, cand));
@@ -160,7 +178,7 @@ int main(int argc, char** argv) {
     std::sort(m.begin(), m.end());
     const double med = m[m.size() / 2], best = m[0];
     const bool is_stream = (size_t)(&v - &vs[0]) >= nvar;
-    const double bytes = (double)n * d * (v.dtype ? 2 : 4) + (is_stream ? 0.0 : n * 4.0 + b * d * 4.0);
+    const double bytes = (double)n * d * (v.dtype == 1 ? 2 : 4) + (is_stream ? 0.0 : n * 4.0 + b * d * 4.0);
     printf("{\"variant\": \"%s\", \"median_us\": %.1f, \"min_us\": %.1f, \"GBps_median\": %.0f, \"frac_8TBs\": %.3f}\n",
            v.name.c_str(), med * 1e3, best * 1e3, bytes / (med * 1e-3) / 1e9, bytes / (med * 1e-3) / 8e12);
   }
