@@ -29,6 +29,12 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "rag-serving-system_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+SCORE_KERNEL_DOC = ("similarity + top-k kernel: sk_score_kernel (split-K, LDS-DMA) where the shape allows, "
+                    "else fused_score_kernel")
+
+
+def is_score_kernel(name: str) -> bool:
+    return "sk_score_kernel" in name or "fused_score_kernel" in name
 
 
 def cpu_baseline(n_docs: int, d: int, batch: int, k: int, batches: int, threads: int) -> dict:
@@ -212,12 +218,14 @@ def main() -> None:
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": traffic,
                          "traffic_note": traffic_note,
-                         "kernel": "fused_score_kernel (similarity + top-k)",
+                         "kernel": SCORE_KERNEL_DOC,
                          "kernel_avg_us": round(avg_kernel_s * 1e6, 2),
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "other_dtypes": variants or None,
-            "dtype_note": {"fp32": "fp32 rows stored exactly, v_mfma_f32_32x32x2_f32 (fmaf chain per score)",
+            "dtype_note": {"fp32": "fp32 rows stored exactly; split-K kernel splits corpus and query values exactly "
+                                   "into 3 bf16 each, 6 bf16 MFMAs (every kept product exact, dropped terms "
+                                   "< 2^-23 |xq|), fp32 accumulate",
                            "bf16": "bf16 rows (RNE), bf16 MFMA, fp32 accumulate",
                            "fp32-split": "fp32 rows as f16 hi+lo with per-row 2^e scale (22-bit significand), "
                                          "3 f16 MFMAs, fp32 accumulate"},
@@ -252,10 +260,10 @@ def pmc_traffic(args):
             for f in files:
                 if f.endswith("counter_collection.csv"):
                     for row in csv.DictReader(open(os.path.join(root, f))):
-                        if "fused_score_kernel" in row["Kernel_Name"] and row["Counter_Name"] == "FETCH_SIZE":
+                        if is_score_kernel(row["Kernel_Name"]) and row["Counter_Name"] == "FETCH_SIZE":
                             vals.append(float(row["Counter_Value"]))
         if not vals:
-            return None, "no fused_score_kernel FETCH_SIZE rows"
+            return None, "no similarity-kernel FETCH_SIZE rows"
         return round(statistics.median(vals) * 1024 * 2), (
             f"rocprofv3 --pmc FETCH_SIZE child pass, median of {len(vals)} fused launches, x1024 B/KiB x2 (gfx950)")
     except Exception as e:  # never fail the benchmark on the profiler

@@ -24,10 +24,12 @@
  *   - Scores: RR_METRIC_DOT = fp32 dot product (SimpleRetriever, retriever.py:112);
  *     RR_METRIC_COSINE = clip(dot / (|q|*|d| + 1e-8), -1, 1) in the reference's fp32 operation order
  *     (retriever.py:600-609).
- *   - Sharding: the corpus rows are split into contiguous shards, one per device. Shards live either in
- *     one process (rr_create with n_dev > 1; RCCL communicator from ncclCommInitAll) or one per process
- *     (rr_init_dist; RCCL communicator from a unique id). Per-shard top-k candidates are exchanged with
- *     a single ncclAllGather and merged on device; every rank ends with the global result.
+ *   - Sharding: the corpus rows are split into contiguous shards. Shards live either one per process
+ *     (rr_init_dist; RCCL communicator from a unique id; per-shard top-k candidates exchanged with one
+ *     ncclAllGather over xGMI) or all in one process (rr_create with n_dev > 1; the candidates are
+ *     exchanged by peer DMA copies ordered with events; a device may repeat, several shards then
+ *     share it). Either way every shard merges the same candidate set on device and ends with the
+ *     global result, bit-identical for any shard count.
  */
 #ifndef RAG_RETRIEVAL_H
 #define RAG_RETRIEVAL_H
@@ -75,7 +77,8 @@ typedef struct rr_handle rr_handle;
 
 /* ---- lifecycle ---------------------------------------------------------------------------------- */
 
-/* Create a handle over n_dev local devices (HIP ordinals). devices == NULL means {0}.
+/* Create a handle over n_dev local shards on the given devices (HIP ordinals, repeats allowed).
+ * devices == NULL means {0}.
  * Replaces CupyRetriever.__init__'s device setup (retriever.py:580-586). */
 int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** out);
 
@@ -147,6 +150,16 @@ int rr_fetch_results(rr_handle* h, float* out_scores, int64_t* out_idx);
  * copy into every local shard's query buffer (skips the reference's .cpu().numpy() round trip,
  * batch_processor.py:92). dev_q is a device pointer on the handle's first local device. */
 int rr_set_queries_device(rr_handle* h, const float* dev_q, int32_t b, int32_t d);
+
+/* ---- kernel selection (diagnostics / A-B tests) --------------------------------------------------- */
+
+#define RR_KERNEL_AUTO  0   /* split-K LDS-DMA kernel where the shape allows it (d*elem/8 a multiple of
+                               128 bytes, at most 512 bytes), else the register-streaming kernel */
+#define RR_KERNEL_FUSED 1   /* always the register-streaming kernel (fp32: f32 MFMA) */
+
+/* Choose the similarity kernel for k <= RR_FUSED_KMAX searches on this handle. Results of the two kernels
+ * differ only by fp32 summation order. */
+int rr_set_kernel(rr_handle* h, int kernel);
 
 /* ---- timing (benchmarks) ----------------------------------------------------------------------- */
 

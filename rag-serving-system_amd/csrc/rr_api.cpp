@@ -70,7 +70,9 @@ struct Shard {
   size_t full_cap = 0;                   // elements
   void* sort_temp = nullptr;
   size_t sort_temp_bytes = 0;
-  ncclComm_t comm = nullptr;
+  ncclComm_t comm = nullptr;             // multi-process mode (rr_init_dist)
+  hipEvent_t keys_ready = nullptr;       // single-process exchange: shard_keys written
+  hipEvent_t copies_done = nullptr;      // single-process exchange: this shard's peer copies issued+done
   std::vector<hipEvent_t> ev;            // timing event pairs (local shard 0 only)
   size_t ev_used = 0;
 
@@ -92,6 +94,7 @@ struct rr_handle {
   int32_t cur_b = 0;    // last staged batch
   int32_t last_k = 0;   // k of the last search
   bool timing = false;
+  int kernel = RR_KERNEL_AUTO;   // rr_set_kernel
   double t_ms = 0.0;
   int64_t t_count = 0;
 };
@@ -134,6 +137,8 @@ int free_shard(Shard& s) {
     if (p) hipFree(p);
   for (hipEvent_t e : s.ev) hipEventDestroy(e);
   s.ev.clear();
+  if (s.keys_ready) hipEventDestroy(s.keys_ready);
+  if (s.copies_done) hipEventDestroy(s.copies_done);
   if (s.comm) ncclCommDestroy(s.comm);
   if (s.stream) hipStreamDestroy(s.stream);
   s = Shard();
@@ -264,6 +269,21 @@ int ensure_buffers(rr_handle* h, int b, int k) {
   return RR_OK;
 }
 
+// Split-K kernel dtype for a public corpus dtype (rr_sk.hip): exact-split bf16x3 for fp32 storage.
+int sk_dtype_of(int dtype) {
+  switch (dtype) {
+    case RR_DTYPE_BF16: return rr::KDT_BF16;
+    case RR_DTYPE_F32_SPLIT: return rr::KDT_F32_SPLIT;
+    default: return rr::KDT_F32_X3;
+  }
+}
+
+// Whether the top-k (k <= RR_FUSED_KMAX) search runs the split-K kernel for this handle.
+bool use_sk(const rr_handle* h) {
+  if (h->kernel == RR_KERNEL_FUSED) return false;
+  return rr::sk_slabs(sk_dtype_of(h->dtype), h->d) != 0;
+}
+
 int fused_grid(const Shard& s) {
   const int64_t ntiles = (s.rows() + rr::kTileDocs - 1) / rr::kTileDocs;
   const int64_t want = (ntiles + rr::kWaves - 1) / rr::kWaves;
@@ -295,20 +315,51 @@ int collect_timing(rr_handle* h) {
   return RR_OK;
 }
 
+// Single-process exchange (several local shards, possibly on the same device): every shard copies every
+// other shard's [32][kk] keys into its `gathered` slot with peer DMA, ordered by events. The same
+// layout the RCCL all-gather produces in multi-process mode.
+int local_gather(rr_handle* h, int kk) {
+  const size_t bytes = (size_t)rr::kQSlots * kk * 8;
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    HIP_TRY(hipEventRecord(s.keys_ready, s.stream));
+  }
+  for (Shard& dst : h->shards) {
+    HIP_TRY(hipSetDevice(dst.dev));
+    for (size_t i = 0; i < h->shards.size(); ++i) {
+      const Shard& src = h->shards[i];
+      if (&src != &dst) HIP_TRY(hipStreamWaitEvent(dst.stream, src.keys_ready, 0));
+      HIP_TRY(hipMemcpyPeerAsync(dst.gathered + i * (size_t)rr::kQSlots * kk, dst.dev, src.shard_keys, src.dev, bytes,
+                                 dst.stream));
+    }
+    HIP_TRY(hipEventRecord(dst.copies_done, dst.stream));
+  }
+  return RR_OK;
+}
+
 // Enqueue the device pipeline for query block [q0, q0 + bb) on every local shard.
 int enqueue_block(rr_handle* h, int q0, int bb, int k) {
   const int d = h->d;
   const int kt = rr::fused_kt(k);
   const bool multi = h->world > 1;
+  const bool local_multi = multi && !h->dist;
   for (size_t si = 0; si < h->shards.size(); ++si) {
     Shard& s = h->shards[si];
     HIP_TRY(hipSetDevice(s.dev));
+    // before shard_keys is rewritten, the other shards' copies of its previous contents must be done
+    auto wait_copies = [&]() -> hipError_t {
+      if (local_multi)
+        for (const Shard& o : h->shards)
+          if (&o != &s)
+            if (hipError_t e = hipStreamWaitEvent(s.stream, o.copies_done, 0)) return e;
+      return hipSuccess;
+    };
     const float* qb = s.queries + (size_t)q0 * d;
     float* osc = s.out_scores + (size_t)q0 * k;
     int64_t* oix = s.out_idx + (size_t)q0 * k;
     const uint32_t base = (uint32_t)s.row_begin;
     if (kt) {
-      const int grid = fused_grid(s);
+      int grid = fused_grid(s);
       hipEvent_t e0 = nullptr, e1 = nullptr;
       const bool timed = h->timing && si == 0;
       if (timed) {
@@ -316,8 +367,15 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k) {
         HIP_TRY(hipEventRecord(e0, s.stream));
       }
       if (s.rows() > 0) {
-        HIP_TRY(rr::launch_fused(kdt_of(h->dtype), h->metric, kt, grid, s.corpus, s.norms, s.rscale, qb, s.rows(),
-                                 d, bb, base, s.cand, s.stream));
+        if (use_sk(h)) {
+          const int sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(s.cand_grid, (s.rows() + 31) / 32));
+          HIP_TRY(rr::launch_sk(sk_dtype_of(h->dtype), h->metric, kt, sgrid, s.corpus, s.norms, s.rscale, qb,
+                                s.rows(), d, bb, base, s.cand, s.stream));
+          grid = sgrid;
+        } else {
+          HIP_TRY(rr::launch_fused(kdt_of(h->dtype), h->metric, kt, grid, s.corpus, s.norms, s.rscale, qb,
+                                   s.rows(), d, bb, base, s.cand, s.stream));
+        }
       } else {
         HIP_TRY(hipMemsetAsync(s.cand, 0, (size_t)rr::kQSlots * kt * 8, s.stream));
       }
@@ -325,11 +383,13 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k) {
       if (!multi) {
         HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, nullptr, osc, oix, s.stream));
       } else {
+        HIP_TRY(wait_copies());
         HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, s.shard_keys, nullptr, nullptr, s.stream));
       }
     } else {
       // k > RR_FUSED_KMAX: all keys of this shard, segmented radix sort, keep the first k.
       const int64_t rows = s.rows();
+      HIP_TRY(wait_copies());
       HIP_TRY(hipMemsetAsync(s.shard_keys, 0, (size_t)rr::kQSlots * k * 8, s.stream));
       if (rows > 0) {
         const int grid = fused_grid(s);
@@ -344,14 +404,15 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k) {
   }
   if (!multi) return RR_OK;
 
-  // ---- exchange: one all-gather of every shard's [32][kk] candidate keys ---------------------------
+  // ---- exchange: every shard's [32][kk] candidate keys to every shard --------------------------------
   const int kk = kt ? kt : k;
-  NCCL_TRY(ncclGroupStart());
-  for (Shard& s : h->shards) {
+  if (h->dist) {   // one process per GPU: one RCCL all-gather over xGMI
+    Shard& s = h->shards[0];
     HIP_TRY(hipSetDevice(s.dev));
     NCCL_TRY(ncclAllGather(s.shard_keys, s.gathered, (size_t)rr::kQSlots * kk, ncclUint64, s.comm, s.stream));
+  } else if (int rc = local_gather(h, kk)) {
+    return rc;
   }
-  NCCL_TRY(ncclGroupEnd());
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
     float* osc = s.out_scores + (size_t)q0 * k;
@@ -416,15 +477,14 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
       return fail(RR_E_HIP, "device %d setup failed: %s", devices[i], hipGetErrorString(e));
     }
   }
-  if (n_dev > 1) {
-    std::vector<ncclComm_t> comms(n_dev);
-    std::vector<int> devs(devices, devices + n_dev);
-    ncclResult_t r = ncclCommInitAll(comms.data(), n_dev, devs.data());
-    if (r != ncclSuccess) {
+  for (Shard& s : h->shards) {   // single-process exchange events (unused with one shard)
+    hipError_t e = hipSetDevice(s.dev);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.keys_ready, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.copies_done, hipEventDisableTiming);
+    if (e != hipSuccess) {
       rr_destroy(h);
-      return fail(RR_E_RCCL, "ncclCommInitAll failed: %s", ncclGetErrorString(r));
+      return fail(RR_E_HIP, "event setup failed: %s", hipGetErrorString(e));
     }
-    for (int i = 0; i < n_dev; ++i) h->shards[i].comm = comms[i];
   }
   *out = h;
   return RR_OK;
@@ -642,6 +702,13 @@ int rr_search(rr_handle* h, const float* host_q, int32_t b, int32_t d, int32_t k
   if (int rc = rr_set_queries(h, host_q, b, d)) return rc;
   if (int rc = rr_search_staged(h, k)) return rc;
   return rr_fetch_results(h, out_scores, out_idx);
+}
+
+int rr_set_kernel(rr_handle* h, int kernel) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  if (kernel != RR_KERNEL_AUTO && kernel != RR_KERNEL_FUSED) return fail(RR_E_INVALID, "bad kernel %d", kernel);
+  h->kernel = kernel;
+  return RR_OK;
 }
 
 int rr_set_timing(rr_handle* h, int enable) {

@@ -1,0 +1,80 @@
+// rr_device.h — device-side helpers shared by the retrieval kernels (rr_kernels.hip, rr_sk.hip):
+// vector types, a compile-time loop, the 64-bit (score, index) keys and the per-lane top-KT list.
+//
+// Score/index keys. A candidate is one uint64: high 32 bits = order-preserving image of the fp32
+// score, low 32 bits = 0xFFFFFFFF - global_index. Unsigned key order == (score desc, index asc), the
+// deterministic tie rule of this implementation (the reference's tie order is implementation
+// defined: numpy introselect / CUB). Key 0 = empty slot.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+
+namespace rr {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// keys
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ord_of(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float float_of_ord(uint32_t o) {
+  const uint32_t u = (o & 0x80000000u) ? (o & 0x7fffffffu) : ~o;
+  return __uint_as_float(u);
+}
+__device__ __forceinline__ uint64_t make_key(float s, uint32_t gidx) {
+  return ((uint64_t)ord_of(s) << 32) | (uint64_t)(0xFFFFFFFFu - gidx);
+}
+__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
+// Per-lane sorted (descending) list of the KT best keys, fully in registers (static indexing only).
+template <int KT>
+struct TopK {
+  uint64_t v[KT];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int i = 0; i < KT; ++i) v[i] = 0;
+  }
+  __device__ __forceinline__ uint64_t last() const { return v[KT - 1]; }
+  // Branch-free insertion of x (caller checked x > last()).
+  __device__ __forceinline__ void insert(uint64_t x) {
+#pragma unroll
+    for (int i = KT - 1; i > 0; --i) {
+      const uint64_t up = v[i - 1];
+      v[i] = (x > up) ? up : umax64(x, v[i]);
+    }
+    v[0] = umax64(x, v[0]);
+  }
+  __device__ __forceinline__ void pop() {
+#pragma unroll
+    for (int i = 0; i < KT - 1; ++i) v[i] = v[i + 1];
+    v[KT - 1] = 0;
+  }
+};
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, off, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), off, 64);
+    x = umax64(x, ((uint64_t)hi << 32) | lo);
+  }
+  return x;
+}
+
+}  // namespace rr

@@ -22,6 +22,9 @@ constexpr int kGroupChunks = 8;   // 16-byte loads per lane kept in flight per p
 constexpr int KDT_F32_MFMA = 0;
 constexpr int KDT_BF16 = 1;
 constexpr int KDT_F32_SPLIT = 2;
+//   KDT_F32_X3   : fp32 rows, each value split exactly into three bf16 in registers, 6 bf16 MFMAs
+//                  (split-K kernel only; rr_sk.hip)
+constexpr int KDT_F32_X3 = 3;
 
 // Smallest fused-kernel list width KT >= k (4, 8, 16, 32); 0 if k > RR_FUSED_KMAX.
 int fused_kt(int k);
@@ -35,6 +38,14 @@ size_t fused_lds_bytes(int d, int kt, int kdt);
 hipError_t launch_fused(int kdt, int metric, int kt, int grid, const void* corpus, const float* norms,
                         const float* rscale, const float* queries, int64_t n, int d, int b, uint32_t idx_base,
                         uint64_t* cand, hipStream_t s);
+
+// Split-K streaming kernel (rr_sk.hip): same output contract as launch_fused. sdt = KDT_* (0..3).
+// sk_slabs(sdt, d) = 128-byte slabs per wave per row (1..4; bf16 1..2), 0 if d is not supported.
+int sk_slabs(int sdt, int d);
+size_t sk_lds_bytes(int sdt, bool cos);
+hipError_t launch_sk(int sdt, int metric, int kt, int grid, const void* corpus, const float* norms,
+                     const float* rscale, const float* queries, int64_t n, int d, int b, uint32_t idx_base,
+                     uint64_t* cand, hipStream_t s);
 
 // Merge nlists candidate lists laid out [nlists][32][in_kt] into the top-kt per query.
 // out_keys [32][kt] (may be null); out_scores/out_idx [b][k_out] (may be null).

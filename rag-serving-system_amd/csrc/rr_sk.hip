@@ -1,0 +1,457 @@
+// rr_sk.hip — split-K streaming kernel: similarity + top-k in one corpus pass, the corpus staged through
+// LDS by non-temporal LDS-DMA (gfx950 / MI355X).
+//
+// Same contract as fused_score_kernel (rr_kernels.hip; reference retriever.py:594-611 + :742-769): one
+// workgroup per CU computes the (32 doc x 32 query) score blocks of its rows and keeps a top-KT per
+// query; cand[blockIdx][32][KT] goes to merge_kernel. What changes is how the corpus reaches the MFMAs:
+//
+//   * The workgroup owns ONE contiguous row range and walks it in 32-row tiles. Wave w owns bytes
+//     [w*KS, (w+1)*KS) of every row (KS = row bytes / 8): a split of the dot product's K dimension over
+//     the 8 waves, so each wave's slice of all 32 queries fits in its VGPRs (no LDS query image).
+//   * A wave moves its slice of a tile in 4-KiB slabs (32 rows x 128 contiguous bytes) with
+//     `global_load_lds_dwordx4 ... nt`: 8 rows x 128 B per instruction. Measured on MI355X
+//     (tools/kbench.hip): non-temporal loads of >= 128 contiguous bytes per row per instruction stream
+//     at 6.9-7.1 TB/s, the default-policy / 32-byte-per-row register loads of fused_score_kernel at
+//     6.2-6.3. The LDS image is source-swizzled (16-byte column c of row r lands at c ^ (r & 7)) so the
+//     MFMA-shaped ds_read_b128 of 32 rows is conflict-free.
+//   * Two slab slots per wave: slab s + 1 is in flight while slab s is read and multiplied (counted
+//     vmcnt; LDS-DMA has no VGPR destination, so nothing hipcc allocates can be hit by a landing load).
+//   * Per tile the 8 K-partials are summed through LDS (double-buffered, one raw s_barrier per tile)
+//     in a fixed order; wave w then runs the metric epilogue for queries 4w..4w+3 (2 rows x 1 query
+//     per lane) and a per-lane top-KT insert. At the end each query's 16 lane lists are merged with
+//     shuffles.
+//
+// Kernel dtypes (template DT), all reading the storage formats rr_api.cpp writes:
+//   0 fp32 rows (pair_unit order), v_mfma_f32_32x32x2_f32: a plain fmaf chain per K-slice.
+//   1 bf16 rows (pair_unit order), v_mfma_f32_32x32x16_bf16 against the query's bf16 hi + lo.
+//   2 split-f16 rows (hi/lo per 8 elements), 3 x v_mfma_f32_32x32x16_f16, exact 2^e rescale.
+//   3 fp32 rows (pair_unit order), each fp32 value split EXACTLY into three bf16 (x = b0 + b1 + b2,
+//     round-to-nearest splits), the query likewise; 6 bf16 MFMAs (b0c0 b0c1 b1c0 b1c1 b0c2 b2c0): every
+//     partial product is exact in fp32 and the dropped terms (b1c2, b2c1, b2c2) are below 2^-23 |x q|
+//     (unbiased), the size of one fp32 rounding per product, so a score carries fp32 summation error
+//     only. Half of DT 0's matrix-core cycles (and no f32-MFMA clock throttling).
+// The K order inside a wave's slice is a permutation applied identically to both operands.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "rr_device.h"
+#include "rr_internal.h"
+
+namespace rr {
+namespace sk {
+
+constexpr int kSlabRowBytes = 128;                // contiguous bytes of one row per slab
+constexpr int kSlabBytes = 32 * kSlabRowBytes;    // 4 KiB
+constexpr int kRing = 2;                          // slab slots per wave
+constexpr int kRedStride = 36;                    // floats per (wave, query) block of 32 rows (+4 pad)
+constexpr int kSegRows = 1024;                    // rows of per-doc factors held in LDS at a time
+constexpr size_t kRingBytes = (size_t)kWaves * kRing * kSlabBytes;                  // 64 KiB
+constexpr size_t kRedBytes = (size_t)2 * kWaves * kQSlots * kRedStride * 4;         // 72 KiB
+
+// storage position P (16-byte unit of a pair_unit-ordered row) -> logical unit
+__device__ __forceinline__ int inv_pair(int p) { return (p & ~3) | ((p & 1) << 1) | ((p >> 1) & 1); }
+
+// One 16-byte-per-lane LDS-DMA load, non-temporal. M0 (the LDS destination base) is written and restored
+// in the same statement (cdna_hip_programming.md, inline-asm rules). The leading lgkmcnt(0) retires this
+// wave's ds_reads of the slot being overwritten (issued one iteration earlier).
+__device__ __forceinline__ void glds16(const void* src, unsigned lds) {
+  unsigned keep;
+  asm volatile(
+      "s_waitcnt lgkmcnt(0)\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// LDS writes of this wave visible, then the workgroup barrier (no vmcnt: slabs stay in flight across it)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// two fp32 -> packed bf16 (round to nearest even), a in the low half
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// x = b0 + b1 + b2 exactly: three round-to-nearest bf16 splits (b0 = bf16(x), b1 = bf16(x - b0),
+// b2 = x - b0 - b1; each residual is exact in fp32 and the last one fits bf16's 8 significant bits).
+// |b1| <= 2^-8 |x|, |b2| <= 2^-16 |x|. 11 VALU ops per pair of values.
+__device__ __forceinline__ void split3(const float (&x)[8], bf16x8& b0, bf16x8& b1, bf16x8& b2) {
+  u32x4 p0, p1, p2;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = x[2 * i], b = x[2 * i + 1];
+    p0[i] = cvt_pk_bf16(a, b);
+    const float ra = a - __uint_as_float(p0[i] << 16), rb = b - __uint_as_float(p0[i] & 0xFFFF0000u);
+    p1[i] = cvt_pk_bf16(ra, rb);
+    const float sa = ra - __uint_as_float(p1[i] << 16), sb = rb - __uint_as_float(p1[i] & 0xFFFF0000u);
+    p2[i] = cvt_pk_bf16(sa, sb);
+  }
+  b0 = __builtin_bit_cast(bf16x8, p0);
+  b1 = __builtin_bit_cast(bf16x8, p1);
+  b2 = __builtin_bit_cast(bf16x8, p2);
+}
+
+// Query operand (B) fragments of one wave's K-slice, per slab j and K-step.
+template <int DT, int NS>
+struct QFrag;
+template <int NS>
+struct QFrag<0, NS> { float v[NS][16]; };                     // per MFMA m: one fp32
+template <int NS>
+struct QFrag<1, NS> { bf16x8 hi[NS][4], lo[NS][4]; };         // 4 K-steps of 16 bf16 per slab
+template <int NS>
+struct QFrag<2, NS> { f16x8 hi[NS][2], lo[NS][2]; };          // 2 K-steps of 16 per slab
+template <int NS>
+struct QFrag<3, NS> { bf16x8 c0[NS][2], c1[NS][2], c2[NS][2]; };
+
+
+// LDS byte offset (within a slot) of 16-byte column position cp of tile row r (swizzled image)
+__device__ __forceinline__ int slab_off(int r, int cp) { return (r >> 3) * 1024 + (r & 7) * 128 + ((cp ^ (r & 7)) << 4); }
+
+template <int DT, int NS, int KT, bool COS>
+__global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict__ corpus,
+                                                          const float* __restrict__ norms,
+                                                          const float* __restrict__ rscale,
+                                                          const float* __restrict__ queries, int64_t n, int d,
+                                                          int b, uint32_t idx_base, uint64_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  constexpr int EB = DT == 1 ? 2 : 4;                           // storage bytes per element
+  const int row_bytes = d * EB;
+  constexpr int KS = NS * kSlabRowBytes;                        // bytes of a row per wave
+  const int p0 = w * (KS / 16);                                 // first 16-byte storage unit of the slice
+
+  float* red = (float*)(smem + kRingBytes);
+  constexpr int SW = (COS ? 1 : 0) + (DT == 2 ? 1 : 0);          // per-doc floats in the segment
+  float* seg = (float*)(smem + kRingBytes + kRedBytes);
+  float* qinfo = seg + kSegRows * (SW > 0 ? SW : 1);            // [32] |q|, [32] 2^-e (split), [32] int e
+  int* qexp = (int*)(qinfo + 2 * kQSlots);
+
+  // ---- per-query scalars: |q| (cosine, fp32 as cp.linalg.norm, retriever.py:602) and split exponents
+  if (COS || DT == 2) {
+    for (int q = w * 4; q < w * 4 + 4; ++q) {
+      float ss = 0.f, m = 0.f;
+      if (q < b)
+        for (int c = lane; c < (d >> 2); c += 64) {
+          const f32x4 v = ((const f32x4*)queries)[(size_t)q * (d >> 2) + c];
+          ss = fmaf(v.x, v.x, ss); ss = fmaf(v.y, v.y, ss); ss = fmaf(v.z, v.z, ss); ss = fmaf(v.w, v.w, ss);
+          m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        ss += __shfl_xor(ss, off, 64);
+        m = fmaxf(m, __shfl_xor(m, off, 64));
+      }
+      int E = 0;
+      if (m > 0.f) frexpf(m, &E);
+      const int ex = m > 0.f ? 15 - E : 0;
+      if (lane == 0) {
+        qinfo[q] = sqrtf(ss);
+        qinfo[kQSlots + q] = ldexpf(1.0f, -ex);
+        qexp[q] = ex;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- this wave's K-slice of every query as MFMA B operands (lane: query r, K half h) ----------------
+  QFrag<DT, NS> qf;
+  {
+    const bool qv = r < b;
+    const float* qrow = queries + (size_t)(qv ? r : 0) * d;
+    auto qval = [&](int e) -> float { return qv ? qrow[e] : 0.f; };
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      if constexpr (DT == 0) {
+        // MFMA m of slab j: lane half h holds position 4h + (m >> 2), element m & 3
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+          const int P = p0 + 8 * j + 4 * h + (m >> 2);
+          qf.v[j][m] = qval(4 * inv_pair(P) + (m & 3));
+        }
+      } else if constexpr (DT == 1) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {   // K-step t: lane half h reads position 2t + h (8 bf16)
+          const int L = inv_pair(p0 + 8 * j + 2 * t + h);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float x = qval(8 * L + e);
+            const __bf16 bh = (__bf16)x;
+            qf.hi[j][t][e] = bh;
+            qf.lo[j][t][e] = (__bf16)(x - (float)bh);
+          }
+        }
+      } else if constexpr (DT == 2) {
+        const int ex = qv ? qexp[r] : 0;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {   // K-step t: lane half h reads units 4t + 2h (hi), + 1 (lo)
+          const int g8 = (p0 + 8 * j + 4 * t + 2 * h) >> 1;   // 8-element group
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float xs = ldexpf(qval(8 * g8 + e), ex);
+            const _Float16 fh = (_Float16)xs;
+            qf.hi[j][t][e] = fh;
+            qf.lo[j][t][e] = (_Float16)(xs - (float)fh);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {   // K-step t: lane half h reads positions 4t + 2h, 4t + 2h + 1
+          float x[8];
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int L = inv_pair(p0 + 8 * j + 4 * t + 2 * h + u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[4 * u + e] = qval(4 * L + e);
+          }
+          split3(x, qf.c0[j][t], qf.c1[j][t], qf.c2[j][t]);
+        }
+      }
+    }
+  }
+
+  // ---- this workgroup's rows ----------------------------------------------------------------------------
+  const int64_t G = gridDim.x, g = blockIdx.x;
+  const int64_t per = n / G, rem = n % G;
+  const int64_t r0 = g * per + (g < rem ? g : rem);
+  const int64_t r1 = r0 + per + (g < rem ? 1 : 0);
+  const int64_t ntile = (r1 - r0 + 31) / 32;
+
+  // epilogue lane mapping: query qe = 4w + lane / 16, tile rows 2 (lane % 16) + {0, 1}
+  const int qe = 4 * w + (lane >> 4), er = 2 * (lane & 15);
+  const bool qev = qe < b;
+  const float qn = COS ? qinfo[qe] : 0.f;
+  const float qs = DT == 2 ? qinfo[kQSlots + qe] : 1.f;
+
+  TopK<KT> tk;
+  tk.init();
+
+  // LDS-DMA lane mapping: instruction i of a slab covers tile rows 8i + lane/8, 16-byte column
+  // (lane % 8) ^ (lane / 8) of the slab — so the image holds column c of row r at c ^ (r & 7)
+  const int rl = lane >> 3, cl = lane & 7;
+  const unsigned ring_lds = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(smem + (size_t)w * kRing * kSlabBytes));
+  const char* ring = smem + (size_t)w * kRing * kSlabBytes;
+  const char* lane_src = corpus + (size_t)w * KS + ((cl ^ rl) << 4);
+
+  auto issue = [&](int64_t tile, int j, int slot) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int64_t row = r0 + tile * 32 + 8 * i + rl;
+      row = row < r1 ? row : r1 - 1;                  // partial last tile: re-read a valid row
+      glds16(lane_src + row * row_bytes + j * kSlabRowBytes, ring_lds + slot * kSlabBytes + i * 1024);
+    }
+  };
+
+  int64_t seg_lo = INT64_MIN / 2;
+  if (ntile > 0) issue(0, 0, 0);
+  int slot = 0;
+  for (int64_t tile = 0; tile < ntile; ++tile) {
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    static_for<0, NS>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      // keep one slab in flight: issue the next one, then wait for this one (4 loads younger remain)
+      const bool more = j + 1 < NS || tile + 1 < ntile;
+      if (more) {
+        issue(j + 1 < NS ? tile : tile + 1, j + 1 < NS ? j + 1 : 0, slot ^ 1);
+        wait_vm<4>();
+      } else {
+        wait_vm<0>();
+      }
+      const char* sl = ring + slot * kSlabBytes;
+      if constexpr (DT == 0) {
+        f32x4 a[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = *(const f32x4*)(sl + slab_off(r, 4 * h + i));
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m >> 2][m & 3], qf.v[j][m], acc, 0, 0, 0);
+      } else if constexpr (DT == 1) {
+        bf16x8 a[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) a[t] = *(const bf16x8*)(sl + slab_off(r, 2 * t + h));
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], qf.hi[j][t], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], qf.lo[j][t], acc, 0, 0, 0);
+        }
+      } else if constexpr (DT == 2) {
+        f16x8 ah[2], al[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          ah[t] = *(const f16x8*)(sl + slab_off(r, 4 * t + 2 * h));
+          al[t] = *(const f16x8*)(sl + slab_off(r, 4 * t + 2 * h + 1));
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t], qf.hi[j][t], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t], qf.lo[j][t], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[t], qf.hi[j][t], acc, 0, 0, 0);
+        }
+      } else {
+        f32x4 a[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = *(const f32x4*)(sl + slab_off(r, 4 * (i >> 1) + 2 * h + (i & 1)));
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const float x[8] = {a[2 * t].x, a[2 * t].y, a[2 * t].z, a[2 * t].w,
+                              a[2 * t + 1].x, a[2 * t + 1].y, a[2 * t + 1].z, a[2 * t + 1].w};
+          bf16x8 b0, b1, b2;
+          split3(x, b0, b1, b2);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qf.c0[j][t], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qf.c1[j][t], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qf.c0[j][t], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qf.c1[j][t], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qf.c2[j][t], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, qf.c0[j][t], acc, 0, 0, 0);
+        }
+      }
+      slot ^= 1;
+    });
+
+    // ---- sum the 8 K-partials of this tile (fixed order), then the metric epilogue --------------------
+    float* rb = red + (size_t)(tile & 1) * kWaves * kQSlots * kRedStride;
+#pragma unroll
+    for (int a4 = 0; a4 < 4; ++a4) {   // C/D map: acc[4a + i] = (doc 8a + 4h + i, query r)
+      const f32x4 v = {acc[4 * a4], acc[4 * a4 + 1], acc[4 * a4 + 2], acc[4 * a4 + 3]};
+      *(f32x4*)(rb + (w * kQSlots + r) * kRedStride + 8 * a4 + 4 * h) = v;
+    }
+    lds_barrier();
+    const int64_t tb = r0 + tile * 32;
+    if constexpr (SW > 0) {
+      if (tb < seg_lo || tb + 32 > seg_lo + kSegRows) {   // workgroup-uniform: refill the per-doc factors
+        seg_lo = tb;
+        for (int i = tid; i < kSegRows; i += kThreads) {
+          int64_t row = tb + i;
+          row = row < r1 ? row : r1 - 1;
+          if constexpr (COS && DT == 2) {
+            seg[2 * i] = norms[row];
+            seg[2 * i + 1] = rscale[row];
+          } else if constexpr (COS) {
+            seg[i] = norms[row];
+          } else {
+            seg[i] = rscale[row];
+          }
+        }
+        lds_barrier();
+      }
+    }
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < kWaves; ++ww) {
+      const float2 p = *(const float2*)(rb + (ww * kQSlots + qe) * kRedStride + er);
+      s0 += p.x;
+      s1 += p.y;
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int64_t row = tb + er + e;
+      float s = e ? s1 : s0;
+      const int64_t li = row - seg_lo;
+      if constexpr (DT == 2) s = s * (COS ? seg[2 * li + 1] : seg[li]) * qs;   // exact 2^e rescales
+      if constexpr (COS) {
+        // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
+        const float nd = DT == 2 ? seg[2 * li] : seg[li];
+        s = s / (qn * nd + 1e-8f);
+        s = fminf(fmaxf(s, -1.0f), 1.0f);
+      }
+      const uint64_t key = make_key(s, idx_base + (uint32_t)row);
+      if (qev && row < r1 && key > tk.last()) tk.insert(key);
+    }
+  }
+
+  // ---- per query: merge its 16 lane lists (KT rounds of a 16-lane max; keys are unique) ---------------
+  uint64_t* dst = out + ((size_t)g * kQSlots + qe) * KT;
+#pragma unroll 1
+  for (int rnd = 0; rnd < KT; ++rnd) {
+    uint64_t m = tk.v[0];
+#pragma unroll
+    for (int off = 8; off >= 1; off >>= 1) {
+      const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)m, off, 64);
+      const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(m >> 32), off, 64);
+      m = umax64(m, ((uint64_t)hi << 32) | lo);
+    }
+    if (m != 0 && tk.v[0] == m) tk.pop();
+    if ((lane & 15) == 0) dst[rnd] = m;
+  }
+}
+
+template <int DT, int NS, int KT, bool COS>
+hipError_t launch_t(int grid, const void* c, const float* nr, const float* rs, const float* q, int64_t n, int d,
+                    int b, uint32_t base, uint64_t* out, hipStream_t s) {
+  auto kern = sk_score_kernel<DT, NS, KT, COS>;
+  const size_t lds = sk_lds_bytes(DT, COS);
+  if (hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds))
+    return e;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, (const char*)c, nr, rs, q, n, d, b, base, out);
+  return hipGetLastError();
+}
+
+template <int DT, int NS, bool COS>
+hipError_t launch_kt(int kt, int grid, const void* c, const float* nr, const float* rs, const float* q, int64_t n,
+                     int d, int b, uint32_t base, uint64_t* out, hipStream_t s) {
+  switch (kt) {
+    case 4: return launch_t<DT, NS, 4, COS>(grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 8: return launch_t<DT, NS, 8, COS>(grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 16: return launch_t<DT, NS, 16, COS>(grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 32: return launch_t<DT, NS, 32, COS>(grid, c, nr, rs, q, n, d, b, base, out, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int DT, bool COS>
+hipError_t launch_ns(int ns, int kt, int grid, const void* c, const float* nr, const float* rs, const float* q,
+                     int64_t n, int d, int b, uint32_t base, uint64_t* out, hipStream_t s) {
+  switch (ns) {
+    case 1: return launch_kt<DT, 1, COS>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 2: return launch_kt<DT, 2, COS>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 3: if constexpr (DT != 1) return launch_kt<DT, 3, COS>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
+            else return hipErrorInvalidValue;
+    case 4: if constexpr (DT != 1) return launch_kt<DT, 4, COS>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
+            else return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace sk
+
+size_t sk_lds_bytes(int sdt, bool cos) {
+  const int sw = (cos ? 1 : 0) + (sdt == 2 ? 1 : 0);
+  return sk::kRingBytes + sk::kRedBytes + (size_t)sk::kSegRows * (sw > 0 ? sw : 1) * 4 + 3 * kQSlots * 4;
+}
+
+int sk_slabs(int sdt, int d) {
+  const int eb = sdt == 1 ? 2 : 4;
+  const int ks = d * eb / kWaves;   // row bytes per wave
+  if (d <= 0 || ks % sk::kSlabRowBytes != 0) return 0;
+  const int ns = ks / sk::kSlabRowBytes;
+  return (ns >= 1 && ns <= (sdt == 1 ? 2 : 4)) ? ns : 0;
+}
+
+hipError_t launch_sk(int sdt, int metric, int kt, int grid, const void* c, const float* nr, const float* rs,
+                     const float* q, int64_t n, int d, int b, uint32_t base, uint64_t* cand, hipStream_t s) {
+  const int ns = sk_slabs(sdt, d);
+  if (!ns || b < 1 || b > kQSlots || n < 1) return hipErrorInvalidValue;
+  switch (sdt) {
+    case 0: return metric ? sk::launch_ns<0, true>(ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s)
+                          : sk::launch_ns<0, false>(ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+    case 1: return metric ? sk::launch_ns<1, true>(ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s)
+                          : sk::launch_ns<1, false>(ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+    case 2: return metric ? sk::launch_ns<2, true>(ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s)
+                          : sk::launch_ns<2, false>(ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+    case 3: return metric ? sk::launch_ns<3, true>(ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s)
+                          : sk::launch_ns<3, false>(ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace rr

@@ -36,6 +36,8 @@ RR_SYNTH_EXACT_INT = 0
 RR_SYNTH_UNIT_NORM = 1
 RR_UNIQUE_ID_BYTES = 128
 RR_FUSED_KMAX = 32
+RR_KERNEL_AUTO = 0
+RR_KERNEL_FUSED = 1
 RR_ABI_VERSION = 1
 
 DTYPES = {"fp32": RR_DTYPE_F32, "float32": RR_DTYPE_F32, "f32": RR_DTYPE_F32,
@@ -64,6 +66,7 @@ SIGNATURES = {
     "rr_synchronize": (_c_int, [_vp]),
     "rr_fetch_results": (_c_int, [_vp, _fp, _i64p]),
     "rr_set_queries_device": (_c_int, [_vp, _vp, _c_i32, _c_i32]),
+    "rr_set_kernel": (_c_int, [_vp, _c_int]),
     "rr_set_timing": (_c_int, [_vp, _c_int]),
     "rr_kernel_time": (_c_int, [_vp, ctypes.POINTER(ctypes.c_double), _i64p, _c_int]),
 }
@@ -248,6 +251,10 @@ class Index:
         idx = np.empty((b, k), dtype=np.int64)
         _check(self._lib.rr_fetch_results(self._h, _fptr(scores), _i64ptr(idx)))
         return scores, idx
+
+    def set_kernel(self, kernel: str) -> None:
+        """'auto' (split-K LDS-DMA kernel where the shape allows) or 'fused' (register-streaming kernel)."""
+        _check(self._lib.rr_set_kernel(self._h, {"auto": RR_KERNEL_AUTO, "fused": RR_KERNEL_FUSED}[kernel]))
 
     def set_timing(self, enable: bool) -> None:
         _check(self._lib.rr_set_timing(self._h, 1 if enable else 0))

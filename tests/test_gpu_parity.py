@@ -192,6 +192,7 @@ def test_unit_norm_corpus_bf16(Index, golden_synth, f3_small, metric, flav):
 SHAPES = [  # (n, d, b, k)
     (1, 64, 1, 1), (31, 64, 3, 5), (33, 128, 32, 4), (100, 1024, 33, 8), (1000, 1024, 70, 17),
     (4097, 256, 5, 32), (5000, 128, 2, 33), (777, 64, 9, 64), (50, 128, 4, 80), (20000, 1024, 32, 16),
+    (3001, 512, 17, 10), (2500, 768, 32, 3), (40000, 1024, 8, 32),
 ]
 
 
@@ -312,3 +313,124 @@ def test_1m_unit_norm_against_reference(Index, golden_synth):
     ix.load(bf)
     scores, idx = ix.search(q, 10)
     check_topk(idx, scores, golden_synth["f3bf_1m_k10_simple_idx"], bf, q, "dot")
+
+
+# ---- row sharding inside one process (several shards on cuda:0, peer-copy exchange) ----------------
+@pytest.mark.parametrize("shards", [2, 3, 8])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp32-split"])
+def test_sharded_equals_single(Index, shards, dtype):
+    """Row shards (rr_create with repeated devices) exchange candidates by peer copy and merge on every
+    shard: results must be bit-identical to one shard's for every k path (fused <= 32, sort > 32)."""
+    rng = np.random.default_rng(shards * 7 + len(dtype))
+    n, d = 5003, 256
+    corpus = rng.standard_normal((n, d)).astype(np.float32)
+    q = rng.standard_normal((45, d)).astype(np.float32)     # two 32-query blocks
+    for metric in ("dot", "cosine"):
+        one = Index(devices=[0], dtype=dtype, metric=metric)
+        one.load(corpus)
+        many = Index(devices=[0] * shards, dtype=dtype, metric=metric)
+        many.load(corpus)
+        bounds = [many.shard_range(i) for i in range(shards)]
+        per = -(-n // shards)
+        assert bounds == [(min(n, i * per), min(n, (i + 1) * per)) for i in range(shards)]
+        for k in (1, 5, 32, 40):
+            s1, i1 = one.search(q, k)
+            s2, i2 = many.search(q, k)
+            assert np.array_equal(i1, i2), (metric, k)
+            assert np.array_equal(s1, s2), (metric, k)
+        one.close()
+        many.close()
+
+
+def test_sharded_more_shards_than_rows(Index):
+    corpus = np.arange(3 * 64, dtype=np.float32).reshape(3, 64) / 100.0
+    q = np.ones((2, 64), np.float32)
+    ix = Index(devices=[0] * 5, dtype="fp32", metric="dot")
+    ix.load(corpus)
+    for k in (2, 4, 40):
+        scores, idx = ix.search(q, k)
+        assert list(idx[0][:3]) == [2, 1, 0][:k]
+        assert np.all(idx[:, 3:] == -1)
+
+
+def test_sharded_staged_repeat_and_synthetic(Index):
+    """Back-to-back staged searches reuse the exchange buffers (event ordering), and the device
+    generator fills each shard from global row indices."""
+    one = Index(devices=[0], dtype="fp32", metric="cosine")
+    one.fill_synthetic(1, 42, 20000, 512)
+    many = Index(devices=[0, 0, 0, 0], dtype="fp32", metric="cosine")
+    many.fill_synthetic(1, 42, 20000, 512)
+    q = np.random.default_rng(1).standard_normal((32, 512)).astype(np.float32)
+    ref = one.search(q, 8)
+    many.set_queries(q)
+    for _ in range(20):
+        many.search_staged(8)
+    s, i = many.fetch()
+    assert np.array_equal(i, ref[1]) and np.array_equal(s, ref[0])
+    assert np.array_equal(many.read_rows(9999, 3), one.read_rows(9999, 3))
+
+
+# ---- the two similarity kernels (split-K LDS-DMA vs register streaming) ------------------------------
+SK_SHAPES = [  # (n, d, b, k): split-K eligible for fp32 / fp32-split at d % 256 == 0, bf16 at d % 512 == 0
+    (1, 256, 1, 1), (33, 256, 3, 4), (1000, 512, 32, 8), (31, 1024, 32, 5), (12345, 1024, 20, 16),
+    (2049, 768, 7, 32), (70000, 1024, 32, 5),
+]
+
+
+@pytest.mark.parametrize("n,d,b,k", SK_SHAPES)
+@pytest.mark.parametrize("metric", ["dot", "cosine"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp32-split"])
+def test_split_k_kernel_matches_register_kernel_and_oracle(Index, n, d, b, k, metric, dtype):
+    if dtype == "bf16" and d % 512:
+        pytest.skip("split-K bf16 needs d % 512 == 0")
+    rng = np.random.default_rng(n + 7 * d + b + k)
+    corpus = rng.standard_normal((n, d)).astype(np.float32) * rng.uniform(0.5, 2, size=(n, 1)).astype(np.float32)
+    q = rng.standard_normal((b, d)).astype(np.float32)
+    if dtype == "bf16":
+        corpus = synth.bf16_round(corpus)
+    ix = Index(dtype=dtype, metric=metric)
+    ix.load(corpus)
+    s_sk, i_sk = ix.search(q, k)
+    ix.set_kernel("fused")
+    s_rk, i_rk = ix.search(q, k)
+    _, cidx = canonical_topk(exact_scores(corpus, q, metric), k)
+    tol = 1e-3 * (np.sqrt(d) if metric == "dot" else 1.0)
+    for idx, scores in ((i_sk, s_sk), (i_rk, s_rk)):
+        check_topk(idx, scores, cidx, corpus, q, metric, near_tie=1e-5 * np.sqrt(d), score_tol=tol)
+    agree = np.mean(i_sk == i_rk)
+    assert agree >= 0.98, agree
+    np.testing.assert_allclose(s_sk, s_rk, rtol=0, atol=2e-5 * (np.sqrt(d) if metric == "dot" else 1.0))
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp32-split"])
+def test_split_k_exact_integer_bit_exact(Index, golden_synth, f2_small, dtype):
+    """Exact-integer corpus: the split-K kernel's K-partial sums are exact, so scores equal fp64."""
+    corpus, q = f2_small
+    ix = get_index(Index, "f2_small", corpus, dtype, "dot")
+    for kernel in ("auto", "fused"):
+        ix.set_kernel(kernel)
+        scores, idx = ix.search(q, 10)
+        val, cidx = canonical_topk(exact_scores(corpus, q, "dot"), 10)
+        assert np.array_equal(scores.astype(np.float64), val), kernel
+        assert np.array_equal(idx, cidx), kernel
+    ix.set_kernel("auto")
+
+
+def test_split_k_fp32_error_is_fp32_class(Index):
+    """fp32 storage through the split-K kernel (exact three-way bf16 split, 6 MFMAs): score error against
+    fp64 stays within a few fp32 roundings of sum |x q| — the same class as an fp32 FMA chain."""
+    rng = np.random.default_rng(11)
+    n, d = 4096, 1024
+    corpus = rng.standard_normal((n, d)).astype(np.float32)
+    q = rng.standard_normal((32, d)).astype(np.float32)
+    ix = Index(dtype="fp32", metric="dot")
+    ix.load(corpus)
+    scores, idx = ix.search(q, 32)
+    ix.set_kernel("fused")
+    s_f, i_f = ix.search(q, 32)
+    c64, q64 = corpus.astype(np.float64), q.astype(np.float64)
+    for sc, ii in ((scores, idx), (s_f, i_f)):
+        exact = np.einsum("bd,bkd->bk", q64, c64[ii])
+        mag = np.einsum("bd,bkd->bk", np.abs(q64), np.abs(c64[ii]))
+        rel = np.abs(sc - exact) / mag
+        assert rel.max() < 2.0 ** -19, rel.max()

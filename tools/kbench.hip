@@ -5,6 +5,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I rag-serving-system_amd/csrc \
 //         tools/kbench.hip -o tools/kbench && tools/kbench [n_docs] [rounds]
 #include "../rag-serving-system_amd/csrc/rr_kernels.hip"
+#include "../rag-serving-system_amd/csrc/rr_sk.hip"
 
 #include <cstdio>
 #include <cstdlib>
@@ -62,6 +63,147 @@ __global__ __launch_bounds__(512) void stream_lin(const u32x4* __restrict__ c, i
   out[gw * 64 + lane] = acc;
 }
 
+// (c) LDS-DMA stream: each wave moves 1 KiB pieces of its contiguous range into its own LDS ring with
+// global_load_lds_dwordx4 (R pieces in flight, counted vmcnt), then reads each piece back (ds_read_b128).
+template <int R, int NT>
+__global__ __launch_bounds__(512) void stream_glds(const u32x4* __restrict__ c, int64_t n16, unsigned* out) {
+  extern __shared__ __attribute__((aligned(16))) char ring_smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t nwave = (int64_t)gridDim.x * 8, gw = (int64_t)blockIdx.x * 8 + wid;
+  const int64_t per = n16 / nwave / 64 * 64, b0 = gw * per;   // 16-byte units, whole pieces
+  const int64_t npieces = per / 64;
+  u32x4* ring = (u32x4*)ring_smem + wid * R * 64;
+  const unsigned ring_base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)ring);
+  unsigned acc = 0;
+  auto issue = [&](int64_t p) {
+    const u32x4* src = c + b0 + p * 64 + lane;
+    const unsigned dst = ring_base + (unsigned)((p % R) * 1024);
+    unsigned keep;
+    if constexpr (NT)
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+    else
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+  };
+  for (int64_t p = 0; p < R - 1 && p < npieces; ++p) issue(p);
+  for (int64_t p = 0; p < npieces; ++p) {
+    if (p + R - 1 < npieces) {
+      issue(p + R - 1);
+      asm volatile("s_waitcnt vmcnt(%0)" :: "i"(R - 1) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const u32x4 v = ring[(p % R) * 64 + lane];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  out[gw * 64 + lane] = acc;
+}
+template <int NT>
+__global__ __launch_bounds__(512) void stream_lin_nt(const u32x4* __restrict__ c, int64_t n16, unsigned* out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwave = (int64_t)gridDim.x * 8, gw = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 6);
+  const int64_t per = n16 / nwave, b0 = gw * per;
+  unsigned acc = 0;
+  for (int64_t i = b0 + lane; i + 64 * 7 < b0 + per; i += 64 * 8) {
+    u32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(c + i + 64 * u);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  out[gw * 64 + lane] = acc;
+}
+
+// (d) nt loads with LPR lanes per row (16*LPR contiguous bytes of a row per instruction, 64/LPR rows),
+// a wave sweeping a block of rows column-chunk by column-chunk (U instructions in flight).
+template <int LPR, int NT>
+__global__ __launch_bounds__(512) void stream_pat(const u32x4* __restrict__ c, int64_t n, int d, unsigned* out) {
+  const int lane = threadIdx.x & 63;
+  constexpr int RPI = 64 / LPR;                  // rows per instruction
+  const int upr = d >> 2;                        // 16-byte units per row
+  const int64_t nwave = (int64_t)gridDim.x * 8, gw = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 6);
+  const int64_t per = n / nwave / 32 * 32, b0 = gw * per;
+  unsigned acc = 0;
+  const int rl = lane / LPR, cl = lane % LPR;
+  for (int64_t base = b0; base < b0 + per; base += 32) {
+    // 32 rows x upr units: instruction i covers rows (i % (32/RPI))*RPI + rl, column chunk (i / (32/RPI))
+    constexpr int RB = 32 / RPI;
+    const int nin = RB * (upr / LPR);
+    for (int i0 = 0; i0 < nin; i0 += 8) {
+      u32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u;
+        const int64_t row = base + (i % RB) * RPI + rl;
+        const u32x4* p = c + row * upr + (i / RB) * LPR + cl;
+        v[u] = NT ? __builtin_nontemporal_load(p) : *p;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+  }
+  out[gw * 64 + lane] = acc;
+}
+
+// (e) split-K streaming skeleton: a workgroup walks its contiguous rows in 32-row tiles; wave w owns bytes
+// [w*KS, (w+1)*KS) of every row and moves them in 4-KiB slabs (32 rows x 128 B, 4 LDS-DMA instructions of
+// 8 rows x 128 B, source-swizzled) through an RS-slot LDS ring, then reads MFMA-shaped fragments
+// (lane (r, h): 16 B of row r) back with ds_read_b128. A raw s_barrier per tile stands in for the
+// cross-wave reduction.
+__device__ __forceinline__ void glds16(const void* src, unsigned lds, int nt) {
+  unsigned keep;
+  if (nt)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
+}
+template <int RS, int NT, int BAR>
+__global__ __launch_bounds__(512) void stream_sk(const char* __restrict__ c, int64_t n, int row_bytes, unsigned* out) {
+  extern __shared__ __attribute__((aligned(16))) char sk_smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int KS = row_bytes / 8, nslab = KS / 128;
+  const int64_t per = n / gridDim.x / 32 * 32, b0 = (int64_t)blockIdx.x * per;
+  const int64_t ntile = per / 32, total = ntile * nslab;
+  char* ring = sk_smem + wid * RS * 4096;
+  const unsigned ring_lds = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)ring);
+  const int rl = lane >> 3, cl = lane & 7;
+  auto issue = [&](int64_t s) {
+    const int64_t t = s / nslab;
+    const int j = (int)(s - t * nslab);
+    const unsigned slot = ring_lds + (unsigned)((s % RS) * 4096);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = b0 + t * 32 + 8 * i + rl;
+      const char* src = c + row * row_bytes + wid * KS + j * 128 + ((cl ^ rl) << 4);
+      glds16(src, slot + i * 1024, NT);
+    }
+  };
+  unsigned acc = 0;
+  const int r = lane & 31, h = lane >> 5;
+  for (int64_t s = 0; s < RS - 1 && s < total; ++s) issue(s);
+  for (int64_t s = 0; s < total; ++s) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       // previous slab's ds_reads done (slot reuse)
+    if (s + RS - 1 < total) {
+      issue(s + RS - 1);
+      asm volatile("s_waitcnt vmcnt(%0)" :: "i"(4 * (RS - 1)) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const char* slot = ring + (s % RS) * 4096;
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      const int chunk = 2 * cc + h;
+      const u32x4 v = *(const u32x4*)(slot + (r >> 3) * 1024 + (r & 7) * 128 + ((chunk ^ (r & 7)) << 4));
+      acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (BAR && (s % nslab) == nslab - 1) __builtin_amdgcn_s_barrier();
+  }
+  out[((int64_t)blockIdx.x * 8 + wid) * 64 + lane] = acc;
+}
+
 struct Variant {
   std::string name;
   int dtype;
@@ -117,9 +259,10 @@ int main(int argc, char** argv) {
     [&](const void* c, uint64_t* o) { return launch_fused_t<1, 8, COS, 0, NB, LM, AS, DBG, U>(grid, c, norms, rscale, q, n, d, b, 0, o, s); }, {}}
 #define VS(NB, LM, AS, COS, DBG, U) Variant{"fp32-split NB=" #NB " LM=" #LM " AS=" #AS " COS=" #COS " DBG=" #DBG " U=" #U, 2, \
     [&](const void* c, uint64_t* o) { return launch_fused_t<2, 8, COS, 0, NB, LM, AS, DBG, U>(grid, c, norms2, rscale, q, n, d, b, 0, o, s); }, {}}
-  std::vector<Variant> vs = {V32(2, 1, 1, true, 0, 8), V32(2, 1, 1, true, 1, 8), V32(3, 1, 1, true, 0, 8), V32(2, 1, 1, true, 0, 4), VS(2, 1, 1, true, 0, 8), VS(2, 1, 1, false, 0, 8),
-                             VS(2, 1, 1, true, 2, 8), V16(2, 1, 1, true, 0, 8), V16(3, 1, 1, true, 0, 8),
-                             V16(2, 1, 1, false, 0, 8), V16(2, 1, 1, true, 1, 8)};
+#define VK(DT, BUF, COS) Variant{"sk DT=" #DT " COS=" #COS, BUF, \
+    [&](const void* c, uint64_t* o) { return launch_sk(DT, COS, 8, grid, c, DT == 2 ? norms2 : norms, rscale, q, n, d, b, 0, o, s); }, {}}
+  std::vector<Variant> vs = {V32(2, 1, 1, true, 0, 8), VS(2, 1, 1, true, 0, 8), V16(2, 1, 1, true, 0, 8),
+                             VK(3, 0, 1), VK(4, 0, 1), VK(2, 2, 1), VK(1, 1, 1), VK(3, 0, 0), VK(4, 0, 0)};
   std::vector<Variant> streams = {
       Variant{"stream frag U=8 fp32", 0, [&](const void* c, uint64_t*) {
         hipLaunchKernelGGL(stream_frag<8>, dim3(grid), dim3(512), 0, s, (const u32x4*)c, n, d, sink);
@@ -132,10 +275,59 @@ int main(int argc, char** argv) {
       Variant{"stream lin fp32", 0, [&](const void* c, uint64_t*) {
         hipLaunchKernelGGL(stream_lin, dim3(grid), dim3(512), 0, s, (const u32x4*)c, n * d / 4, sink);
         return hipGetLastError(); }, {}},
+      Variant{"stream glds R=8 default", 0, [&](const void* c, uint64_t*) {
+        hipLaunchKernelGGL((stream_glds<8, 0>), dim3(grid), dim3(512), 8 * 8 * 1024, s, (const u32x4*)c, n * d / 4, sink);
+        return hipGetLastError(); }, {}},
+      Variant{"stream glds R=8 nt", 0, [&](const void* c, uint64_t*) {
+        hipLaunchKernelGGL((stream_glds<8, 1>), dim3(grid), dim3(512), 8 * 8 * 1024, s, (const u32x4*)c, n * d / 4, sink);
+        return hipGetLastError(); }, {}},
+      Variant{"stream glds R=16 nt", 0, [&](const void* c, uint64_t*) {
+        hipLaunchKernelGGL((stream_glds<16, 1>), dim3(grid), dim3(512), 8 * 16 * 1024, s, (const u32x4*)c, n * d / 4, sink);
+        return hipGetLastError(); }, {}},
+      Variant{"stream glds R=4 nt", 0, [&](const void* c, uint64_t*) {
+        hipLaunchKernelGGL((stream_glds<4, 1>), dim3(grid), dim3(512), 8 * 4 * 1024, s, (const u32x4*)c, n * d / 4, sink);
+        return hipGetLastError(); }, {}},
+      Variant{"stream lin nt-builtin", 0, [&](const void* c, uint64_t*) {
+        hipLaunchKernelGGL(stream_lin_nt<1>, dim3(grid), dim3(512), 0, s, (const u32x4*)c, n * d / 4, sink);
+        return hipGetLastError(); }, {}},
+      Variant{"stream sk RS=2 nt=1 bar=1", 0, [&](const void* c, uint64_t*) {
+        hipLaunchKernelGGL((stream_sk<2, 1, 1>), dim3(grid), dim3(512), 8 * 2 * 4096, s, (const char*)c, n, d * 4, sink);
+        return hipGetLastError(); }, {}},
+      Variant{"stream sk bf16 RS=2 nt=1 bar=1", 1, [&](const void* c, uint64_t*) {
+        hipLaunchKernelGGL((stream_sk<2, 1, 1>), dim3(grid), dim3(512), 8 * 2 * 4096, s, (const char*)c, n, d * 2, sink);
+        return hipGetLastError(); }, {}},
+      Variant{"stream sk RS=3 nt=1 bar=1", 0, [&](const void* c, uint64_t*) {
+        hipLaunchKernelGGL((stream_sk<3, 1, 1>), dim3(grid), dim3(512), 8 * 3 * 4096, s, (const char*)c, n, d * 4, sink);
+        return hipGetLastError(); }, {}},
+      Variant{"stream sk bf16 RS=3 nt=1 bar=1", 1, [&](const void* c, uint64_t*) {
+        hipLaunchKernelGGL((stream_sk<3, 1, 1>), dim3(grid), dim3(512), 8 * 3 * 4096, s, (const char*)c, n, d * 2, sink);
+        return hipGetLastError(); }, {}},
+      Variant{"stream sk RS=4 nt=1 bar=1", 0, [&](const void* c, uint64_t*) {
+        hipLaunchKernelGGL((stream_sk<4, 1, 1>), dim3(grid), dim3(512), 8 * 4 * 4096, s, (const char*)c, n, d * 4, sink);
+        return hipGetLastError(); }, {}},
+      Variant{"stream sk bf16 RS=4 nt=1 bar=1", 1, [&](const void* c, uint64_t*) {
+        hipLaunchKernelGGL((stream_sk<4, 1, 1>), dim3(grid), dim3(512), 8 * 4 * 4096, s, (const char*)c, n, d * 2, sink);
+        return hipGetLastError(); }, {}},
+      Variant{"stream sk RS=2 nt=0 bar=1", 0, [&](const void* c, uint64_t*) {
+        hipLaunchKernelGGL((stream_sk<2, 0, 1>), dim3(grid), dim3(512), 8 * 2 * 4096, s, (const char*)c, n, d * 4, sink);
+        return hipGetLastError(); }, {}},
+      Variant{"stream sk bf16 RS=2 nt=0 bar=1", 1, [&](const void* c, uint64_t*) {
+        hipLaunchKernelGGL((stream_sk<2, 0, 1>), dim3(grid), dim3(512), 8 * 2 * 4096, s, (const char*)c, n, d * 2, sink);
+        return hipGetLastError(); }, {}},
+      Variant{"stream sk RS=3 nt=1 bar=0", 0, [&](const void* c, uint64_t*) {
+        hipLaunchKernelGGL((stream_sk<3, 1, 0>), dim3(grid), dim3(512), 8 * 3 * 4096, s, (const char*)c, n, d * 4, sink);
+        return hipGetLastError(); }, {}},
+      Variant{"stream sk bf16 RS=3 nt=1 bar=0", 1, [&](const void* c, uint64_t*) {
+        hipLaunchKernelGGL((stream_sk<3, 1, 0>), dim3(grid), dim3(512), 8 * 3 * 4096, s, (const char*)c, n, d * 2, sink);
+        return hipGetLastError(); }, {}},
       Variant{"stream lin x4grid fp32", 0, [&](const void* c, uint64_t*) {
         hipLaunchKernelGGL(stream_lin, dim3(grid * 4), dim3(512), 0, s, (const u32x4*)c, n * d / 4, sink);
         return hipGetLastError(); }, {}},
   };
+  CK(hipFuncSetAttribute((const void*)stream_glds<16, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 16 * 1024));
+  CK(hipFuncSetAttribute((const void*)stream_sk<3, 1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 3 * 4096));
+  CK(hipFuncSetAttribute((const void*)stream_sk<3, 1, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 3 * 4096));
+  CK(hipFuncSetAttribute((const void*)stream_sk<4, 1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 4 * 4096));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));

@@ -18,7 +18,8 @@ for f in glob.glob(os.path.join(stats_dir, "**", "*kernel_stats.csv"), recursive
 vals = []
 for f in glob.glob(os.path.join(pmc_dir, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        if "fused_score_kernel" in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE":
+        if ("sk_score_kernel" in r["Kernel_Name"] or "fused_score_kernel" in r["Kernel_Name"]) \
+                and r["Counter_Name"] == "FETCH_SIZE":
             vals.append(float(r["Counter_Value"]))
 if vals:
     b = statistics.median(vals) * 1024 * 2
