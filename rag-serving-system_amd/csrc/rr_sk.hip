@@ -71,11 +71,15 @@ __device__ __forceinline__ void wait_vm() {
 // LDS writes of this wave visible, then the workgroup barrier (no vmcnt: slabs stay in flight across it)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// two fp32 -> packed bf16 (round to nearest even), a in the low half
+// two fp32 -> packed bf16 (round to nearest even), a in the low half. A plain conversion: hipcc emits
+// v_cvt_pk_bf16_f32 for it on gfx950 AND pads its hazards. (An inline-asm v_cvt_pk here fed the MFMAs
+// with one wait state where a VALU write -> MFMA operand read needs two: hipcc pads asm outputs by one
+// state only, and the MFMA intermittently read the previous value of the register — a ~1e-4 relative
+// score error on a few launches.)
 __device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
-  uint32_t r;
-  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
 }
 
 // x = b0 + b1 + b2 exactly: three round-to-nearest bf16 splits (b0 = bf16(x), b1 = bf16(x - b0),

@@ -81,17 +81,21 @@ def test_missing_library_fails_loudly(tmp_path):
 
 
 def test_inline_asm_loads_are_hazard_free():
-    """Every fused-kernel instantiation: no compiler instruction writes a VGPR that an in-flight
-    inline-asm corpus load will still land in (tools/check_asm_loads.py; the hazard of
-    cdna_hip_programming.md §5.7 item 1). Needs the gfx950 .s from `make isa`."""
+    """Every fused / split-K kernel instantiation: no compiler instruction writes a VGPR that an in-flight
+    inline-asm corpus load will still land in, and no VALU result comes out of inline asm (hipcc pads an
+    asm output by one wait state; an MFMA operand needs two) — tools/check_asm_loads.py, the hazards of
+    cdna_hip_programming.md §5.7 items 1-2. Needs the gfx950 .s from `make isa`."""
     pkg = _lib.PKG_ROOT
-    s_file = os.path.join(pkg, "build", "isa", "rr_kernels-hip-amdgcn-amd-amdhsa-gfx950.s")
-    src = os.path.join(pkg, "csrc", "rr_kernels.hip")
-    if not os.path.exists(s_file) or os.path.getmtime(s_file) < os.path.getmtime(src):
-        subprocess.check_call(["make", "-C", pkg, "isa"], stdout=subprocess.DEVNULL)
-    syms = re.findall(r"^(_ZN2rr18fused_score_kernel\w+):", open(s_file).read(), flags=re.M)
-    assert len(syms) >= 16
     checker = os.path.join(os.path.dirname(pkg), "tools", "check_asm_loads.py")
-    for sym in syms:
-        r = subprocess.run(["python3", checker, s_file, sym], capture_output=True, text=True)
-        assert r.returncode == 0, r.stdout
+    for unit, pattern, least in (("rr_kernels", r"_ZN2rr18fused_score_kernel\w+", 16),
+                                 ("rr_sk", r"_ZN2rr2sk15sk_score_kernel\w+", 16)):
+        s_file = os.path.join(pkg, "build", "isa", f"{unit}-hip-amdgcn-amd-amdhsa-gfx950.s")
+        src = os.path.join(pkg, "csrc", f"{unit}.hip")
+        deps = [src, os.path.join(pkg, "csrc", "rr_device.h")]
+        if not os.path.exists(s_file) or os.path.getmtime(s_file) < max(map(os.path.getmtime, deps)):
+            subprocess.check_call(["make", "-C", pkg, "isa"], stdout=subprocess.DEVNULL)
+        syms = re.findall(rf"^({pattern}):", open(s_file).read(), flags=re.M)
+        assert len(syms) >= least, (unit, len(syms))
+        for sym in syms:
+            r = subprocess.run(["python3", checker, s_file, sym], capture_output=True, text=True)
+            assert r.returncode == 0, (sym, r.stdout)

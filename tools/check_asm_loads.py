@@ -40,6 +40,10 @@ for i in range(start, end):
         n_asm += inasm
         continue
     if inasm:
+        # item 2 of the same section: hipcc pads an asm statement's outputs by one wait state only, but a
+        # VALU write -> MFMA operand read needs two; so no VALU result may come out of inline asm
+        if re.match(r"v_(?!mfma)\w+\s", t):
+            bad.append((i + 1, "VALU inside inline asm: " + t))
         continue
     # any compiler instruction that reads or writes an in-flight destination (incl. spills)
     if not fifo or t.startswith((";", ".", "s_")) or not t:
