@@ -189,7 +189,7 @@ def main() -> None:
         traffic, traffic_note = pmc_traffic(args)
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline:   # rank 0 at N=1 only
             threads = min(16, os.cpu_count() or 1)
             cpu = cpu_baseline(args.docs, args.dim, args.batch, args.k, args.cpu_batches, threads)
         value = args.batch * args.steps / elapsed

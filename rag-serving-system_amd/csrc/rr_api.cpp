@@ -61,6 +61,15 @@ struct Shard {
   int cand_grid = 0;
   uint64_t* shard_keys = nullptr;        // [32][k_cap] this shard's top-k (all-gather send buffer)
   uint64_t* gathered = nullptr;          // [world][32][k_cap] (all-gather receive buffer)
+  // pipelined exchange (k <= RR_FUSED_KMAX, world > 1): the exchange of search i (all-gather + final
+  // merge) runs on xstream while the compute stream already scores search i + 1; buffers alternate by
+  // parity. px_keys[p] / px_gathered[p] are [32][KMAX] / [world][32][KMAX].
+  hipStream_t xstream = nullptr;
+  uint64_t* px_keys[2] = {nullptr, nullptr};
+  uint64_t* px_gathered[2] = {nullptr, nullptr};
+  hipEvent_t ev_keys[2] = {nullptr, nullptr};   // compute stream: px_keys[p] written
+  hipEvent_t ev_xdone[2] = {nullptr, nullptr};  // xstream: exchange of parity p finished (buffers free)
+  hipEvent_t ev_cdone = nullptr;                // compute stream: a serial (k > KMAX) exchange finished
   float* out_scores = nullptr;           // [q_cap][k_cap]
   int64_t* out_idx = nullptr;            // [q_cap][k_cap]
   int k_cap = 0;
@@ -95,6 +104,7 @@ struct rr_handle {
   int32_t last_k = 0;   // k of the last search
   bool timing = false;
   int kernel = RR_KERNEL_AUTO;   // rr_set_kernel
+  int parity = 0;                // pipelined exchange: buffer set of the next search block
   double t_ms = 0.0;
   int64_t t_count = 0;
 };
@@ -132,13 +142,16 @@ int dmalloc(T** p, size_t bytes) {
 int free_shard(Shard& s) {
   hipSetDevice(s.dev);
   void* ptrs[] = {s.corpus, s.norms, s.rscale, s.queries, s.cand, s.shard_keys, s.gathered, s.out_scores, s.out_idx,
-                  s.full_keys, s.sorted, s.sort_temp};
+                  s.full_keys, s.sorted, s.sort_temp, s.px_keys[0], s.px_keys[1], s.px_gathered[0], s.px_gathered[1]};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (hipEvent_t e : s.ev) hipEventDestroy(e);
   s.ev.clear();
   if (s.keys_ready) hipEventDestroy(s.keys_ready);
   if (s.copies_done) hipEventDestroy(s.copies_done);
+  for (hipEvent_t e : {s.ev_keys[0], s.ev_keys[1], s.ev_xdone[0], s.ev_xdone[1], s.ev_cdone})
+    if (e) hipEventDestroy(e);
+  if (s.xstream) hipStreamDestroy(s.xstream);
   if (s.comm) ncclCommDestroy(s.comm);
   if (s.stream) hipStreamDestroy(s.stream);
   s = Shard();
@@ -250,6 +263,12 @@ int ensure_buffers(rr_handle* h, int b, int k) {
       s.cand_grid = s.cus;
       if (int rc = dmalloc(&s.cand, (size_t)s.cand_grid * rr::kQSlots * RR_FUSED_KMAX * 8)) return rc;
     }
+    if (h->world > 1 && !s.px_keys[0]) {
+      for (int p = 0; p < 2; ++p) {
+        if (int rc = dmalloc(&s.px_keys[p], (size_t)rr::kQSlots * RR_FUSED_KMAX * 8)) return rc;
+        if (int rc = dmalloc(&s.px_gathered[p], (size_t)h->world * rr::kQSlots * RR_FUSED_KMAX * 8)) return rc;
+      }
+    }
     if (k > RR_FUSED_KMAX) {
       const size_t need = (size_t)rr::kQSlots * std::max<int64_t>(s.rows(), (int64_t)h->world * k);
       if (need > s.full_cap) {
@@ -337,12 +356,44 @@ int local_gather(rr_handle* h, int kk) {
   return RR_OK;
 }
 
+// Pipelined exchange (k <= RR_FUSED_KMAX, world > 1) of the search block just scored into px_keys[p]:
+// each shard's xstream gathers every shard's [32][kt] list (one RCCL all-gather over xGMI with one
+// process per GPU, peer copies within one process) into px_gathered[p] and merges it into the results,
+// while the compute stream goes on with the next block. px_keys[p] is rewritten two blocks later and only
+// after ev_xdone[p] of every shard that read it (enqueue_block).
+int enqueue_exchange_px(rr_handle* h, int p, int q0, int bb, int k, int kt) {
+  const size_t slot = (size_t)rr::kQSlots * kt;
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    HIP_TRY(hipEventRecord(s.ev_keys[p], s.stream));
+  }
+  for (Shard& dst : h->shards) {
+    HIP_TRY(hipSetDevice(dst.dev));
+    if (h->dist) {
+      HIP_TRY(hipStreamWaitEvent(dst.xstream, dst.ev_keys[p], 0));
+      NCCL_TRY(ncclAllGather(dst.px_keys[p], dst.px_gathered[p], slot, ncclUint64, dst.comm, dst.xstream));
+    } else {
+      for (size_t i = 0; i < h->shards.size(); ++i) {
+        const Shard& src = h->shards[i];
+        HIP_TRY(hipStreamWaitEvent(dst.xstream, src.ev_keys[p], 0));
+        HIP_TRY(hipMemcpyPeerAsync(dst.px_gathered[p] + i * slot, dst.dev, src.px_keys[p], src.dev, slot * 8,
+                                   dst.xstream));
+      }
+    }
+    HIP_TRY(rr::launch_merge(kt, dst.px_gathered[p], h->world, kt, bb, k, nullptr, dst.out_scores + (size_t)q0 * k,
+                             dst.out_idx + (size_t)q0 * k, dst.xstream));
+    HIP_TRY(hipEventRecord(dst.ev_xdone[p], dst.xstream));
+  }
+  return RR_OK;
+}
+
 // Enqueue the device pipeline for query block [q0, q0 + bb) on every local shard.
 int enqueue_block(rr_handle* h, int q0, int bb, int k) {
   const int d = h->d;
   const int kt = rr::fused_kt(k);
   const bool multi = h->world > 1;
   const bool local_multi = multi && !h->dist;
+  const int p = h->parity;
   for (size_t si = 0; si < h->shards.size(); ++si) {
     Shard& s = h->shards[si];
     HIP_TRY(hipSetDevice(s.dev));
@@ -352,6 +403,14 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k) {
         for (const Shard& o : h->shards)
           if (&o != &s)
             if (hipError_t e = hipStreamWaitEvent(s.stream, o.copies_done, 0)) return e;
+      return hipSuccess;
+    };
+    // pipelined exchange: px_keys[p] is rewritten only after every exchange that read it has finished
+    // (its own all-gather; within one process also the other shards' peer copies of it)
+    auto wait_px = [&](int par) -> hipError_t {
+      for (const Shard& o : h->shards)
+        if (&o == &s || local_multi)
+          if (hipError_t e = hipStreamWaitEvent(s.stream, o.ev_xdone[par], 0)) return e;
       return hipSuccess;
     };
     const float* qb = s.queries + (size_t)q0 * d;
@@ -383,12 +442,17 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k) {
       if (!multi) {
         HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, nullptr, osc, oix, s.stream));
       } else {
-        HIP_TRY(wait_copies());
-        HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, s.shard_keys, nullptr, nullptr, s.stream));
+        HIP_TRY(wait_px(p));
+        HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, s.px_keys[p], nullptr, nullptr, s.stream));
       }
     } else {
-      // k > RR_FUSED_KMAX: all keys of this shard, segmented radix sort, keep the first k.
+      // k > RR_FUSED_KMAX: all keys of this shard, segmented radix sort, keep the first k. The exchange
+      // is serial on the compute stream, after every pipelined exchange still writing results.
       const int64_t rows = s.rows();
+      if (multi) {
+        HIP_TRY(wait_px(0));
+        HIP_TRY(wait_px(1));
+      }
       HIP_TRY(wait_copies());
       HIP_TRY(hipMemsetAsync(s.shard_keys, 0, (size_t)rr::kQSlots * k * 8, s.stream));
       if (rows > 0) {
@@ -403,9 +467,14 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k) {
     }
   }
   if (!multi) return RR_OK;
+  if (kt) {
+    if (int rc = enqueue_exchange_px(h, p, q0, bb, k, kt)) return rc;
+    h->parity ^= 1;
+    return RR_OK;
+  }
 
-  // ---- exchange: every shard's [32][kk] candidate keys to every shard --------------------------------
-  const int kk = kt ? kt : k;
+  // ---- serial exchange (k > RR_FUSED_KMAX): every shard's [32][k] keys to every shard -----------------
+  const int kk = k;
   if (h->dist) {   // one process per GPU: one RCCL all-gather over xGMI
     Shard& s = h->shards[0];
     HIP_TRY(hipSetDevice(s.dev));
@@ -417,16 +486,15 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k) {
     HIP_TRY(hipSetDevice(s.dev));
     float* osc = s.out_scores + (size_t)q0 * k;
     int64_t* oix = s.out_idx + (size_t)q0 * k;
-    if (kt) {
-      HIP_TRY(rr::launch_merge(kt, s.gathered, h->world, kt, bb, k, nullptr, osc, oix, s.stream));
-    } else {
-      const int64_t seg = (int64_t)h->world * k;
-      HIP_TRY(rr::launch_regroup(s.gathered, h->world, k, bb, s.full_keys, s.stream));
-      size_t tb = s.sort_temp_bytes;
-      HIP_TRY(rr::segmented_sort_desc(s.sort_temp, &tb, s.full_keys, s.sorted, bb, seg, s.stream));
-      HIP_TRY(rr::launch_take_prefix(s.sorted, bb, seg, k, s.shard_keys, s.stream));
-      HIP_TRY(rr::launch_decode(s.shard_keys, bb, k, osc, oix, s.stream));
-    }
+    const int64_t seg = (int64_t)h->world * k;
+    HIP_TRY(rr::launch_regroup(s.gathered, h->world, k, bb, s.full_keys, s.stream));
+    size_t tb = s.sort_temp_bytes;
+    HIP_TRY(rr::segmented_sort_desc(s.sort_temp, &tb, s.full_keys, s.sorted, bb, seg, s.stream));
+    HIP_TRY(rr::launch_take_prefix(s.sorted, bb, seg, k, s.shard_keys, s.stream));
+    HIP_TRY(rr::launch_decode(s.shard_keys, bb, k, osc, oix, s.stream));
+    // later pipelined exchanges write the results after this one
+    HIP_TRY(hipEventRecord(s.ev_cdone, s.stream));
+    HIP_TRY(hipStreamWaitEvent(s.xstream, s.ev_cdone, 0));
   }
   return RR_OK;
 }
@@ -481,6 +549,9 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
     hipError_t e = hipSetDevice(s.dev);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.keys_ready, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.copies_done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.xstream, hipStreamNonBlocking);
+    for (hipEvent_t* ev : {&s.ev_keys[0], &s.ev_keys[1], &s.ev_xdone[0], &s.ev_xdone[1], &s.ev_cdone})
+      if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e != hipSuccess) {
       rr_destroy(h);
       return fail(RR_E_HIP, "event setup failed: %s", hipGetErrorString(e));
@@ -681,6 +752,7 @@ int rr_synchronize(rr_handle* h) {
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
     HIP_TRY(hipStreamSynchronize(s.stream));
+    HIP_TRY(hipStreamSynchronize(s.xstream));
   }
   return collect_timing(h);
 }

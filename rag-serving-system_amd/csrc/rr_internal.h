@@ -41,11 +41,15 @@ hipError_t launch_fused(int kdt, int metric, int kt, int grid, const void* corpu
 
 // Split-K streaming kernel (rr_sk.hip): same output contract as launch_fused. sdt = KDT_* (0..3).
 // sk_slabs(sdt, d) = 128-byte slabs per wave per row (1..4; bf16 1..2), 0 if d is not supported.
+// ring = LDS slab slots per wave (0 = kSkRing). Shipped: 2. A third slot (builds with RR_SK_RING3) needs a
+// single-buffered K-partial block and a second barrier per tile; on MI355X it ran 5 % slower for fp32
+// storage and within 1 % for bf16 / fp32-split (profiles/r01/kbench_ring.log).
+constexpr int kSkRing = 2;
 int sk_slabs(int sdt, int d);
-size_t sk_lds_bytes(int sdt, bool cos);
+size_t sk_lds_bytes(int sdt, bool cos, int ring);
 hipError_t launch_sk(int sdt, int metric, int kt, int grid, const void* corpus, const float* norms,
                      const float* rscale, const float* queries, int64_t n, int d, int b, uint32_t idx_base,
-                     uint64_t* cand, hipStream_t s);
+                     uint64_t* cand, hipStream_t s, int ring = 0);
 
 // Merge nlists candidate lists laid out [nlists][32][in_kt] into the top-kt per query.
 // out_keys [32][kt] (may be null); out_scores/out_idx [b][k_out] (may be null).

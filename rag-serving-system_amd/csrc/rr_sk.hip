@@ -41,11 +41,18 @@ namespace sk {
 
 constexpr int kSlabRowBytes = 128;                // contiguous bytes of one row per slab
 constexpr int kSlabBytes = 32 * kSlabRowBytes;    // 4 KiB
-constexpr int kRing = 2;                          // slab slots per wave
 constexpr int kRedStride = 36;                    // floats per (wave, query) block of 32 rows (+4 pad)
 constexpr int kSegRows = 1024;                    // rows of per-doc factors held in LDS at a time
-constexpr size_t kRingBytes = (size_t)kWaves * kRing * kSlabBytes;                  // 64 KiB
-constexpr size_t kRedBytes = (size_t)2 * kWaves * kQSlots * kRedStride * 4;         // 72 KiB
+
+// Ring of RS slab slots per wave: RS - 1 slabs stay in flight while one is multiplied. With RS = 2 the
+// K-partial block is double-buffered (one barrier per tile); with RS = 3 (2 x 32 KiB more ring) it is
+// single-buffered to fit 160 KiB, and a second barrier before the next tile's partials are written
+// (normally passed without waiting: a whole tile of MFMAs lies between it and the reads it guards).
+__host__ __device__ constexpr size_t ring_bytes(int rs) { return (size_t)kWaves * rs * kSlabBytes; }
+__host__ __device__ constexpr int red_bufs(int rs) { return rs == 2 ? 2 : 1; }
+__host__ __device__ constexpr size_t red_bytes(int rs) {
+  return (size_t)red_bufs(rs) * kWaves * kQSlots * kRedStride * 4;
+}
 
 // storage position P (16-byte unit of a pair_unit-ordered row) -> logical unit
 __device__ __forceinline__ int inv_pair(int p) { return (p & ~3) | ((p & 1) << 1) | ((p >> 1) & 1); }
@@ -117,12 +124,13 @@ struct QFrag<3, NS> { bf16x8 c0[NS][2], c1[NS][2], c2[NS][2]; };
 // LDS byte offset (within a slot) of 16-byte column position cp of tile row r (swizzled image)
 __device__ __forceinline__ int slab_off(int r, int cp) { return (r >> 3) * 1024 + (r & 7) * 128 + ((cp ^ (r & 7)) << 4); }
 
-template <int DT, int NS, int KT, bool COS>
+template <int DT, int NS, int KT, bool COS, int RS>
 __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict__ corpus,
                                                           const float* __restrict__ norms,
                                                           const float* __restrict__ rscale,
                                                           const float* __restrict__ queries, int64_t n, int d,
                                                           int b, uint32_t idx_base, uint64_t* __restrict__ out) {
+  static_assert(RS == 2 || RS == 3, "ring depth 2 or 3 (the tail waits are written for these)");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -132,9 +140,9 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
   constexpr int KS = NS * kSlabRowBytes;                        // bytes of a row per wave
   const int p0 = w * (KS / 16);                                 // first 16-byte storage unit of the slice
 
-  float* red = (float*)(smem + kRingBytes);
+  float* red = (float*)(smem + ring_bytes(RS));
   constexpr int SW = (COS ? 1 : 0) + (DT == 2 ? 1 : 0);          // per-doc floats in the segment
-  float* seg = (float*)(smem + kRingBytes + kRedBytes);
+  float* seg = (float*)(smem + ring_bytes(RS) + red_bytes(RS));
   float* qinfo = seg + kSegRows * (SW > 0 ? SW : 1);            // [32] |q|, [32] 2^-e (split), [32] int e
   int* qexp = (int*)(qinfo + 2 * kQSlots);
 
@@ -240,8 +248,8 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
   // LDS-DMA lane mapping: instruction i of a slab covers tile rows 8i + lane/8, 16-byte column
   // (lane % 8) ^ (lane / 8) of the slab — so the image holds column c of row r at c ^ (r & 7)
   const int rl = lane >> 3, cl = lane & 7;
-  const unsigned ring_lds = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(smem + (size_t)w * kRing * kSlabBytes));
-  const char* ring = smem + (size_t)w * kRing * kSlabBytes;
+  const unsigned ring_lds = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(smem + (size_t)w * RS * kSlabBytes));
+  const char* ring = smem + (size_t)w * RS * kSlabBytes;
   const char* lane_src = corpus + (size_t)w * KS + ((cl ^ rl) << 4);
 
   auto issue = [&](int64_t tile, int j, int slot) {
@@ -254,18 +262,28 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
   };
 
   int64_t seg_lo = INT64_MIN / 2;
-  if (ntile > 0) issue(0, 0, 0);
-  int slot = 0;
+  const int64_t total = ntile * NS;                   // slabs this wave consumes
+  // prologue: the first RS - 1 slabs (slab p = tile p / NS, column block p % NS, slot p)
+#pragma unroll
+  for (int p = 0; p < RS - 1; ++p)
+    if (p < total) issue(p / NS, p % NS, p);
+  int slot = 0;                                       // slot of the slab being consumed
   for (int64_t tile = 0; tile < ntile; ++tile) {
     f32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
     static_for<0, NS>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      // keep one slab in flight: issue the next one, then wait for this one (4 loads younger remain)
-      const bool more = j + 1 < NS || tile + 1 < ntile;
-      if (more) {
-        issue(j + 1 < NS ? tile : tile + 1, j + 1 < NS ? j + 1 : 0, slot ^ 1);
+      // keep RS - 1 slabs in flight: issue slab s + RS - 1 into the slot consumed last, then wait for
+      // slab s (4 LDS-DMA instructions per slab; the younger ones stay outstanding)
+      constexpr int jn = j + RS - 1;
+      const int64_t tn = tile + jn / NS;
+      int nslot = slot + RS - 1;
+      nslot -= nslot >= RS ? RS : 0;
+      if (tn < ntile) {
+        issue(tn, jn % NS, nslot);
+        wait_vm<4 * (RS - 1)>();
+      } else if (RS == 3 && tile * NS + j + 2 == total) {   // tail: one younger slab still in flight
         wait_vm<4>();
       } else {
         wait_vm<0>();
@@ -318,11 +336,14 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, qf.c0[j][t], acc, 0, 0, 0);
         }
       }
-      slot ^= 1;
+      slot = slot + 1 == RS ? 0 : slot + 1;
     });
 
     // ---- sum the 8 K-partials of this tile (fixed order), then the metric epilogue --------------------
-    float* rb = red + (size_t)(tile & 1) * kWaves * kQSlots * kRedStride;
+    float* rb = red + (red_bufs(RS) == 2 ? (size_t)(tile & 1) * kWaves * kQSlots * kRedStride : 0);
+    if constexpr (red_bufs(RS) == 1) {
+      if (tile > 0) lds_barrier();   // every wave has read the previous tile's partials
+    }
 #pragma unroll
     for (int a4 = 0; a4 < 4; ++a4) {   // C/D map: acc[4a + i] = (doc 8a + 4h + i, query r)
       const f32x4 v = {acc[4 * a4], acc[4 * a4 + 1], acc[4 * a4 + 2], acc[4 * a4 + 3]};
@@ -388,50 +409,56 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
   }
 }
 
-template <int DT, int NS, int KT, bool COS>
+template <int DT, int NS, int KT, bool COS, int RS>
 hipError_t launch_t(int grid, const void* c, const float* nr, const float* rs, const float* q, int64_t n, int d,
                     int b, uint32_t base, uint64_t* out, hipStream_t s) {
-  auto kern = sk_score_kernel<DT, NS, KT, COS>;
-  const size_t lds = sk_lds_bytes(DT, COS);
+  auto kern = sk_score_kernel<DT, NS, KT, COS, RS>;
+  const size_t lds = sk_lds_bytes(DT, COS, RS);
   if (hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds))
     return e;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, (const char*)c, nr, rs, q, n, d, b, base, out);
   return hipGetLastError();
 }
 
-template <int DT, int NS, bool COS>
+template <int DT, int NS, bool COS, int RS>
 hipError_t launch_kt(int kt, int grid, const void* c, const float* nr, const float* rs, const float* q, int64_t n,
                      int d, int b, uint32_t base, uint64_t* out, hipStream_t s) {
   switch (kt) {
-    case 4: return launch_t<DT, NS, 4, COS>(grid, c, nr, rs, q, n, d, b, base, out, s);
-    case 8: return launch_t<DT, NS, 8, COS>(grid, c, nr, rs, q, n, d, b, base, out, s);
-    case 16: return launch_t<DT, NS, 16, COS>(grid, c, nr, rs, q, n, d, b, base, out, s);
-    case 32: return launch_t<DT, NS, 32, COS>(grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 4: return launch_t<DT, NS, 4, COS, RS>(grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 8: return launch_t<DT, NS, 8, COS, RS>(grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 16: return launch_t<DT, NS, 16, COS, RS>(grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 32: return launch_t<DT, NS, 32, COS, RS>(grid, c, nr, rs, q, n, d, b, base, out, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-template <int DT, bool COS>
+template <int DT, bool COS, int RS>
 hipError_t launch_ns(int ns, int kt, int grid, const void* c, const float* nr, const float* rs, const float* q,
                      int64_t n, int d, int b, uint32_t base, uint64_t* out, hipStream_t s) {
   switch (ns) {
-    case 1: return launch_kt<DT, 1, COS>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
-    case 2: return launch_kt<DT, 2, COS>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
-    case 3: if constexpr (DT != 1) return launch_kt<DT, 3, COS>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 1: return launch_kt<DT, 1, COS, RS>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 2: return launch_kt<DT, 2, COS, RS>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 3: if constexpr (DT != 1) return launch_kt<DT, 3, COS, RS>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
             else return hipErrorInvalidValue;
-    case 4: if constexpr (DT != 1) return launch_kt<DT, 4, COS>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 4: if constexpr (DT != 1) return launch_kt<DT, 4, COS, RS>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
             else return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
+}
+
+template <int DT, int RS>
+hipError_t launch_metric(int metric, int ns, int kt, int grid, const void* c, const float* nr, const float* rs,
+                         const float* q, int64_t n, int d, int b, uint32_t base, uint64_t* out, hipStream_t s) {
+  return metric ? launch_ns<DT, true, RS>(ns, kt, grid, c, nr, rs, q, n, d, b, base, out, s)
+                : launch_ns<DT, false, RS>(ns, kt, grid, c, nr, rs, q, n, d, b, base, out, s);
 }
 
 }  // namespace sk
 
-size_t sk_lds_bytes(int sdt, bool cos) {
+size_t sk_lds_bytes(int sdt, bool cos, int ring) {
   const int sw = (cos ? 1 : 0) + (sdt == 2 ? 1 : 0);
-  return sk::kRingBytes + sk::kRedBytes + (size_t)sk::kSegRows * (sw > 0 ? sw : 1) * 4 + 3 * kQSlots * 4;
+  return sk::ring_bytes(ring) + sk::red_bytes(ring) + (size_t)sk::kSegRows * (sw > 0 ? sw : 1) * 4 + 3 * kQSlots * 4;
 }
-
 int sk_slabs(int sdt, int d) {
   const int eb = sdt == 1 ? 2 : 4;
   const int ks = d * eb / kWaves;   // row bytes per wave
@@ -441,21 +468,30 @@ int sk_slabs(int sdt, int d) {
 }
 
 hipError_t launch_sk(int sdt, int metric, int kt, int grid, const void* c, const float* nr, const float* rs,
-                     const float* q, int64_t n, int d, int b, uint32_t base, uint64_t* cand, hipStream_t s) {
+                     const float* q, int64_t n, int d, int b, uint32_t base, uint64_t* cand, hipStream_t s, int ring) {
   const int ns = sk_slabs(sdt, d);
   if (!ns || b < 1 || b > kQSlots || n < 1) return hipErrorInvalidValue;
-  switch (sdt) {
-    case 0: return metric ? sk::launch_ns<0, true>(ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s)
-                          : sk::launch_ns<0, false>(ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-    case 1: return metric ? sk::launch_ns<1, true>(ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s)
-                          : sk::launch_ns<1, false>(ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-    case 2: return metric ? sk::launch_ns<2, true>(ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s)
-                          : sk::launch_ns<2, false>(ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-    case 3: return metric ? sk::launch_ns<3, true>(ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s)
-                          : sk::launch_ns<3, false>(ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-
-    default: return hipErrorInvalidValue;
+  if (ring == 0) ring = kSkRing;
+  if (ring == 2) {
+    switch (sdt) {
+      case 0: return sk::launch_metric<0, 2>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      case 1: return sk::launch_metric<1, 2>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      case 2: return sk::launch_metric<2, 2>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      case 3: return sk::launch_metric<3, 2>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      default: return hipErrorInvalidValue;
+    }
   }
+#ifdef RR_SK_RING3   // A/B builds only (tools/kbench.hip): measured no faster, see kSkRing
+  if (ring == 3) {   // (the f32-MFMA form DT 0 is a kbench reference only: ring 2)
+    switch (sdt) {
+      case 1: return sk::launch_metric<1, 3>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      case 2: return sk::launch_metric<2, 3>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      case 3: return sk::launch_metric<3, 3>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
+#endif
+  return hipErrorInvalidValue;
 }
 
 }  // namespace rr

@@ -434,3 +434,24 @@ def test_split_k_fp32_error_is_fp32_class(Index):
         mag = np.einsum("bd,bkd->bk", np.abs(q64), np.abs(c64[ii]))
         rel = np.abs(sc - exact) / mag
         assert rel.max() < 2.0 ** -19, rel.max()
+
+
+def test_sharded_pipelined_exchange_mixed_k(Index):
+    """Back-to-back staged searches alternate the pipelined exchange (k <= 32: second stream, parity
+    buffers) with the serial k > 32 path; every fetch must equal the single-shard result."""
+    rng = np.random.default_rng(21)
+    corpus = rng.standard_normal((9001, 256)).astype(np.float32)
+    q = rng.standard_normal((40, 256)).astype(np.float32)
+    one = Index(devices=[0], dtype="fp32", metric="cosine")
+    one.load(corpus)
+    many = Index(devices=[0, 0, 0], dtype="fp32", metric="cosine")
+    many.load(corpus)
+    many.set_queries(q)
+    for k in (5, 40, 8, 8, 33, 1, 32, 32, 32, 2):
+        want = one.search(q, k)
+        for _ in range(3):
+            many.search_staged(k)
+        s, i = many.fetch()
+        assert np.array_equal(i, want[1]) and np.array_equal(s, want[0]), k
+    one.close()
+    many.close()

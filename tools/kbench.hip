@@ -4,6 +4,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I rag-serving-system_amd/csrc \
 //         tools/kbench.hip -o tools/kbench && tools/kbench [n_docs] [rounds]
+#define RR_SK_RING3 1
 #include "../rag-serving-system_amd/csrc/rr_kernels.hip"
 #include "../rag-serving-system_amd/csrc/rr_sk.hip"
 
@@ -259,10 +260,11 @@ int main(int argc, char** argv) {
     [&](const void* c, uint64_t* o) { return launch_fused_t<1, 8, COS, 0, NB, LM, AS, DBG, U>(grid, c, norms, rscale, q, n, d, b, 0, o, s); }, {}}
 #define VS(NB, LM, AS, COS, DBG, U) Variant{"fp32-split NB=" #NB " LM=" #LM " AS=" #AS " COS=" #COS " DBG=" #DBG " U=" #U, 2, \
     [&](const void* c, uint64_t* o) { return launch_fused_t<2, 8, COS, 0, NB, LM, AS, DBG, U>(grid, c, norms2, rscale, q, n, d, b, 0, o, s); }, {}}
-#define VK(DT, BUF, COS) Variant{"sk DT=" #DT " COS=" #COS, BUF, \
-    [&](const void* c, uint64_t* o) { return launch_sk(DT, COS, 8, grid, c, DT == 2 ? norms2 : norms, rscale, q, n, d, b, 0, o, s); }, {}}
+#define VK(DT, BUF, COS, RS) Variant{"sk DT=" #DT " COS=" #COS " ring=" #RS, BUF, \
+    [&](const void* c, uint64_t* o) { return launch_sk(DT, COS, 8, grid, c, DT == 2 ? norms2 : norms, rscale, q, n, d, b, 0, o, s, RS); }, {}}
   std::vector<Variant> vs = {V32(2, 1, 1, true, 0, 8), VS(2, 1, 1, true, 0, 8), V16(2, 1, 1, true, 0, 8),
-                             VK(3, 0, 1), VK(4, 0, 1), VK(2, 2, 1), VK(1, 1, 1), VK(3, 0, 0), VK(4, 0, 0)};
+                             VK(3, 0, 1, 2), VK(3, 0, 1, 3), VK(2, 2, 1, 2), VK(2, 2, 1, 3), VK(1, 1, 1, 2), VK(1, 1, 1, 3),
+                             VK(3, 0, 0, 2), VK(3, 0, 0, 3)};
   std::vector<Variant> streams = {
       Variant{"stream frag U=8 fp32", 0, [&](const void* c, uint64_t*) {
         hipLaunchKernelGGL(stream_frag<8>, dim3(grid), dim3(512), 0, s, (const u32x4*)c, n, d, sink);
