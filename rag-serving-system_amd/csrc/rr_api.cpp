@@ -113,6 +113,10 @@ namespace {
 
 size_t elem_bytes(int dtype) { return dtype == RR_DTYPE_BF16 ? 2 : 4; }
 
+// Query slots per corpus pass, at most (the split-K kernel serves 64 queries per pass for bf16 and
+// fp32-split storage; every other path 32).
+constexpr int kMaxSlots = 64;
+
 // How each public corpus dtype is stored and multiplied (rr_internal.h KDT_*).
 int kdt_of(int dtype) {
   switch (dtype) {
@@ -248,8 +252,8 @@ int ensure_buffers(rr_handle* h, int b, int k) {
     if (b > s.q_cap || k > s.k_cap) {
       const int qc = std::max(b, s.q_cap), kc = std::max(k, s.k_cap);
       if (b > s.q_cap) {
-        if (int rc = dmalloc(&s.queries, (size_t)((qc + 31) / 32 * 32) * h->d * 4)) return rc;
-        HIP_TRY(hipMemset(s.queries, 0, (size_t)((qc + 31) / 32 * 32) * h->d * 4));
+        if (int rc = dmalloc(&s.queries, (size_t)((qc + kMaxSlots - 1) / kMaxSlots * kMaxSlots) * h->d * 4)) return rc;
+        HIP_TRY(hipMemset(s.queries, 0, (size_t)((qc + kMaxSlots - 1) / kMaxSlots * kMaxSlots) * h->d * 4));
       }
       if (int rc = dmalloc(&s.out_scores, (size_t)qc * kc * 4)) return rc;
       if (int rc = dmalloc(&s.out_idx, (size_t)qc * kc * 8)) return rc;
@@ -261,12 +265,12 @@ int ensure_buffers(rr_handle* h, int b, int k) {
     }
     if (!s.cand) {
       s.cand_grid = s.cus;
-      if (int rc = dmalloc(&s.cand, (size_t)s.cand_grid * rr::kQSlots * RR_FUSED_KMAX * 8)) return rc;
+      if (int rc = dmalloc(&s.cand, (size_t)s.cand_grid * kMaxSlots * RR_FUSED_KMAX * 8)) return rc;
     }
     if (h->world > 1 && !s.px_keys[0]) {
       for (int p = 0; p < 2; ++p) {
-        if (int rc = dmalloc(&s.px_keys[p], (size_t)rr::kQSlots * RR_FUSED_KMAX * 8)) return rc;
-        if (int rc = dmalloc(&s.px_gathered[p], (size_t)h->world * rr::kQSlots * RR_FUSED_KMAX * 8)) return rc;
+        if (int rc = dmalloc(&s.px_keys[p], (size_t)kMaxSlots * RR_FUSED_KMAX * 8)) return rc;
+        if (int rc = dmalloc(&s.px_gathered[p], (size_t)h->world * kMaxSlots * RR_FUSED_KMAX * 8)) return rc;
       }
     }
     if (k > RR_FUSED_KMAX) {
@@ -361,8 +365,8 @@ int local_gather(rr_handle* h, int kk) {
 // process per GPU, peer copies within one process) into px_gathered[p] and merges it into the results,
 // while the compute stream goes on with the next block. px_keys[p] is rewritten two blocks later and only
 // after ev_xdone[p] of every shard that read it (enqueue_block).
-int enqueue_exchange_px(rr_handle* h, int p, int q0, int bb, int k, int kt) {
-  const size_t slot = (size_t)rr::kQSlots * kt;
+int enqueue_exchange_px(rr_handle* h, int p, int q0, int bb, int k, int kt, int slots) {
+  const size_t slot = (size_t)slots * kt;
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
     HIP_TRY(hipEventRecord(s.ev_keys[p], s.stream));
@@ -381,14 +385,21 @@ int enqueue_exchange_px(rr_handle* h, int p, int q0, int bb, int k, int kt) {
       }
     }
     HIP_TRY(rr::launch_merge(kt, dst.px_gathered[p], h->world, kt, bb, k, nullptr, dst.out_scores + (size_t)q0 * k,
-                             dst.out_idx + (size_t)q0 * k, dst.xstream));
+                             dst.out_idx + (size_t)q0 * k, dst.xstream, slots));
     HIP_TRY(hipEventRecord(dst.ev_xdone[p], dst.xstream));
   }
   return RR_OK;
 }
 
-// Enqueue the device pipeline for query block [q0, q0 + bb) on every local shard.
-int enqueue_block(rr_handle* h, int q0, int bb, int k) {
+// Query slots of one corpus pass for a search of b queries at k.
+int block_slots(const rr_handle* h, int b, int k) {
+  const int kt = rr::fused_kt(k);
+  if (b > rr::kQSlots && kt && kt <= 16 && use_sk(h) && rr::sk_supports_64(sk_dtype_of(h->dtype))) return kMaxSlots;
+  return rr::kQSlots;
+}
+
+// Enqueue the device pipeline for query block [q0, q0 + bb) (bb <= slots) on every local shard.
+int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
   const int d = h->d;
   const int kt = rr::fused_kt(k);
   const bool multi = h->world > 1;
@@ -429,21 +440,21 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k) {
         if (use_sk(h)) {
           const int sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(s.cand_grid, (s.rows() + 31) / 32));
           HIP_TRY(rr::launch_sk(sk_dtype_of(h->dtype), h->metric, kt, sgrid, s.corpus, s.norms, s.rscale, qb,
-                                s.rows(), d, bb, base, s.cand, s.stream));
+                                s.rows(), d, bb, base, s.cand, s.stream, 0, slots));
           grid = sgrid;
         } else {
           HIP_TRY(rr::launch_fused(kdt_of(h->dtype), h->metric, kt, grid, s.corpus, s.norms, s.rscale, qb,
                                    s.rows(), d, bb, base, s.cand, s.stream));
         }
       } else {
-        HIP_TRY(hipMemsetAsync(s.cand, 0, (size_t)rr::kQSlots * kt * 8, s.stream));
+        HIP_TRY(hipMemsetAsync(s.cand, 0, (size_t)slots * kt * 8, s.stream));
       }
       if (timed) HIP_TRY(hipEventRecord(e1, s.stream));
       if (!multi) {
-        HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, nullptr, osc, oix, s.stream));
+        HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, nullptr, osc, oix, s.stream, slots));
       } else {
         HIP_TRY(wait_px(p));
-        HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, s.px_keys[p], nullptr, nullptr, s.stream));
+        HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, s.px_keys[p], nullptr, nullptr, s.stream, slots));
       }
     } else {
       // k > RR_FUSED_KMAX: all keys of this shard, segmented radix sort, keep the first k. The exchange
@@ -468,7 +479,7 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k) {
   }
   if (!multi) return RR_OK;
   if (kt) {
-    if (int rc = enqueue_exchange_px(h, p, q0, bb, k, kt)) return rc;
+    if (int rc = enqueue_exchange_px(h, p, q0, bb, k, kt, slots)) return rc;
     h->parity ^= 1;
     return RR_OK;
   }
@@ -739,9 +750,10 @@ int rr_search_staged(rr_handle* h, int32_t k) {
   if (k < 1) return fail(RR_E_INVALID, "k=%d must be >= 1", k);
   const int b = h->cur_b;
   if (int rc = ensure_buffers(h, b, k)) return rc;
-  for (int q0 = 0; q0 < b; q0 += rr::kQSlots) {
-    const int bb = std::min(rr::kQSlots, b - q0);
-    if (int rc = enqueue_block(h, q0, bb, k)) return rc;
+  const int slots = block_slots(h, b, k);
+  for (int q0 = 0; q0 < b; q0 += slots) {
+    const int bb = std::min(slots, b - q0);
+    if (int rc = enqueue_block(h, q0, bb, k, slots)) return rc;
   }
   h->last_k = k;
   return RR_OK;

@@ -45,16 +45,19 @@ hipError_t launch_fused(int kdt, int metric, int kt, int grid, const void* corpu
 // single-buffered K-partial block and a second barrier per tile; on MI355X it ran 5 % slower for fp32
 // storage and within 1 % for bf16 / fp32-split (profiles/r01/kbench_ring.log).
 constexpr int kSkRing = 2;
+// qslots = query slots per corpus pass (32, or 64 where sk_supports_64: bf16 / fp32-split storage, KT <= 16);
+// cand is then [grid][qslots][KT].
 int sk_slabs(int sdt, int d);
-size_t sk_lds_bytes(int sdt, bool cos, int ring);
+bool sk_supports_64(int sdt);
+size_t sk_lds_bytes(int sdt, bool cos, int ring, int qslots);
 hipError_t launch_sk(int sdt, int metric, int kt, int grid, const void* corpus, const float* norms,
                      const float* rscale, const float* queries, int64_t n, int d, int b, uint32_t idx_base,
-                     uint64_t* cand, hipStream_t s, int ring = 0);
+                     uint64_t* cand, hipStream_t s, int ring = 0, int qslots = 32);
 
-// Merge nlists candidate lists laid out [nlists][32][in_kt] into the top-kt per query.
-// out_keys [32][kt] (may be null); out_scores/out_idx [b][k_out] (may be null).
+// Merge nlists candidate lists laid out [nlists][slots][in_kt] into the top-kt per query.
+// out_keys [slots][kt] (may be null); out_scores/out_idx [b][k_out] (may be null).
 hipError_t launch_merge(int kt, const uint64_t* in, int nlists, int in_kt, int b, int k_out,
-                        uint64_t* out_keys, float* out_scores, int64_t* out_idx, hipStream_t s);
+                        uint64_t* out_keys, float* out_scores, int64_t* out_idx, hipStream_t s, int slots = 32);
 
 // Full-score path for k > RR_FUSED_KMAX: keys [b][n] for every (query, doc) pair.
 hipError_t launch_full_keys(int kdt, int metric, int grid, const void* corpus, const float* norms,

@@ -449,14 +449,14 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
-// merge of candidate lists: in [nlists][32][in_kt] -> top-KT per query slot
+// merge of candidate lists: in [nlists][slots][in_kt] -> top-KT per query slot
 // ------------------------------------------------------------------------------------------------
 // One workgroup per query slot. Every input list is already sorted (descending), so: thread t takes
 // list t (lists beyond 256 are folded in by insertion), each wave extracts its top-KT by KT rounds of a
 // wave-wide max over the lanes' list heads (the winning lane advances its head from LDS; no barrier),
 // and wave 0 merges the 4 per-wave winner lists the same way.
 template <int KT>
-__global__ __launch_bounds__(256) void merge_kernel(const uint64_t* __restrict__ in, int nlists, int b,
+__global__ __launch_bounds__(256) void merge_kernel(const uint64_t* __restrict__ in, int nlists, int slots, int b,
                                                     int k_out, uint64_t* __restrict__ out_keys,
                                                     float* __restrict__ out_scores,
                                                     int64_t* __restrict__ out_idx) {
@@ -465,14 +465,14 @@ __global__ __launch_bounds__(256) void merge_kernel(const uint64_t* __restrict__
   __shared__ uint64_t W[4 * KT];
   TopK<KT> tk;
   if (tid < nlists) {
-    const uint64_t* src = in + ((size_t)tid * kQSlots + q) * KT;
+    const uint64_t* src = in + ((size_t)tid * slots + q) * KT;
 #pragma unroll
     for (int i = 0; i < KT; ++i) tk.v[i] = src[i];
   } else {
     tk.init();
   }
   for (int l = tid + 256; l < nlists; l += 256) {
-    const uint64_t* src = in + ((size_t)l * kQSlots + q) * KT;
+    const uint64_t* src = in + ((size_t)l * slots + q) * KT;
     for (int i = 0; i < KT; ++i) {
       const uint64_t key = src[i];
       if (key <= tk.last()) break;            // sorted input: nothing further can enter
@@ -815,15 +815,16 @@ hipError_t launch_full_keys(int kdt, int metric, int grid, const void* c, const 
 }
 
 hipError_t launch_merge(int kt, const uint64_t* in, int nlists, int in_kt, int b, int k_out, uint64_t* out_keys,
-                        float* out_scores, int64_t* out_idx, hipStream_t s) {
+                        float* out_scores, int64_t* out_idx, hipStream_t s, int slots) {
   if (in_kt != kt) return hipErrorInvalidValue;   // lists are always produced at the kernel's KT
   // Rows >= b of out_keys are still produced (from the zero-filled slots) so the buffer is uniform.
-  const int grid = out_keys ? kQSlots : b;
+  if (b > slots) return hipErrorInvalidValue;
+  const int grid = out_keys ? slots : b;
   switch (kt) {
-    case 4: hipLaunchKernelGGL(merge_kernel<4>, dim3(grid), dim3(256), 0, s, in, nlists, b, k_out, out_keys, out_scores, out_idx); break;
-    case 8: hipLaunchKernelGGL(merge_kernel<8>, dim3(grid), dim3(256), 0, s, in, nlists, b, k_out, out_keys, out_scores, out_idx); break;
-    case 16: hipLaunchKernelGGL(merge_kernel<16>, dim3(grid), dim3(256), 0, s, in, nlists, b, k_out, out_keys, out_scores, out_idx); break;
-    case 32: hipLaunchKernelGGL(merge_kernel<32>, dim3(grid), dim3(256), 0, s, in, nlists, b, k_out, out_keys, out_scores, out_idx); break;
+    case 4: hipLaunchKernelGGL(merge_kernel<4>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx); break;
+    case 8: hipLaunchKernelGGL(merge_kernel<8>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx); break;
+    case 16: hipLaunchKernelGGL(merge_kernel<16>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx); break;
+    case 32: hipLaunchKernelGGL(merge_kernel<32>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

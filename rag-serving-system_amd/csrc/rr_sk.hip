@@ -48,10 +48,11 @@ constexpr int kSegRows = 1024;                    // rows of per-doc factors hel
 // K-partial block is double-buffered (one barrier per tile); with RS = 3 (2 x 32 KiB more ring) it is
 // single-buffered to fit 160 KiB, and a second barrier before the next tile's partials are written
 // (normally passed without waiting: a whole tile of MFMAs lies between it and the reads it guards).
+// With 64 query slots (QH = 2 halves of 32) the partial block doubles, so it is single-buffered too.
 __host__ __device__ constexpr size_t ring_bytes(int rs) { return (size_t)kWaves * rs * kSlabBytes; }
-__host__ __device__ constexpr int red_bufs(int rs) { return rs == 2 ? 2 : 1; }
-__host__ __device__ constexpr size_t red_bytes(int rs) {
-  return (size_t)red_bufs(rs) * kWaves * kQSlots * kRedStride * 4;
+__host__ __device__ constexpr int red_bufs(int rs, int qh) { return rs == 2 && qh == 1 ? 2 : 1; }
+__host__ __device__ constexpr size_t red_bytes(int rs, int qh) {
+  return (size_t)red_bufs(rs, qh) * kWaves * (32 * qh) * kRedStride * 4;
 }
 
 // storage position P (16-byte unit of a pair_unit-ordered row) -> logical unit
@@ -124,13 +125,17 @@ struct QFrag<3, NS> { bf16x8 c0[NS][2], c1[NS][2], c2[NS][2]; };
 // LDS byte offset (within a slot) of 16-byte column position cp of tile row r (swizzled image)
 __device__ __forceinline__ int slab_off(int r, int cp) { return (r >> 3) * 1024 + (r & 7) * 128 + ((cp ^ (r & 7)) << 4); }
 
-template <int DT, int NS, int KT, bool COS, int RS>
+// QH = query halves: 32 * QH query slots per pass (64 for the batch-64 configs: one corpus pass serves
+// them all; each A fragment then feeds the MFMAs of both halves).
+template <int DT, int NS, int KT, bool COS, int RS, int QH>
 __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict__ corpus,
                                                           const float* __restrict__ norms,
                                                           const float* __restrict__ rscale,
                                                           const float* __restrict__ queries, int64_t n, int d,
                                                           int b, uint32_t idx_base, uint64_t* __restrict__ out) {
   static_assert(RS == 2 || RS == 3, "ring depth 2 or 3 (the tail waits are written for these)");
+  static_assert(QH == 1 || QH == 2, "32 or 64 query slots");
+  constexpr int QS = 32 * QH;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -142,13 +147,13 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
 
   float* red = (float*)(smem + ring_bytes(RS));
   constexpr int SW = (COS ? 1 : 0) + (DT == 2 ? 1 : 0);          // per-doc floats in the segment
-  float* seg = (float*)(smem + ring_bytes(RS) + red_bytes(RS));
-  float* qinfo = seg + kSegRows * (SW > 0 ? SW : 1);            // [32] |q|, [32] 2^-e (split), [32] int e
-  int* qexp = (int*)(qinfo + 2 * kQSlots);
+  float* seg = (float*)(smem + ring_bytes(RS) + red_bytes(RS, QH));
+  float* qinfo = seg + kSegRows * (SW > 0 ? SW : 1);            // [QS] |q|, [QS] 2^-e (split), [QS] int e
+  int* qexp = (int*)(qinfo + 2 * QS);
 
   // ---- per-query scalars: |q| (cosine, fp32 as cp.linalg.norm, retriever.py:602) and split exponents
   if (COS || DT == 2) {
-    for (int q = w * 4; q < w * 4 + 4; ++q) {
+    for (int q = w * 4 * QH; q < (w + 1) * 4 * QH; ++q) {
       float ss = 0.f, m = 0.f;
       if (q < b)
         for (int c = lane; c < (d >> 2); c += 64) {
@@ -166,7 +171,7 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
       const int ex = m > 0.f ? 15 - E : 0;
       if (lane == 0) {
         qinfo[q] = sqrtf(ss);
-        qinfo[kQSlots + q] = ldexpf(1.0f, -ex);
+        qinfo[QS + q] = ldexpf(1.0f, -ex);
         qexp[q] = ex;
       }
     }
@@ -174,10 +179,13 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
   }
 
   // ---- this wave's K-slice of every query as MFMA B operands (lane: query r, K half h) ----------------
-  QFrag<DT, NS> qf;
-  {
-    const bool qv = r < b;
-    const float* qrow = queries + (size_t)(qv ? r : 0) * d;
+  QFrag<DT, NS> qfs[QH];
+#pragma unroll
+  for (int qh = 0; qh < QH; ++qh) {
+    QFrag<DT, NS>& qf = qfs[qh];
+    const int rq = r + 32 * qh;
+    const bool qv = rq < b;
+    const float* qrow = queries + (size_t)(qv ? rq : 0) * d;
     auto qval = [&](int e) -> float { return qv ? qrow[e] : 0.f; };
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
@@ -201,7 +209,7 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
           }
         }
       } else if constexpr (DT == 2) {
-        const int ex = qv ? qexp[r] : 0;
+        const int ex = qv ? qexp[rq] : 0;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {   // K-step t: lane half h reads units 4t + 2h (hi), + 1 (lo)
           const int g8 = (p0 + 8 * j + 4 * t + 2 * h) >> 1;   // 8-element group
@@ -236,11 +244,13 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
   const int64_t r1 = r0 + per + (g < rem ? 1 : 0);
   const int64_t ntile = (r1 - r0 + 31) / 32;
 
-  // epilogue lane mapping: query qe = 4w + lane / 16, tile rows 2 (lane % 16) + {0, 1}
-  const int qe = 4 * w + (lane >> 4), er = 2 * (lane & 15);
+  // epilogue lane mapping: wave w owns queries 4·QH·w + [0, 4·QH); LPQ lanes per query, each with DPL
+  // consecutive tile rows (QH 1: 16 lanes x 2 rows, QH 2: 8 lanes x 4 rows)
+  constexpr int LPQ = 16 / QH, DPL = 2 * QH;
+  const int qe = 4 * QH * w + lane / LPQ, er = DPL * (lane % LPQ);
   const bool qev = qe < b;
   const float qn = COS ? qinfo[qe] : 0.f;
-  const float qs = DT == 2 ? qinfo[kQSlots + qe] : 1.f;
+  const float qs = DT == 2 ? qinfo[QS + qe] : 1.f;
 
   TopK<KT> tk;
   tk.init();
@@ -269,9 +279,11 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
     if (p < total) issue(p / NS, p % NS, p);
   int slot = 0;                                       // slot of the slab being consumed
   for (int64_t tile = 0; tile < ntile; ++tile) {
-    f32x16 acc;
+    f32x16 accs[QH];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    for (int qh = 0; qh < QH; ++qh)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) accs[qh][i] = 0.f;
     static_for<0, NS>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       // keep RS - 1 slabs in flight: issue slab s + RS - 1 into the slot consumed last, then wait for
@@ -295,15 +307,15 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
         for (int i = 0; i < 4; ++i) a[i] = *(const f32x4*)(sl + slab_off(r, 4 * h + i));
 #pragma unroll
         for (int m = 0; m < 16; ++m)
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m >> 2][m & 3], qf.v[j][m], acc, 0, 0, 0);
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m >> 2][m & 3], qfs[qh].v[j][m], accs[qh], 0, 0, 0);
       } else if constexpr (DT == 1) {
         bf16x8 a[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) a[t] = *(const bf16x8*)(sl + slab_off(r, 2 * t + h));
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], qf.hi[j][t], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], qf.lo[j][t], acc, 0, 0, 0);
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], qfs[qh].hi[j][t], accs[qh], 0, 0, 0);
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], qfs[qh].lo[j][t], accs[qh], 0, 0, 0);
         }
       } else if constexpr (DT == 2) {
         f16x8 ah[2], al[2];
@@ -314,9 +326,9 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t], qf.hi[j][t], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t], qf.lo[j][t], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[t], qf.hi[j][t], acc, 0, 0, 0);
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t], qfs[qh].hi[j][t], accs[qh], 0, 0, 0);
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t], qfs[qh].lo[j][t], accs[qh], 0, 0, 0);
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[t], qfs[qh].hi[j][t], accs[qh], 0, 0, 0);
         }
       } else {
         f32x4 a[4];
@@ -328,27 +340,29 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
                               a[2 * t + 1].x, a[2 * t + 1].y, a[2 * t + 1].z, a[2 * t + 1].w};
           bf16x8 b0, b1, b2;
           split3(x, b0, b1, b2);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qf.c0[j][t], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qf.c1[j][t], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qf.c0[j][t], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qf.c1[j][t], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qf.c2[j][t], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, qf.c0[j][t], acc, 0, 0, 0);
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c1[j][t], accs[qh], 0, 0, 0);
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qfs[qh].c1[j][t], accs[qh], 0, 0, 0);
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c2[j][t], accs[qh], 0, 0, 0);
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
         }
       }
       slot = slot + 1 == RS ? 0 : slot + 1;
     });
 
     // ---- sum the 8 K-partials of this tile (fixed order), then the metric epilogue --------------------
-    float* rb = red + (red_bufs(RS) == 2 ? (size_t)(tile & 1) * kWaves * kQSlots * kRedStride : 0);
-    if constexpr (red_bufs(RS) == 1) {
+    float* rb = red + (red_bufs(RS, QH) == 2 ? (size_t)(tile & 1) * kWaves * QS * kRedStride : 0);
+    if constexpr (red_bufs(RS, QH) == 1) {
       if (tile > 0) lds_barrier();   // every wave has read the previous tile's partials
     }
 #pragma unroll
-    for (int a4 = 0; a4 < 4; ++a4) {   // C/D map: acc[4a + i] = (doc 8a + 4h + i, query r)
-      const f32x4 v = {acc[4 * a4], acc[4 * a4 + 1], acc[4 * a4 + 2], acc[4 * a4 + 3]};
-      *(f32x4*)(rb + (w * kQSlots + r) * kRedStride + 8 * a4 + 4 * h) = v;
-    }
+    for (int qh = 0; qh < QH; ++qh)
+#pragma unroll
+      for (int a4 = 0; a4 < 4; ++a4) {   // C/D map: acc[4a + i] = (doc 8a + 4h + i, query r)
+        const f32x4 v = {accs[qh][4 * a4], accs[qh][4 * a4 + 1], accs[qh][4 * a4 + 2], accs[qh][4 * a4 + 3]};
+        *(f32x4*)(rb + (w * QS + 32 * qh + r) * kRedStride + 8 * a4 + 4 * h) = v;
+      }
     lds_barrier();
     const int64_t tb = r0 + tile * 32;
     if constexpr (SW > 0) {
@@ -369,96 +383,128 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
         lds_barrier();
       }
     }
-    float s0 = 0.f, s1 = 0.f;
+    float sv[DPL];
 #pragma unroll
-    for (int ww = 0; ww < kWaves; ++ww) {
-      const float2 p = *(const float2*)(rb + (ww * kQSlots + qe) * kRedStride + er);
-      s0 += p.x;
-      s1 += p.y;
+    for (int e = 0; e < DPL; ++e) sv[e] = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < kWaves; ++ww) {   // fixed wave order: the same sums for any QH
+      const float* src = rb + (ww * QS + qe) * kRedStride + er;
+      if constexpr (DPL == 2) {
+        const float2 p = *(const float2*)src;
+        sv[0] += p.x;
+        sv[1] += p.y;
+      } else {
+        const f32x4 p = *(const f32x4*)src;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sv[e] += p[e];
+      }
+    }
+    // Cosine prefilter: a score whose estimate dot * rcp(den) (within a few ulp of the quotient) is below
+    // the lane's current k-th score minus a 2^-20 relative margin cannot enter the list, so only the
+    // few that pass pay the exact IEEE division (the list only grows inside the loop: the threshold
+    // taken here is conservative).
+    float thr = -INFINITY;
+    if constexpr (COS) {
+      const uint64_t last = tk.last();
+      if (last != 0) {
+        const float t = float_of_ord((uint32_t)(last >> 32));
+        thr = t - fabsf(t) * 0x1p-20f - 0x1p-100f;
+      }
     }
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
+    for (int e = 0; e < DPL; ++e) {
       const int64_t row = tb + er + e;
-      float s = e ? s1 : s0;
+      float s = sv[e];
       const int64_t li = row - seg_lo;
       if constexpr (DT == 2) s = s * (COS ? seg[2 * li + 1] : seg[li]) * qs;   // exact 2^e rescales
+      const bool valid = qev && row < r1;
       if constexpr (COS) {
         // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
         const float nd = DT == 2 ? seg[2 * li] : seg[li];
-        s = s / (qn * nd + 1e-8f);
-        s = fminf(fmaxf(s, -1.0f), 1.0f);
+        const float den = qn * nd + 1e-8f;
+        if (valid && s * __builtin_amdgcn_rcpf(den) >= thr) {
+          float c = s / den;   // IEEE division, as the reference's elementwise kernel
+          c = fminf(fmaxf(c, -1.0f), 1.0f);
+          const uint64_t key = make_key(c, idx_base + (uint32_t)row);
+          if (key > tk.last()) tk.insert(key);
+        }
+      } else {
+        const uint64_t key = make_key(s, idx_base + (uint32_t)row);
+        if (valid && key > tk.last()) tk.insert(key);
       }
-      const uint64_t key = make_key(s, idx_base + (uint32_t)row);
-      if (qev && row < r1 && key > tk.last()) tk.insert(key);
     }
   }
 
-  // ---- per query: merge its 16 lane lists (KT rounds of a 16-lane max; keys are unique) ---------------
-  uint64_t* dst = out + ((size_t)g * kQSlots + qe) * KT;
+  // ---- per query: merge its LPQ lane lists (KT rounds of an LPQ-lane max; keys are unique) -------------
+  uint64_t* dst = out + ((size_t)g * QS + qe) * KT;
 #pragma unroll 1
   for (int rnd = 0; rnd < KT; ++rnd) {
     uint64_t m = tk.v[0];
 #pragma unroll
-    for (int off = 8; off >= 1; off >>= 1) {
+    for (int off = LPQ / 2; off >= 1; off >>= 1) {
       const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)m, off, 64);
       const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(m >> 32), off, 64);
       m = umax64(m, ((uint64_t)hi << 32) | lo);
     }
     if (m != 0 && tk.v[0] == m) tk.pop();
-    if ((lane & 15) == 0) dst[rnd] = m;
+    if (lane % LPQ == 0) dst[rnd] = m;
   }
 }
 
-template <int DT, int NS, int KT, bool COS, int RS>
+template <int DT, int NS, int KT, bool COS, int RS, int QH>
 hipError_t launch_t(int grid, const void* c, const float* nr, const float* rs, const float* q, int64_t n, int d,
                     int b, uint32_t base, uint64_t* out, hipStream_t s) {
-  auto kern = sk_score_kernel<DT, NS, KT, COS, RS>;
-  const size_t lds = sk_lds_bytes(DT, COS, RS);
+  auto kern = sk_score_kernel<DT, NS, KT, COS, RS, QH>;
+  const size_t lds = sk_lds_bytes(DT, COS, RS, 32 * QH);
   if (hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds))
     return e;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, (const char*)c, nr, rs, q, n, d, b, base, out);
   return hipGetLastError();
 }
 
-template <int DT, int NS, bool COS, int RS>
+template <int DT, int NS, bool COS, int RS, int QH>
 hipError_t launch_kt(int kt, int grid, const void* c, const float* nr, const float* rs, const float* q, int64_t n,
                      int d, int b, uint32_t base, uint64_t* out, hipStream_t s) {
   switch (kt) {
-    case 4: return launch_t<DT, NS, 4, COS, RS>(grid, c, nr, rs, q, n, d, b, base, out, s);
-    case 8: return launch_t<DT, NS, 8, COS, RS>(grid, c, nr, rs, q, n, d, b, base, out, s);
-    case 16: return launch_t<DT, NS, 16, COS, RS>(grid, c, nr, rs, q, n, d, b, base, out, s);
-    case 32: return launch_t<DT, NS, 32, COS, RS>(grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 4: return launch_t<DT, NS, 4, COS, RS, QH>(grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 8: return launch_t<DT, NS, 8, COS, RS, QH>(grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 16: return launch_t<DT, NS, 16, COS, RS, QH>(grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 32: if constexpr (QH == 1) return launch_t<DT, NS, 32, COS, RS, QH>(grid, c, nr, rs, q, n, d, b, base, out, s);
+             else return hipErrorInvalidValue;   // 64 slots x KT 32 spills: served as two 32-slot passes
     default: return hipErrorInvalidValue;
   }
 }
 
-template <int DT, bool COS, int RS>
+template <int DT, bool COS, int RS, int QH>
 hipError_t launch_ns(int ns, int kt, int grid, const void* c, const float* nr, const float* rs, const float* q,
                      int64_t n, int d, int b, uint32_t base, uint64_t* out, hipStream_t s) {
   switch (ns) {
-    case 1: return launch_kt<DT, 1, COS, RS>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
-    case 2: return launch_kt<DT, 2, COS, RS>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
-    case 3: if constexpr (DT != 1) return launch_kt<DT, 3, COS, RS>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 1: return launch_kt<DT, 1, COS, RS, QH>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 2: return launch_kt<DT, 2, COS, RS, QH>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 3: if constexpr (DT != 1) return launch_kt<DT, 3, COS, RS, QH>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
             else return hipErrorInvalidValue;
-    case 4: if constexpr (DT != 1) return launch_kt<DT, 4, COS, RS>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 4: if constexpr (DT != 1) return launch_kt<DT, 4, COS, RS, QH>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
             else return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }
 
-template <int DT, int RS>
+template <int DT, int RS, int QH>
 hipError_t launch_metric(int metric, int ns, int kt, int grid, const void* c, const float* nr, const float* rs,
                          const float* q, int64_t n, int d, int b, uint32_t base, uint64_t* out, hipStream_t s) {
-  return metric ? launch_ns<DT, true, RS>(ns, kt, grid, c, nr, rs, q, n, d, b, base, out, s)
-                : launch_ns<DT, false, RS>(ns, kt, grid, c, nr, rs, q, n, d, b, base, out, s);
+  return metric ? launch_ns<DT, true, RS, QH>(ns, kt, grid, c, nr, rs, q, n, d, b, base, out, s)
+                : launch_ns<DT, false, RS, QH>(ns, kt, grid, c, nr, rs, q, n, d, b, base, out, s);
 }
 
 }  // namespace sk
 
-size_t sk_lds_bytes(int sdt, bool cos, int ring) {
+size_t sk_lds_bytes(int sdt, bool cos, int ring, int qslots) {
   const int sw = (cos ? 1 : 0) + (sdt == 2 ? 1 : 0);
-  return sk::ring_bytes(ring) + sk::red_bytes(ring) + (size_t)sk::kSegRows * (sw > 0 ? sw : 1) * 4 + 3 * kQSlots * 4;
+  return sk::ring_bytes(ring) + sk::red_bytes(ring, qslots / 32) + (size_t)sk::kSegRows * (sw > 0 ? sw : 1) * 4 +
+         3 * qslots * 4;
 }
+
+bool sk_supports_64(int sdt) { return sdt == KDT_BF16 || sdt == KDT_F32_SPLIT; }
 int sk_slabs(int sdt, int d) {
   const int eb = sdt == 1 ? 2 : 4;
   const int ks = d * eb / kWaves;   // row bytes per wave
@@ -468,25 +514,34 @@ int sk_slabs(int sdt, int d) {
 }
 
 hipError_t launch_sk(int sdt, int metric, int kt, int grid, const void* c, const float* nr, const float* rs,
-                     const float* q, int64_t n, int d, int b, uint32_t base, uint64_t* cand, hipStream_t s, int ring) {
+                     const float* q, int64_t n, int d, int b, uint32_t base, uint64_t* cand, hipStream_t s, int ring,
+                     int qslots) {
   const int ns = sk_slabs(sdt, d);
-  if (!ns || b < 1 || b > kQSlots || n < 1) return hipErrorInvalidValue;
+  if (!ns || b < 1 || b > qslots || n < 1 || (qslots != 32 && qslots != 64)) return hipErrorInvalidValue;
   if (ring == 0) ring = kSkRing;
+  if (qslots == 64) {   // one corpus pass for up to 64 queries: bf16 and fp32-split storage, ring 2
+    if (ring != 2) return hipErrorInvalidValue;
+    switch (sdt) {
+      case 1: return sk::launch_metric<1, 2, 2>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      case 2: return sk::launch_metric<2, 2, 2>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
   if (ring == 2) {
     switch (sdt) {
-      case 0: return sk::launch_metric<0, 2>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-      case 1: return sk::launch_metric<1, 2>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-      case 2: return sk::launch_metric<2, 2>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-      case 3: return sk::launch_metric<3, 2>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      case 0: return sk::launch_metric<0, 2, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      case 1: return sk::launch_metric<1, 2, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      case 2: return sk::launch_metric<2, 2, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      case 3: return sk::launch_metric<3, 2, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
       default: return hipErrorInvalidValue;
     }
   }
 #ifdef RR_SK_RING3   // A/B builds only (tools/kbench.hip): measured no faster, see kSkRing
   if (ring == 3) {   // (the f32-MFMA form DT 0 is a kbench reference only: ring 2)
     switch (sdt) {
-      case 1: return sk::launch_metric<1, 3>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-      case 2: return sk::launch_metric<2, 3>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-      case 3: return sk::launch_metric<3, 3>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      case 1: return sk::launch_metric<1, 3, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      case 2: return sk::launch_metric<2, 3, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      case 3: return sk::launch_metric<3, 3, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
       default: return hipErrorInvalidValue;
     }
   }

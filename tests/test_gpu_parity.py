@@ -455,3 +455,52 @@ def test_sharded_pipelined_exchange_mixed_k(Index):
         assert np.array_equal(i, want[1]) and np.array_equal(s, want[0]), k
     one.close()
     many.close()
+
+
+# ---- 64 query slots per corpus pass (bf16 / fp32-split storage, k <= 16) ------------------------------
+@pytest.mark.parametrize("dtype", ["bf16", "fp32-split"])
+@pytest.mark.parametrize("metric", ["dot", "cosine"])
+def test_split_k_64_query_slots(Index, dtype, metric):
+    """b in 33..64 runs ONE split-K pass with 64 query slots (BASELINE config 5 is batch 64): results are
+    bit-identical to 32-query passes over the same queries and match the oracle's canonical top-k."""
+    rng = np.random.default_rng(64 + len(dtype))
+    n, d = 12345, 1024
+    corpus = rng.standard_normal((n, d)).astype(np.float32)
+    if dtype == "bf16":
+        corpus = synth.bf16_round(corpus)
+    q = rng.standard_normal((100, d)).astype(np.float32)
+    ix = Index(dtype=dtype, metric=metric)
+    ix.load(corpus)
+    ex = exact_scores(corpus, q, metric)
+    tol = 1e-3 * (np.sqrt(d) if metric == "dot" else 1.0)
+    for b in (33, 64, 100):
+        for k in (1, 5, 16, 17):
+            ix.set_timing(True)
+            ix.kernel_time(reset=True)
+            s64, i64 = ix.search(q[:b], k)
+            _, launches = ix.kernel_time(reset=True)
+            ix.set_timing(False)
+            if k <= 16:
+                assert launches == -(-b // 64), (b, k, launches)
+            parts = [ix.search(q[q0:min(b, q0 + 32)], k) for q0 in range(0, b, 32)]
+            assert np.array_equal(i64, np.concatenate([p[1] for p in parts])), (b, k)
+            assert np.array_equal(s64, np.concatenate([p[0] for p in parts])), (b, k)
+            _, cidx = canonical_topk(ex[:b], k)
+            check_topk(i64, s64, cidx, corpus, q[:b], metric, near_tie=1e-5 * np.sqrt(d), score_tol=tol)
+    ix.close()
+
+
+def test_split_k_64_slots_sharded(Index):
+    """64-slot passes through the pipelined cross-shard exchange equal the single-shard result."""
+    rng = np.random.default_rng(7)
+    corpus = synth.bf16_round(rng.standard_normal((20011, 1024)).astype(np.float32))
+    q = rng.standard_normal((64, 1024)).astype(np.float32)
+    one = Index(devices=[0], dtype="bf16", metric="cosine")
+    one.load(corpus)
+    many = Index(devices=[0, 0, 0, 0], dtype="bf16", metric="cosine")
+    many.load(corpus)
+    for k in (5, 10, 40):
+        a, b = one.search(q, k), many.search(q, k)
+        assert np.array_equal(a[1], b[1]) and np.array_equal(a[0], b[0]), k
+    one.close()
+    many.close()
