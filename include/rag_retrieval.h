@@ -52,8 +52,12 @@ extern "C" {
 #define RR_E_OOM         -6   /* device allocation failed */
 
 /* corpus storage dtype in HBM (4 bytes per element for both fp32 forms, 2 for bf16) */
-#define RR_DTYPE_F32       0  /* fp32 rows stored exactly, v_mfma_f32_32x32x2_f32: every score is an fp32
-                                  fmaf chain (the reference's fp32 GEMM, up to summation order) */
+#define RR_DTYPE_F32       0  /* fp32 rows stored exactly. Split-K kernel (d % 256 == 0): every corpus and
+                                  query value split exactly into three bf16, 6 bf16 MFMAs per product block
+                                  (kept partial products exact, dropped terms < 2^-23 |xq|), fp32 accumulate;
+                                  register-streaming kernel: v_mfma_f32_32x32x2_f32 (an fp32 fmaf chain).
+                                  Either way fp32-class scores (the reference's fp32 GEMM up to summation
+                                  order; bit-exact on exactly representable data) */
 #define RR_DTYPE_BF16      1  /* bf16 rows (RNE from fp32), bf16 MFMA with fp32 accumulate */
 #define RR_DTYPE_F32_SPLIT 2  /* opt-in: fp32 rows stored as f16 hi + lo with a per-row power-of-two scale,
                                   x ~ (hi + lo) * 2^-e with a 22-bit significand (|err| <= 2^-22 |x|); scores
@@ -154,7 +158,8 @@ int rr_set_queries_device(rr_handle* h, const float* dev_q, int32_t b, int32_t d
 /* ---- kernel selection (diagnostics / A-B tests) --------------------------------------------------- */
 
 #define RR_KERNEL_AUTO  0   /* split-K LDS-DMA kernel where the shape allows it (d*elem/8 a multiple of
-                               128 bytes, at most 512 bytes), else the register-streaming kernel */
+                               128 bytes, at most 512 bytes; 64 queries per corpus pass for bf16 /
+                               fp32-split at k <= 16), else the register-streaming kernel */
 #define RR_KERNEL_FUSED 1   /* always the register-streaming kernel (fp32: f32 MFMA) */
 
 /* Choose the similarity kernel for k <= RR_FUSED_KMAX searches on this handle. Results of the two kernels
