@@ -183,10 +183,10 @@ def main() -> None:
                             "frac": round(v_ach / HBM_PEAK_GBS, 4), "steps": args.variant_steps,
                             "index_agreement_with_headline": round(float(np.mean(v_idx == head_idx)), 4)}
 
-    traffic, traffic_note = None, "not measured"
+    traffic, traffic_note, mfma = None, "not measured", None
     if rank == 0 and world == 1 and not args.no_pmc:
         ix.close()                 # free HBM for the child pass
-        traffic, traffic_note = pmc_traffic(args)
+        traffic, traffic_note, mfma = pmc_counters(args, avg_kernel_s)
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:   # rank 0 at N=1 only
@@ -218,6 +218,7 @@ def main() -> None:
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": traffic,
                          "traffic_note": traffic_note,
+                         "mfma": mfma,
                          "kernel": SCORE_KERNEL_DOC,
                          "kernel_avg_us": round(avg_kernel_s * 1e6, 2),
                          "alg_bytes_per_launch": alg_bytes},
@@ -235,10 +236,15 @@ def main() -> None:
     ix.close()
 
 
-def pmc_traffic(args):
-    """HBM bytes per fused launch from a rocprofv3 --pmc FETCH_SIZE pass over a short run of this same
-    workload, run as a CHILD process (MI355X_MICROARCH.md §HBM: FETCH_SIZE is in KiB and reports half the
-    bytes of a wide coalesced stream on gfx950, so bytes = FETCH_SIZE * 1024 * 2)."""
+def pmc_counters(args, kernel_s):
+    """One rocprofv3 --pmc pass (FETCH_SIZE, SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE: 3 of 4 TCC, 1 of 8 SQ,
+    1 of 2 GRBM slots) over a short run of this same workload, as a CHILD process. Per similarity-kernel
+    launch (median):
+      traffic   = FETCH_SIZE * 1024 * 2 bytes (KiB; gfx950 reports half of a wide stream, MI355X_MICROARCH.md §HBM)
+      mfma.busy = SQ_VALU_MFMA_BUSY_CYCLES / (4 SIMDs x CUs x kernel cycles), kernel cycles =
+                  GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs) — the matrix-core duty cycle;
+      mfma.alg_tflops = the metric's own flops (2·B·N·D) / the timed kernel duration, against the dense
+                  peak of the dtype the products run on."""
     import csv
     import shutil
     import statistics
@@ -246,28 +252,49 @@ def pmc_traffic(args):
     import tempfile
     exe = shutil.which("rocprofv3")
     if not exe:
-        return None, "rocprofv3 not found"
+        return None, "rocprofv3 not found", None
     out = tempfile.mkdtemp(prefix="bench_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-    cmd = [exe, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", out, "-o", "pmc", "--",
+    cmd = [exe, "--pmc", "FETCH_SIZE", "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "--output-format", "csv",
+           "-d", out, "-o", "pmc", "--",
            sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "3", "--warmup", "1",
            "--latency-steps", "1", "--no-cpu-baseline", "--docs", str(args.docs), "--dim", str(args.dim),
            "--batch", str(args.batch), "--k", str(args.k), "--dtype", args.dtype, "--metric", args.metric,
            "--variants", ""]
     try:
         subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
-        vals = []
+        vals = {}
         for root, _, files in os.walk(out):
             for f in files:
                 if f.endswith("counter_collection.csv"):
                     for row in csv.DictReader(open(os.path.join(root, f))):
-                        if is_score_kernel(row["Kernel_Name"]) and row["Counter_Name"] == "FETCH_SIZE":
-                            vals.append(float(row["Counter_Value"]))
-        if not vals:
-            return None, "no similarity-kernel FETCH_SIZE rows"
-        return round(statistics.median(vals) * 1024 * 2), (
-            f"rocprofv3 --pmc FETCH_SIZE child pass, median of {len(vals)} fused launches, x1024 B/KiB x2 (gfx950)")
+                        if is_score_kernel(row["Kernel_Name"]):
+                            key = (row.get("Dispatch_Id", ""), row["Counter_Name"])
+                            vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
+        per = {}
+        for (_, name), v in vals.items():
+            per.setdefault(name, []).append(v)
+        if "FETCH_SIZE" not in per:
+            return None, "no similarity-kernel FETCH_SIZE rows", None
+        traffic = round(statistics.median(per["FETCH_SIZE"]) * 1024 * 2)
+        note = (f"rocprofv3 --pmc child pass, median of {len(per['FETCH_SIZE'])} similarity-kernel launches, "
+                f"FETCH_SIZE x1024 B/KiB x2 (gfx950)")
+        mfma = None
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in per and "GRBM_GUI_ACTIVE" in per:
+            import torch
+            cus = torch.cuda.get_device_properties(0).multi_processor_count
+            busy = statistics.median(per["SQ_VALU_MFMA_BUSY_CYCLES"])
+            cyc = statistics.median(per["GRBM_GUI_ACTIVE"]) / 8
+            flops = 2.0 * args.batch * args.docs * args.dim
+            peak = {"fp32": 2500.0, "bf16": 2500.0, "fp32-split": 2500.0}[args.dtype]   # products on bf16/f16 MFMAs
+            mfma = {"busy_frac": round(busy / (4 * cus * cyc), 4), "busy_cycles": busy, "kernel_cycles": cyc,
+                    "clock_GHz": round(cyc / kernel_s / 1e9, 3) if kernel_s else None,
+                    "alg_tflops": round(flops / kernel_s / 1e12, 2) if kernel_s else None,
+                    "peak_tflops_dense": peak,
+                    "note": "busy = SQ_VALU_MFMA_BUSY_CYCLES / (4 x CUs x GRBM_GUI_ACTIVE/8); alg_tflops counts "
+                            "2*B*N*D (the split-product MFMAs do 2-6x that on the matrix cores)"}
+        return traffic, note, mfma
     except Exception as e:  # never fail the benchmark on the profiler
-        return None, f"pmc pass failed: {type(e).__name__}"
+        return None, f"pmc pass failed: {type(e).__name__}", None
     finally:
         shutil.rmtree(out, ignore_errors=True)
 
