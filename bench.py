@@ -104,6 +104,8 @@ def main() -> None:
     ap.add_argument("--metric", default="cosine", choices=["cosine", "dot"])
     ap.add_argument("--latency-steps", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ingest-rows", type=int, default=262_144,
+                    help="rows of a host fp32 array timed through rr_load (N=1 only; 0 = skip)")
     ap.add_argument("--cpu-batches", type=int, default=3)
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the rocprofv3 --pmc FETCH_SIZE child pass that fills roofline.traffic")
@@ -166,6 +168,22 @@ def main() -> None:
         return
 
     # ---- the other corpus dtypes on the same workload (1 GPU only; reported beside, never `value`) --
+    # ---- corpus ingest (main.py:20-23 + retriever.py:582): host fp32 numpy -> HBM storage, N=1 only ------
+    ingest = None
+    if world == 1 and args.ingest_rows > 0:
+        host = np.full((args.ingest_rows, args.dim), 0.03125, dtype=np.float32)   # pages touched
+        lx = Index(devices=[local], dtype=args.dtype, metric=args.metric)
+        lx.load(host[: min(1024, args.ingest_rows)])                                 # warm the path
+        t = time.perf_counter()
+        lx.load(host)
+        t_load = time.perf_counter() - t
+        lx.close()
+        ingest = {"GBps": round(host.nbytes / t_load / 1e9, 2), "rows": args.ingest_rows,
+                  "seconds": round(t_load, 4),
+                  "note": "rr_load of a pageable host fp32 array: 2 pinned 32 MiB staging buffers, threaded host "
+                          "copy overlapped with H2D DMA + on-device layout/dtype conversion and norms"}
+        del host
+
     variants = {}
     if world == 1 and args.variants:
         for vd in [v for v in args.variants.split(",") if v and v != args.dtype]:
@@ -224,6 +242,7 @@ def main() -> None:
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "other_dtypes": variants or None,
+            "ingest": ingest,
             "dtype_note": {"fp32": "fp32 rows stored exactly; split-K kernel splits corpus and query values exactly "
                                    "into 3 bf16 each, 6 bf16 MFMAs (every kept product exact, dropped terms "
                                    "< 2^-23 |xq|), fp32 accumulate",

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -200,25 +201,62 @@ hipError_t store_rows(rr_handle* h, Shard& s, const float* tmp, int64_t dst_row,
   }
 }
 
-// Copy host fp32 rows into shard storage at local row offset `dst_row`.
+// Host memcpy split over a few threads: one core's memcpy (~10 GB/s) is below PCIe/xGMI DMA rates.
+void par_memcpy(void* dst, const void* src, size_t bytes) {
+  constexpr size_t kPiece = 4u << 20;
+  const int nt = (int)std::min<size_t>(8, (bytes + kPiece - 1) / kPiece);
+  if (nt <= 1) {
+    memcpy(dst, src, bytes);
+    return;
+  }
+  const size_t per = (bytes / nt + 63) & ~(size_t)63;
+  std::vector<std::thread> ts;
+  for (int t = 1; t < nt; ++t) {
+    const size_t o = (size_t)t * per;
+    if (o < bytes)
+      ts.emplace_back([=] { memcpy((char*)dst + o, (const char*)src + o, std::min(per, bytes - o)); });
+  }
+  memcpy(dst, src, std::min(per, bytes));
+  for (auto& t : ts) t.join();
+}
+
+// Copy host fp32 rows into shard storage at local row offset `dst_row` (corpus ingest, main.py:20-23 +
+// retriever.py:582). Pipelined over two pinned staging buffers: while chunk c is DMA'd and converted on
+// the device (pair_unit permutation, bf16 RNE, or split-f16 + norms + scales), the host copies chunk c + 1
+// into the other pinned buffer. The caller's (pageable) array is never pinned or modified.
 int upload_rows(rr_handle* h, Shard& s, const float* src, int64_t dst_row, int64_t nrows) {
   HIP_TRY(hipSetDevice(s.dev));
   const int d = h->d;
-  // stage fp32 chunks on device, convert (pair_unit permutation, bf16 RNE, or split-f16 + norms + scales)
-  const int64_t chunk_rows = std::max<int64_t>(1, (64ll << 20) / (d * 4));
-  float* tmp = nullptr;
-  HIP_TRY(hipMalloc((void**)&tmp, (size_t)std::min(chunk_rows, nrows) * d * 4));
-  for (int64_t r0 = 0; r0 < nrows; r0 += chunk_rows) {
-    const int64_t nr = std::min(chunk_rows, nrows - r0);
-    hipError_t e = hipMemcpy(tmp, src + r0 * d, (size_t)nr * d * 4, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = store_rows(h, s, tmp, dst_row + r0, nr);
-    if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
-    if (e != hipSuccess) {
-      hipFree(tmp);
-      return fail(RR_E_HIP, "corpus upload failed: %s", hipGetErrorString(e));
-    }
+  const int64_t chunk_rows = std::max<int64_t>(1, (32ll << 20) / ((int64_t)d * 4));
+  const size_t chunk_bytes = (size_t)std::min(chunk_rows, nrows) * d * 4;
+  float* pin[2] = {nullptr, nullptr};
+  float* tmp[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  hipError_t e = hipSuccess;
+  for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+    e = hipHostMalloc((void**)&pin[i], chunk_bytes, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc((void**)&tmp[i], chunk_bytes);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&done[i], hipEventDisableTiming);
   }
-  hipFree(tmp);
+  for (int64_t c = 0, r0 = 0; e == hipSuccess && r0 < nrows; ++c, r0 += chunk_rows) {
+    const int i = (int)(c & 1);
+    const int64_t nr = std::min(chunk_rows, nrows - r0);
+    if (c >= 2) e = hipEventSynchronize(done[i]);   // chunk c - 2 has left pin[i] / tmp[i]
+    if (e != hipSuccess) break;
+    par_memcpy(pin[i], src + r0 * d, (size_t)nr * d * 4);
+    e = hipMemcpyAsync(tmp[i], pin[i], (size_t)nr * d * 4, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess) e = store_rows(h, s, tmp[i], dst_row + r0, nr);
+    if (e == hipSuccess) e = hipEventRecord(done[i], s.stream);
+  }
+  const hipError_t es = hipStreamSynchronize(s.stream);
+  if (e == hipSuccess) e = es;
+  for (int i = 0; i < 2; ++i) {
+    if (pin[i]) hipHostFree(pin[i]);
+    if (tmp[i]) hipFree(tmp[i]);
+    if (done[i]) hipEventDestroy(done[i]);
+  }
+  if (e != hipSuccess)
+    return fail(e == hipErrorOutOfMemory ? RR_E_OOM : RR_E_HIP, "corpus upload failed: %s", hipGetErrorString(e));
   return RR_OK;
 }
 

@@ -140,6 +140,30 @@ def test_fp32_split_storage_round_trip(Index):
     assert np.array_equal(ix.read_rows(0, 64), ints)
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp32-split"])
+def test_pipelined_ingest_multi_chunk(Index, dtype):
+    """rr_load streams the host array through two pinned 32 MiB staging buffers (8192 rows of d = 1024 per
+    chunk): 3 full chunks + a ragged one must land exactly (exact-integer rows are exact in every storage
+    dtype) and search identically to the same rows generated on the device."""
+    n = 3 * 8192 + 17
+    rows = synth.exact_int_rows(99, 0, n, 1024)
+    ix = Index(dtype=dtype, metric="cosine")
+    ix.load(rows)
+    for r0 in (0, 8190, 16384, n - 20):
+        assert np.array_equal(ix.read_rows(r0, 20), rows[r0:r0 + 20])
+    gen = Index(dtype=dtype, metric="cosine")
+    gen.fill_synthetic(0, 99, n, 1024)
+    q = rows[[5, 8192, 16385, n - 1]]
+    s1, i1 = ix.search(q, 5)
+    s2, i2 = gen.search(q, 5)
+    assert np.array_equal(i1, i2) and np.array_equal(s1, s2)
+    assert list(i1[:, 0]) == [5, 8192, 16385, n - 1]
+    sh = Index(devices=[0, 0], dtype=dtype, metric="cosine")   # two shards, each its own pipelined upload
+    sh.load(rows)
+    s3, i3 = sh.search(q, 5)
+    assert np.array_equal(i1, i3) and np.array_equal(s1, s3)
+
+
 def test_device_generator_matches_numpy(Index, golden_synth):
     ix = Index(dtype="fp32", metric="dot")
     ix.fill_synthetic(0, 1234, 4099, 1024)
