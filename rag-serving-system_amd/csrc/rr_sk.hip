@@ -39,6 +39,20 @@
 namespace rr {
 namespace sk {
 
+// Phase timestamps per workgroup (s_memrealtime, 100 MHz) for tools/kbench.hip built with -DRR_SK_PROBE;
+// compiled out of the product library.
+#ifdef RR_SK_PROBE
+__device__ unsigned long long probe[4096 * 8];
+#define SK_PROBE(i)                                                   \
+  do {                                                                \
+    if (threadIdx.x == 0) probe[blockIdx.x * 8 + (i)] = wall_clock64(); \
+  } while (0)
+#else
+#define SK_PROBE(i) \
+  do {              \
+  } while (0)
+#endif
+
 constexpr int kSlabRowBytes = 128;                // contiguous bytes of one row per slab
 constexpr int kSlabBytes = 32 * kSlabRowBytes;    // 4 KiB
 constexpr int kRedStride = 36;                    // floats per (wave, query) block of 32 rows (+4 pad)
@@ -137,6 +151,7 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
   static_assert(QH == 1 || QH == 2, "32 or 64 query slots");
   constexpr int QS = 32 * QH;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  SK_PROBE(0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
@@ -151,109 +166,12 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
   float* qinfo = seg + kSegRows * (SW > 0 ? SW : 1);            // [QS] |q|, [QS] 2^-e (split), [QS] int e
   int* qexp = (int*)(qinfo + 2 * QS);
 
-  // ---- per-query scalars: |q| (cosine, fp32 as cp.linalg.norm, retriever.py:602) and split exponents
-  if (COS || DT == 2) {
-    for (int q = w * 4 * QH; q < (w + 1) * 4 * QH; ++q) {
-      float ss = 0.f, m = 0.f;
-      if (q < b)
-        for (int c = lane; c < (d >> 2); c += 64) {
-          const f32x4 v = ((const f32x4*)queries)[(size_t)q * (d >> 2) + c];
-          ss = fmaf(v.x, v.x, ss); ss = fmaf(v.y, v.y, ss); ss = fmaf(v.z, v.z, ss); ss = fmaf(v.w, v.w, ss);
-          m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-        }
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) {
-        ss += __shfl_xor(ss, off, 64);
-        m = fmaxf(m, __shfl_xor(m, off, 64));
-      }
-      int E = 0;
-      if (m > 0.f) frexpf(m, &E);
-      const int ex = m > 0.f ? 15 - E : 0;
-      if (lane == 0) {
-        qinfo[q] = sqrtf(ss);
-        qinfo[QS + q] = ldexpf(1.0f, -ex);
-        qexp[q] = ex;
-      }
-    }
-    __syncthreads();
-  }
-
-  // ---- this wave's K-slice of every query as MFMA B operands (lane: query r, K half h) ----------------
-  QFrag<DT, NS> qfs[QH];
-#pragma unroll
-  for (int qh = 0; qh < QH; ++qh) {
-    QFrag<DT, NS>& qf = qfs[qh];
-    const int rq = r + 32 * qh;
-    const bool qv = rq < b;
-    const float* qrow = queries + (size_t)(qv ? rq : 0) * d;
-    auto qval = [&](int e) -> float { return qv ? qrow[e] : 0.f; };
-#pragma unroll
-    for (int j = 0; j < NS; ++j) {
-      if constexpr (DT == 0) {
-        // MFMA m of slab j: lane half h holds position 4h + (m >> 2), element m & 3
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-          const int P = p0 + 8 * j + 4 * h + (m >> 2);
-          qf.v[j][m] = qval(4 * inv_pair(P) + (m & 3));
-        }
-      } else if constexpr (DT == 1) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {   // K-step t: lane half h reads position 2t + h (8 bf16)
-          const int L = inv_pair(p0 + 8 * j + 2 * t + h);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float x = qval(8 * L + e);
-            const __bf16 bh = (__bf16)x;
-            qf.hi[j][t][e] = bh;
-            qf.lo[j][t][e] = (__bf16)(x - (float)bh);
-          }
-        }
-      } else if constexpr (DT == 2) {
-        const int ex = qv ? qexp[rq] : 0;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {   // K-step t: lane half h reads units 4t + 2h (hi), + 1 (lo)
-          const int g8 = (p0 + 8 * j + 4 * t + 2 * h) >> 1;   // 8-element group
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float xs = ldexpf(qval(8 * g8 + e), ex);
-            const _Float16 fh = (_Float16)xs;
-            qf.hi[j][t][e] = fh;
-            qf.lo[j][t][e] = (_Float16)(xs - (float)fh);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {   // K-step t: lane half h reads positions 4t + 2h, 4t + 2h + 1
-          float x[8];
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int L = inv_pair(p0 + 8 * j + 4 * t + 2 * h + u);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) x[4 * u + e] = qval(4 * L + e);
-          }
-          split3(x, qf.c0[j][t], qf.c1[j][t], qf.c2[j][t]);
-        }
-      }
-    }
-  }
-
   // ---- this workgroup's rows ----------------------------------------------------------------------------
   const int64_t G = gridDim.x, g = blockIdx.x;
   const int64_t per = n / G, rem = n % G;
   const int64_t r0 = g * per + (g < rem ? g : rem);
   const int64_t r1 = r0 + per + (g < rem ? 1 : 0);
   const int64_t ntile = (r1 - r0 + 31) / 32;
-
-  // epilogue lane mapping: wave w owns queries 4·QH·w + [0, 4·QH); LPQ lanes per query, each with DPL
-  // consecutive tile rows (QH 1: 16 lanes x 2 rows, QH 2: 8 lanes x 4 rows)
-  constexpr int LPQ = 16 / QH, DPL = 2 * QH;
-  const int qe = 4 * QH * w + lane / LPQ, er = DPL * (lane % LPQ);
-  const bool qev = qe < b;
-  const float qn = COS ? qinfo[qe] : 0.f;
-  const float qs = DT == 2 ? qinfo[QS + qe] : 1.f;
-
-  TopK<KT> tk;
-  tk.init();
 
   // LDS-DMA lane mapping: instruction i of a slab covers tile rows 8i + lane/8, 16-byte column
   // (lane % 8) ^ (lane / 8) of the slab — so the image holds column c of row r at c ^ (r & 7)
@@ -271,12 +189,145 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
     }
   };
 
-  int64_t seg_lo = INT64_MIN / 2;
   const int64_t total = ntile * NS;                   // slabs this wave consumes
   // prologue: the first RS - 1 slabs (slab p = tile p / NS, column block p % NS, slot p)
 #pragma unroll
   for (int p = 0; p < RS - 1; ++p)
     if (p < total) issue(p / NS, p % NS, p);
+  // ---- query side: this wave's K-slice of every query as MFMA B operands, |q| and split exponents.
+  // Runs while the prologue slabs above are in flight (their latency overlaps the query loads).
+  QFrag<DT, NS> qfs[QH];
+  auto build_frags = [&]() {
+    // lane: query r (+ 32 per half), K half h
+#pragma unroll
+    for (int qh = 0; qh < QH; ++qh) {
+      QFrag<DT, NS>& qf = qfs[qh];
+      const int rq = r + 32 * qh;
+      const bool qv = rq < b;
+      const float* qrow = queries + (size_t)(qv ? rq : 0) * d;
+      // 16-byte loads of 4 consecutive elements (e % 4 == 0), unconditional (rows >= b read row 0) and
+      // zeroed by a select: no per-element exec-masked branches around the loads
+      auto qvec = [&](int e) -> f32x4 {
+        const f32x4 v = *(const f32x4*)(qrow + e);
+        return qv ? v : (f32x4){0.f, 0.f, 0.f, 0.f};
+      };
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        if constexpr (DT == 0) {
+          // MFMA m of slab j: lane half h holds position 4h + (m >> 2), element m & 3
+#pragma unroll
+          for (int m4 = 0; m4 < 4; ++m4) {
+            const f32x4 v = qvec(4 * inv_pair(p0 + 8 * j + 4 * h + m4));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) qf.v[j][4 * m4 + e] = v[e];
+          }
+        } else if constexpr (DT == 1) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {   // K-step t: lane half h reads position 2t + h (8 bf16)
+            const int L = inv_pair(p0 + 8 * j + 2 * t + h);
+            const f32x4 va = qvec(8 * L), vb = qvec(8 * L + 4);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float x = e < 4 ? va[e] : vb[e - 4];
+              const __bf16 bh = (__bf16)x;
+              qf.hi[j][t][e] = bh;
+              qf.lo[j][t][e] = (__bf16)(x - (float)bh);
+            }
+          }
+        } else if constexpr (DT == 2) {
+          const int ex = qv ? qexp[rq] : 0;
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {   // K-step t: lane half h reads units 4t + 2h (hi), + 1 (lo)
+            const int g8 = (p0 + 8 * j + 4 * t + 2 * h) >> 1;   // 8-element group
+            const f32x4 va = qvec(8 * g8), vb = qvec(8 * g8 + 4);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float xs = ldexpf(e < 4 ? va[e] : vb[e - 4], ex);
+              const _Float16 fh = (_Float16)xs;
+              qf.hi[j][t][e] = fh;
+              qf.lo[j][t][e] = (_Float16)(xs - (float)fh);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {   // K-step t: lane half h reads positions 4t + 2h, 4t + 2h + 1
+            float x[8];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const f32x4 v = qvec(4 * inv_pair(p0 + 8 * j + 4 * t + 2 * h + u));
+#pragma unroll
+              for (int e = 0; e < 4; ++e) x[4 * u + e] = v[e];
+            }
+            split3(x, qf.c0[j][t], qf.c1[j][t], qf.c2[j][t]);
+          }
+        }
+      }
+    }
+  };
+  if constexpr (DT != 2) build_frags();
+  // ---- per-query scalars: |q| (cosine, fp32 as cp.linalg.norm, retriever.py:602) and split exponents.
+  // All loads of a group of 4 queries are issued before any is used (one L2/HBM latency per group, not
+  // one per query); the sums are the same lane-strided fmaf chains + xor tree in the same order.
+  if (COS || DT == 2) {
+    const int nc = d >> 2;                      // float4 per row (d <= 1024 on this kernel: <= 4 per lane)
+#pragma unroll
+    for (int g4 = 0; g4 < QH; ++g4) {
+      f32x4 v[4][4];
+#pragma unroll
+      for (int qi = 0; qi < 4; ++qi) {
+        const int q = w * 4 * QH + 4 * g4 + qi;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int cc = lane + 64 * c;
+          const f32x4 x = ((const f32x4*)queries)[(size_t)(q < b ? q : 0) * nc + (cc < nc ? cc : 0)];
+          v[qi][c] = (q < b && cc < nc) ? x : (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+      }
+#pragma unroll
+      for (int qi = 0; qi < 4; ++qi) {
+        const int q = w * 4 * QH + 4 * g4 + qi;
+        float ss = 0.f, m = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (lane + 64 * c < nc) {
+            const f32x4 x = v[qi][c];
+            ss = fmaf(x.x, x.x, ss); ss = fmaf(x.y, x.y, ss); ss = fmaf(x.z, x.z, ss); ss = fmaf(x.w, x.w, ss);
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+          }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+          ss += __shfl_xor(ss, off, 64);
+          m = fmaxf(m, __shfl_xor(m, off, 64));
+        }
+        int E = 0;
+        if (m > 0.f) frexpf(m, &E);
+        const int ex = m > 0.f ? 15 - E : 0;
+        if (lane == 0) {
+          qinfo[q] = sqrtf(ss);
+          qinfo[QS + q] = ldexpf(1.0f, -ex);
+          qexp[q] = ex;
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  if constexpr (DT == 2) build_frags();
+
+  // epilogue lane mapping: wave w owns queries 4·QH·w + [0, 4·QH); LPQ lanes per query, each with DPL
+  // consecutive tile rows (QH 1: 16 lanes x 2 rows, QH 2: 8 lanes x 4 rows)
+  constexpr int LPQ = 16 / QH, DPL = 2 * QH;
+  const int qe = 4 * QH * w + lane / LPQ, er = DPL * (lane % LPQ);
+  const bool qev = qe < b;
+  const float qn = COS ? qinfo[qe] : 0.f;
+  const float qs = DT == 2 ? qinfo[QS + qe] : 1.f;
+
+  TopK<KT> tk;
+  tk.init();
+
+  SK_PROBE(1);
+  int64_t seg_lo = INT64_MIN / 2;
   int slot = 0;                                       // slot of the slab being consumed
   for (int64_t tile = 0; tile < ntile; ++tile) {
     f32x16 accs[QH];
@@ -433,7 +484,10 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
         if (valid && key > tk.last()) tk.insert(key);
       }
     }
+    if (tile == 0) SK_PROBE(2);
+    if (tile == 1) SK_PROBE(3);
   }
+  SK_PROBE(4);
 
   // ---- per query: merge its LPQ lane lists (KT rounds of an LPQ-lane max; keys are unique) -------------
   uint64_t* dst = out + ((size_t)g * QS + qe) * KT;
@@ -449,6 +503,7 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
     if (m != 0 && tk.v[0] == m) tk.pop();
     if (lane % LPQ == 0) dst[rnd] = m;
   }
+  SK_PROBE(5);
 }
 
 template <int DT, int NS, int KT, bool COS, int RS, int QH>

@@ -8,6 +8,7 @@
 #include "../rag-serving-system_amd/csrc/rr_kernels.hip"
 #include "../rag-serving-system_amd/csrc/rr_sk.hip"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -254,6 +255,38 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&fin, kQSlots * kt * 8));
   unsigned* sink;
   CK(hipMalloc(&sink, (size_t)grid * 4 * 8 * 64 * 4));  // room for the x4 grid
+#ifdef RR_SK_PROBE
+  if (argc > 3 && strcmp(argv[3], "probe") == 0) {   // per-workgroup phase timestamps of the split-K kernel
+    struct P { const char* name; int dt; const void* c; const float* nr; };
+    const P ps[] = {{"sk fp32 (DT 3) cos", 3, c32, norms}, {"sk bf16 (DT 1) cos", 1, c16, norms}};
+    std::vector<unsigned long long> h((size_t)grid * 8);
+    for (const P& p : ps) {
+      for (int rep = 0; rep < 4; ++rep) {
+        CK(launch_sk(p.dt, 1, 8, grid, p.c, p.nr, rscale, q, n, d, b, 0, cand, s, 2));
+        CK(hipStreamSynchronize(s));
+      }
+      CK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(rr::sk::probe), h.size() * 8));
+      unsigned long long t0min = ~0ull, t0max = 0, t5max = 0;
+      for (int g = 0; g < grid; ++g) {
+        t0min = std::min(t0min, h[g * 8]); t0max = std::max(t0max, h[g * 8]); t5max = std::max(t5max, h[g * 8 + 5]);
+      }
+      printf("{\"probe\": \"%s\", \"n\": %lld, \"start_spread_us\": %.2f, \"span_us\": %.2f", p.name, (long long)n,
+             (t0max - t0min) / 100.0, (t5max - t0min) / 100.0);
+      const char* ph[] = {"prep", "tile0", "tile1", "rest", "merge"};
+      for (int i = 1; i <= 5; ++i) {
+        std::vector<double> v;
+        for (int g = 0; g < grid; ++g) v.push_back((double)(h[g * 8 + i] - h[g * 8 + i - 1]) / 100.0);
+        std::sort(v.begin(), v.end());
+        printf(", \"%s_us\": [%.2f, %.2f, %.2f]", ph[i - 1], v[0], v[v.size() / 2], v.back());
+      }
+      std::vector<double> e;
+      for (int g = 0; g < grid; ++g) e.push_back((double)(h[g * 8 + 5] - t0min) / 100.0);
+      std::sort(e.begin(), e.end());
+      printf(", \"end_us_min_med_max\": [%.2f, %.2f, %.2f]}\n", e[0], e[e.size() / 2], e.back());
+    }
+    return 0;
+  }
+#endif
 #define V32(NB, LM, AS, COS, DBG, U) Variant{"fp32 NB=" #NB " LM=" #LM " AS=" #AS " COS=" #COS " DBG=" #DBG " U=" #U, 0, \
     [&](const void* c, uint64_t* o) { return launch_fused_t<0, 8, COS, 0, NB, LM, AS, DBG, U>(grid, c, norms, rscale, q, n, d, b, 0, o, s); }, {}}
 #define V16(NB, LM, AS, COS, DBG, U) Variant{"bf16 NB=" #NB " LM=" #LM " AS=" #AS " COS=" #COS " DBG=" #DBG " U=" #U, 1, \
