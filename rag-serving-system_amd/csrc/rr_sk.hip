@@ -123,6 +123,20 @@ __device__ __forceinline__ void split3(const float (&x)[8], bf16x8& b0, bf16x8& 
   b2 = __builtin_bit_cast(bf16x8, p2);
 }
 
+// All-ones / all-zeros lane mask the compiler cannot see through, and x AND-ed with it: the loads that
+// feed it are then issued unconditionally (a select on the predicate gets turned into exec-masked branches
+// around each load, which serialises their latencies). Exact zeros, whatever x holds.
+__device__ __forceinline__ uint32_t opaque_mask(bool keep) {
+  uint32_t m = keep ? 0xFFFFFFFFu : 0u;
+  asm volatile("" : "+v"(m));
+  return m;
+}
+__device__ __forceinline__ f32x4 zero_unless(f32x4 x, uint32_t m) {
+  u32x4 u = __builtin_bit_cast(u32x4, x);
+  u &= (u32x4){m, m, m, m};
+  return __builtin_bit_cast(f32x4, u);
+}
+
 // Query operand (B) fragments of one wave's K-slice, per slab j and K-step.
 template <int DT, int NS>
 struct QFrag;
@@ -205,12 +219,10 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
       const int rq = r + 32 * qh;
       const bool qv = rq < b;
       const float* qrow = queries + (size_t)(qv ? rq : 0) * d;
+      const uint32_t qmask = opaque_mask(qv);
       // 16-byte loads of 4 consecutive elements (e % 4 == 0), unconditional (rows >= b read row 0) and
       // zeroed by a select: no per-element exec-masked branches around the loads
-      auto qvec = [&](int e) -> f32x4 {
-        const f32x4 v = *(const f32x4*)(qrow + e);
-        return qv ? v : (f32x4){0.f, 0.f, 0.f, 0.f};
-      };
+      auto qvec = [&](int e) -> f32x4 { return zero_unless(*(const f32x4*)(qrow + e), qmask); };
 #pragma unroll
       for (int j = 0; j < NS; ++j) {
         if constexpr (DT == 0) {
@@ -280,7 +292,7 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
         for (int c = 0; c < 4; ++c) {
           const int cc = lane + 64 * c;
           const f32x4 x = ((const f32x4*)queries)[(size_t)(q < b ? q : 0) * nc + (cc < nc ? cc : 0)];
-          v[qi][c] = (q < b && cc < nc) ? x : (f32x4){0.f, 0.f, 0.f, 0.f};
+          v[qi][c] = zero_unless(x, opaque_mask(q < b && cc < nc));
         }
       }
 #pragma unroll
