@@ -108,7 +108,9 @@ int rr_init_dist(rr_handle* h, int world, int rank, const char* unique_id);
 
 /* Load the whole corpus (row-major fp32, n x d) from host memory. In a multi-process world every
  * rank passes the full matrix and keeps only its shard. Converts to bf16 (RNE) for RR_DTYPE_BF16
- * and precomputes per-row L2 norms for RR_METRIC_COSINE. (retriever.py:576-582)  */
+ * and precomputes per-row L2 norms for RR_METRIC_COSINE. (retriever.py:576-582)
+ * The host array may be pageable; it is streamed through two pinned 32 MiB staging buffers (threaded host
+ * copy overlapped with the DMA and the on-device conversion) and is never pinned or modified. */
 int rr_load(rr_handle* h, const float* host_corpus, int64_t n, int32_t d);
 
 /* Load only this handle's shard(s): host_rows holds rows [row_begin, row_begin + n_rows) of a
