@@ -71,8 +71,13 @@ struct Shard {
   hipEvent_t ev_keys[2] = {nullptr, nullptr};   // compute stream: px_keys[p] written
   hipEvent_t ev_xdone[2] = {nullptr, nullptr};  // xstream: exchange of parity p finished (buffers free)
   hipEvent_t ev_cdone = nullptr;                // compute stream: a serial (k > KMAX) exchange finished
+  char* out_base = nullptr;              // one allocation: scores at 0, indices at out_off
   float* out_scores = nullptr;           // [q_cap][k_cap]
   int64_t* out_idx = nullptr;            // [q_cap][k_cap]
+  size_t out_off = 0;
+  float* pin_q = nullptr;                // pinned host staging of the queries (rr_set_queries)
+  size_t pin_q_cap = 0;
+  hipEvent_t pin_q_free = nullptr;       // the last H2D out of pin_q has completed
   int k_cap = 0;
   // k > RR_FUSED_KMAX path
   uint64_t* full_keys = nullptr;         // [32][max(rows, world*k)]
@@ -108,6 +113,9 @@ struct rr_handle {
   int parity = 0;                // pipelined exchange: buffer set of the next search block
   double t_ms = 0.0;
   int64_t t_count = 0;
+  // pinned host staging for the synchronous search path (rr_set_queries / rr_fetch_results)
+  char* pin_out = nullptr;
+  size_t pin_out_cap = 0;
 };
 
 namespace {
@@ -146,13 +154,15 @@ int dmalloc(T** p, size_t bytes) {
 
 int free_shard(Shard& s) {
   hipSetDevice(s.dev);
-  void* ptrs[] = {s.corpus, s.norms, s.rscale, s.queries, s.cand, s.shard_keys, s.gathered, s.out_scores, s.out_idx,
+  void* ptrs[] = {s.corpus, s.norms, s.rscale, s.queries, s.cand, s.shard_keys, s.gathered, s.out_base,
                   s.full_keys, s.sorted, s.sort_temp, s.px_keys[0], s.px_keys[1], s.px_gathered[0], s.px_gathered[1]};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (hipEvent_t e : s.ev) hipEventDestroy(e);
   s.ev.clear();
   if (s.keys_ready) hipEventDestroy(s.keys_ready);
+  if (s.pin_q) hipHostFree(s.pin_q);
+  if (s.pin_q_free) hipEventDestroy(s.pin_q_free);
   if (s.copies_done) hipEventDestroy(s.copies_done);
   for (hipEvent_t e : {s.ev_keys[0], s.ev_keys[1], s.ev_xdone[0], s.ev_xdone[1], s.ev_cdone})
     if (e) hipEventDestroy(e);
@@ -293,8 +303,11 @@ int ensure_buffers(rr_handle* h, int b, int k) {
         if (int rc = dmalloc(&s.queries, (size_t)((qc + kMaxSlots - 1) / kMaxSlots * kMaxSlots) * h->d * 4)) return rc;
         HIP_TRY(hipMemset(s.queries, 0, (size_t)((qc + kMaxSlots - 1) / kMaxSlots * kMaxSlots) * h->d * 4));
       }
-      if (int rc = dmalloc(&s.out_scores, (size_t)qc * kc * 4)) return rc;
-      if (int rc = dmalloc(&s.out_idx, (size_t)qc * kc * 8)) return rc;
+      // scores and indices in one allocation, so a search's results come back in ONE D2H copy
+      s.out_off = ((size_t)qc * kc * 4 + 255) & ~(size_t)255;
+      if (int rc = dmalloc(&s.out_base, s.out_off + (size_t)qc * kc * 8)) return rc;
+      s.out_scores = (float*)s.out_base;
+      s.out_idx = (int64_t*)(s.out_base + s.out_off);
       const int kk = std::max(kc, RR_FUSED_KMAX);
       if (int rc = dmalloc(&s.shard_keys, (size_t)rr::kQSlots * kk * 8)) return rc;
       if (int rc = dmalloc(&s.gathered, (size_t)h->world * rr::kQSlots * kk * 8)) return rc;
@@ -613,6 +626,8 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
 void rr_destroy(rr_handle* h) {
   if (!h) return;
   for (Shard& s : h->shards) free_shard(s);
+  if (h->pin_out) hipHostFree(h->pin_out);
+
   delete h;
 }
 
@@ -756,9 +771,23 @@ int rr_set_queries(rr_handle* h, const float* host_q, int32_t b, int32_t d) {
   if (d != h->d) return fail(RR_E_INVALID, "query dim %d != corpus dim %d", d, h->d);
   if (b < 1) return fail(RR_E_INVALID, "b=%d", b);
   if (int rc = ensure_buffers(h, b, 1)) return rc;
+  // stage through a pinned buffer per shard (the copy is then a plain async DMA); a buffer is rewritten
+  // only after the previous batch's copy out of it has completed
+  const size_t qbytes = (size_t)b * d * 4;
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
-    HIP_TRY(hipMemcpyAsync(s.queries, host_q, (size_t)b * d * 4, hipMemcpyHostToDevice, s.stream));
+    if (s.pin_q_free) HIP_TRY(hipEventSynchronize(s.pin_q_free));
+    else HIP_TRY(hipEventCreateWithFlags(&s.pin_q_free, hipEventDisableTiming));
+    if (qbytes > s.pin_q_cap) {
+      if (s.pin_q) HIP_TRY(hipHostFree(s.pin_q));
+      s.pin_q = nullptr;
+      s.pin_q_cap = 0;
+      HIP_TRY(hipHostMalloc((void**)&s.pin_q, qbytes, hipHostMallocDefault));
+      s.pin_q_cap = qbytes;
+    }
+    memcpy(s.pin_q, host_q, qbytes);
+    HIP_TRY(hipMemcpyAsync(s.queries, s.pin_q, qbytes, hipMemcpyHostToDevice, s.stream));
+    HIP_TRY(hipEventRecord(s.pin_q_free, s.stream));
   }
   h->cur_b = b;
   return RR_OK;
@@ -814,8 +843,23 @@ int rr_fetch_results(rr_handle* h, float* out_scores, int64_t* out_idx) {
   Shard& s = h->shards[0];
   HIP_TRY(hipSetDevice(s.dev));
   const size_t cnt = (size_t)h->cur_b * h->last_k;
-  HIP_TRY(hipMemcpy(out_scores, s.out_scores, cnt * 4, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(out_idx, s.out_idx, cnt * 8, hipMemcpyDeviceToHost));
+  const size_t span = s.out_off + cnt * 8;
+  if (s.out_off > (1u << 20)) {   // capacity grown far beyond this search: two plain copies
+    HIP_TRY(hipMemcpy(out_scores, s.out_scores, cnt * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(out_idx, s.out_idx, cnt * 8, hipMemcpyDeviceToHost));
+    return RR_OK;
+  }
+  if (span > h->pin_out_cap) {
+    if (h->pin_out) HIP_TRY(hipHostFree(h->pin_out));
+    h->pin_out = nullptr;
+    h->pin_out_cap = 0;
+    HIP_TRY(hipHostMalloc((void**)&h->pin_out, span, hipHostMallocDefault));
+    h->pin_out_cap = span;
+  }
+  // one pinned D2H of [scores | pad | indices] (the stream is idle: rr_synchronize above)
+  HIP_TRY(hipMemcpy(h->pin_out, s.out_base, span, hipMemcpyDeviceToHost));
+  memcpy(out_scores, h->pin_out, cnt * 4);
+  memcpy(out_idx, h->pin_out + s.out_off, cnt * 8);
   return RR_OK;
 }
 
