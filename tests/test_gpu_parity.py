@@ -255,6 +255,26 @@ def test_staged_api_and_determinism(Index, squad, golden_data):
     assert np.array_equal(i1, i3)
 
 
+def test_reused_handle_batch_and_k_changes(Index):
+    """One handle, successive synchronous searches whose batch and k grow and shrink (pinned query staging
+    and the single-allocation result buffer are re-sized and re-used; k > 32 takes the sort path): every
+    result equals a fresh handle's."""
+    rng = np.random.default_rng(11)
+    corpus = rng.standard_normal((6000, 256)).astype(np.float32)
+    ix = Index(dtype="fp32", metric="cosine")
+    ix.load(corpus)
+    for b, k in [(5, 5), (70, 8), (32, 40), (1, 3), (64, 100), (3, 1), (70, 8)]:
+        q = rng.standard_normal((b, 256)).astype(np.float32)
+        s1, i1 = ix.search(q, k)
+        fresh = Index(dtype="fp32", metric="cosine")
+        fresh.load(corpus)
+        s2, i2 = fresh.search(q, k)
+        fresh.close()
+        assert s1.shape == (b, k) and np.array_equal(i1, i2) and np.array_equal(s1, s2)
+        _, cidx = canonical_topk(exact_scores(corpus, q, "cosine"), k)
+        check_topk(i1, s1, cidx, corpus, q, "cosine", near_tie=1e-5 * 16, score_tol=1e-3)
+
+
 def test_device_pointer_queries(Index, squad, golden_data):
     torch = pytest.importorskip("torch")
     ix = get_index(Index, "sq", squad, "fp32", "cosine")
