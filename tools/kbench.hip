@@ -257,12 +257,13 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&sink, (size_t)grid * 4 * 8 * 64 * 4));  // room for the x4 grid
 #ifdef RR_SK_PROBE
   if (argc > 3 && strcmp(argv[3], "probe") == 0) {   // per-workgroup phase timestamps of the split-K kernel
-    struct P { const char* name; int dt; const void* c; const float* nr; };
-    const P ps[] = {{"sk fp32 (DT 3) cos", 3, c32, norms}, {"sk bf16 (DT 1) cos", 1, c16, norms}};
+    struct P { const char* name; int dt; int cos; const void* c; const float* nr; };
+    const P ps[] = {{"sk fp32 (DT 3) cos", 3, 1, c32, norms}, {"sk bf16 (DT 1) cos", 1, 1, c16, norms},
+                    {"sk fp32 (DT 3) dot", 3, 0, c32, norms}};
     std::vector<unsigned long long> h((size_t)grid * 8);
     for (const P& p : ps) {
       for (int rep = 0; rep < 4; ++rep) {
-        CK(launch_sk(p.dt, 1, 8, grid, p.c, p.nr, rscale, q, n, d, b, 0, cand, s, 2));
+        CK(launch_sk(p.dt, p.cos, 8, grid, p.c, p.nr, rscale, q, n, d, b, 0, cand, s, 2));
         CK(hipStreamSynchronize(s));
       }
       CK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(rr::sk::probe), h.size() * 8));
