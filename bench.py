@@ -3,7 +3,11 @@
 batch 32, top-k 5, fused similarity + top-k through the C-ABI).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp32|bf16] [--metric cosine|dot]
-    N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+N > 1 runs one process per GPU. Under torch.distributed.run (RANK/WORLD_SIZE set) this process is one
+rank; started plainly (`python bench.py --gpus N`), it launches `python -m torch.distributed.run
+--nproc-per-node N --master-addr 127.0.0.1 ... bench.py` as a CHILD before touching any GPU and exits
+with its status (no exec).
 
 A step = one batch of B queries through the whole device pipeline (fused MFMA similarity + top-k over
 the rank's corpus shard, per-shard merge, RCCL all-gather of candidates when N > 1, final merge), with
@@ -37,23 +41,59 @@ def is_score_kernel(name: str) -> bool:
     return "sk_score_kernel" in name or "fused_score_kernel" in name
 
 
-def cpu_baseline(n_docs: int, d: int, batch: int, k: int, batches: int, threads: int) -> dict:
-    """Reference SimpleRetriever algorithm (oracle restatement) on the host: bounded sample."""
-    from threadpoolctl import threadpool_limits
+def host_cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(n_docs: int, d: int, batch: int, k: int, budget_s: float) -> dict:
+    """The reference algorithm on the host: the oracle restatement of
+    SimpleRetriever.batch_retrieve (retriever.py:131-166: per-query fp32 sgemv + argpartition + argsort)
+    over a bounded sample of batches (as many as fit `budget_s`, at least one), on every core this process
+    may run on, plus the stronger batched point (one Q @ A.T sgemm per batch + per-row argpartition)."""
+    from threadpoolctl import threadpool_info, threadpool_limits
     from oracle import synth
     from oracle.retriever_oracle import simple_batch_retrieve
+    # every core this process may use: its affinity set, capped by the CPU share the host grants it
+    # (OMP_NUM_THREADS; 16 per GPU on the MI355X pool, whose os.cpu_count() shows the whole machine)
+    cores = len(os.sched_getaffinity(0))
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        cores = min(cores, int(os.environ["OMP_NUM_THREADS"]))
     corpus = synth.unit_norm_gaussian(4321, n_docs, d)
-    q = synth.unit_norm_gaussian(8765, batch * batches, d)
-    with threadpool_limits(limits=threads):
+    q = synth.unit_norm_gaussian(8765, batch * 64, d)
+    with threadpool_limits(limits=cores):
+        blas = [{"api": i.get("internal_api"), "version": i.get("version"), "threads": i.get("num_threads")}
+                for i in threadpool_info()]
         simple_batch_retrieve(corpus, q[:2], [k, k])            # warm
         t0 = time.perf_counter()
-        for i in range(batches):
-            simple_batch_retrieve(corpus, q[i * batch:(i + 1) * batch], [k] * batch)
+        nb = 0
+        while nb < 64 and (nb == 0 or time.perf_counter() - t0 < budget_s):
+            simple_batch_retrieve(corpus, q[nb * batch:(nb + 1) * batch], [k] * batch)
+            nb += 1
         dt = time.perf_counter() - t0
-    return {"value": round(batch * batches / dt, 3), "unit": "queries/s", "cores": threads, "kind": "port",
-            "sample": f"{batches} batches x {batch} queries, {n_docs} x {d} fp32 unit-norm corpus, k={k}; "
+        # batched variant: one sgemm for the whole batch, then the same per-row top-k selection
+        t1 = time.perf_counter()
+        nb2 = 0
+        while nb2 < 64 and (nb2 == 0 or time.perf_counter() - t1 < budget_s / 3):
+            qb = q[nb2 * batch:(nb2 + 1) * batch]
+            sims = qb @ corpus.T
+            top = np.argpartition(sims, -k, axis=1)[:, -k:]
+            np.take_along_axis(top, np.argsort(-np.take_along_axis(sims, top, axis=1), axis=1), axis=1)
+            nb2 += 1
+        dt2 = time.perf_counter() - t1
+    return {"value": round(batch * nb / dt, 3), "unit": "queries/s", "cores": cores, "kind": "port",
+            "cpu_model": host_cpu_model(), "os_cpu_count": os.cpu_count(), "blas": blas,
+            "sample": f"{nb} batches x {batch} queries ({dt:.1f} s), {n_docs} x {d} fp32 unit-norm corpus, k={k}; "
                       f"oracle restatement of SimpleRetriever.batch_retrieve (retriever.py:131-166), "
-                      f"OpenBLAS limited to {threads} threads"}
+                      f"BLAS on {cores} threads (the cores granted to this process)",
+            "batched_sgemm": {"value": round(batch * nb2 / dt2, 2), "unit": "queries/s", "batches": nb2,
+                              "note": "not the reference algorithm: one Q @ A.T sgemm per batch + per-row "
+                                      "argpartition/argsort (a stronger CPU point)"}}
 
 
 def algorithmic_bytes(rows: int, d: int, batch: int, dtype: str, metric: str) -> int:
@@ -92,6 +132,22 @@ def timed_steps(ix, k, steps, warmup, dist, cuda_sync, every=1):
     return elapsed, kern_ms, launches
 
 
+def spawn_ranks(n: int) -> int:
+    """Run this script under torch.distributed.run with one rank per GPU, as a child process (this process
+    has not touched the GPU). Returns the child's exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -107,16 +163,27 @@ def main() -> None:
     ap.add_argument("--variant-steps", type=int, default=100)
     ap.add_argument("--metric", default="cosine", choices=["cosine", "dot"])
     ap.add_argument("--latency-steps", type=int, default=200)
-    ap.add_argument("--timing-every", type=int, default=10,
-                    help="bracket the similarity kernel with HIP events on every N-th timed step")
+    ap.add_argument("--timing-every", type=int, default=0,
+                    help="bracket the similarity kernel with HIP events on every N-th timed step "
+                         "(0: every step when --steps < 100, else every 10th)")
+    ap.add_argument("--steady-steps", type=int, default=300,
+                    help="back-to-back steps timed again after the latency loop (steady-state rate, reported "
+                         "beside value)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ingest-rows", type=int, default=262_144,
                     help="rows of a host fp32 array timed through rr_load (N=1 only; 0 = skip)")
-    ap.add_argument("--cpu-batches", type=int, default=3)
+    ap.add_argument("--cpu-budget", type=float, default=12.0,
+                    help="seconds of per-query CPU baseline work (at least one batch)")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the rocprofv3 --pmc FETCH_SIZE child pass that fills roofline.traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / control-plane check without a GPU: every rank joins the gloo group, "
+                         "reaches the timed-loop barrier and rank 0 prints one JSON line")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    every = args.timing_every or (1 if args.steps < 100 else 10)
 
     from rag_service_amd import Index, get_unique_id
     from rag_service_amd import _lib
@@ -124,10 +191,16 @@ def main() -> None:
                                       max_over_ranks)
 
     rank, world, local = env_rank_world()
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank per GPU)")
     dist = init_control_plane(world, rank)
+    if args.dry_run:
+        barrier(dist)
+        ranks_seen = max_over_ranks(dist, float(rank)) + 1
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": int(ranks_seen),
+                              "launched_by": "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ
+                              else "plain"}), flush=True)
+        barrier(dist)
+        return
 
     try:
         import torch
@@ -138,9 +211,11 @@ def main() -> None:
             return None
 
     ix = Index(devices=[local], dtype=args.dtype, metric=args.metric)
+    rccl_ranks = 0
     if world > 1:
         uid = broadcast_bytes(dist, get_unique_id() if rank == 0 else None)
         ix.init_dist(world, rank, uid)
+        rccl_ranks = ix.dist_info()[0]
     ix.fill_synthetic(_lib.RR_SYNTH_UNIT_NORM, 1234, args.docs, args.dim)
     sb, se = ix.shard_range(0)
     rng = np.random.default_rng(5678)
@@ -149,8 +224,7 @@ def main() -> None:
 
     # ---- throughput: queries resident in HBM, K back-to-back steps --------------------------------
     ix.set_queries(q)
-    elapsed, kern_ms, launches = timed_steps(ix, args.k, args.steps, args.warmup, dist, cuda_sync,
-                                             args.timing_every)
+    elapsed, kern_ms, launches = timed_steps(ix, args.k, args.steps, args.warmup, dist, cuda_sync, every)
     elapsed = max_over_ranks(dist, elapsed)
 
     # ---- latency: host queries in -> host results out, one batch at a time ------------------------
@@ -165,11 +239,31 @@ def main() -> None:
     p99 = max_over_ranks(dist, float(np.percentile(lat_ms, 99)))
     _, head_idx = ix.search(q, args.k)
 
+    # ---- pipelined host-inclusive rate: H2D + search + D2H of each batch enqueued asynchronously, two
+    # batches in flight (rr_search_async / rr_wait), the cost the reference's batch_retrieve pays
+    # (retriever.py:738,773) ---------------------------------------------------------------------------
+    barrier(dist)
+    t = time.perf_counter()
+    tickets = []
+    for i in range(args.latency_steps):
+        tickets.append(ix.search_async(q, args.k))
+        if len(tickets) == 2:
+            ix.wait(tickets.pop(0))
+    for tk in tickets:
+        ix.wait(tk)
+    host_pipe_s = max_over_ranks(dist, time.perf_counter() - t)
+
+    # ---- steady state: the same staged loop again, long after the GPU left idle ---------------------
+    st_el, st_ms, st_n = timed_steps(ix, args.k, args.steady_steps, 0, dist, cuda_sync, 10)
+    st_el = max_over_ranks(dist, st_el)
+
     # ---- roofline of the fused kernel (rank 0's shard) ---------------------------------------------
     n_local = se - sb
     alg_bytes = algorithmic_bytes(n_local, args.dim, args.batch, args.dtype, args.metric)
     avg_kernel_s = (kern_ms / max(launches, 1)) / 1e3
     achieved = alg_bytes / avg_kernel_s / 1e9 if launches else None
+    step_s = elapsed / args.steps
+    consistent = bool(launches) and avg_kernel_s <= step_s * 1.001
     if args.pmc_child:            # only the fused-kernel launches matter to the parent's PMC parse
         ix.close()
         return
@@ -197,8 +291,7 @@ def main() -> None:
             vx = Index(devices=[local], dtype=vd, metric=args.metric)
             vx.fill_synthetic(_lib.RR_SYNTH_UNIT_NORM, 1234, args.docs, args.dim)
             vx.set_queries(q)
-            v_el, v_ms, v_n = timed_steps(vx, args.k, args.variant_steps, args.warmup, dist, cuda_sync,
-                                          args.timing_every)
+            v_el, v_ms, v_n = timed_steps(vx, args.k, args.variant_steps, args.warmup, dist, cuda_sync, 10)
             _, v_idx = vx.search(q, args.k)
             vx.close()
             v_kern = v_ms / max(v_n, 1) / 1e3
@@ -216,8 +309,7 @@ def main() -> None:
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:   # rank 0 at N=1 only
-            threads = min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(args.docs, args.dim, args.batch, args.k, args.cpu_batches, threads)
+            cpu = cpu_baseline(args.docs, args.dim, args.batch, args.k, args.cpu_budget)
         value = args.batch * args.steps / elapsed
         out = {
             "metric": "retrieval queries/sec + p99 latency, batch=32, 1M docs d=1024, 1/2/4/8 GPU",
@@ -239,6 +331,21 @@ def main() -> None:
             "p50_ms": round(p50, 4),
             "p99_ms": round(p99, 4),
             "latency_note": "host-inclusive per batch: H2D queries + pipeline + D2H results, synchronous",
+            "host_pipelined": {"value": round(args.batch * args.latency_steps / host_pipe_s, 2), "unit": "queries/s",
+                               "batches": args.latency_steps, "in_flight": 2,
+                               "note": "host numpy queries in, host results out: rr_search_async (pinned H2D + "
+                                       "search + D2H enqueued) / rr_wait, two batches in flight"},
+            "steady_state": {"value": round(args.batch * args.steady_steps / st_el, 2), "unit": "queries/s",
+                             "steps": args.steady_steps,
+                             "ms_per_step": round(st_el / args.steady_steps * 1e3, 4),
+                             "kernel_avg_us": round(st_ms / max(st_n, 1) * 1e3, 2),
+                             "frac": round(alg_bytes / (st_ms / max(st_n, 1) / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+                             if st_n else None,
+                             "note": "the same staged loop after the latency loops (GPU long out of idle); "
+                                     "value above is the first K steps after W warm-up steps from idle"},
+            "exchange": ("rccl ncclAllGather of per-shard top-k keys, device merge on every rank"
+                         if world > 1 else "none (one shard)"),
+            "rccl_ranks": rccl_ranks,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
@@ -247,9 +354,9 @@ def main() -> None:
                          "mfma": mfma,
                          "kernel": SCORE_KERNEL_DOC,
                          "kernel_avg_us": round(avg_kernel_s * 1e6, 2),
-                         "kernel_timing": f"HIP events on the kernel's stream around every {args.timing_every}-th "
-                                          f"similarity-kernel launch of the timed region ({launches} launches; "
-                                          f"event markers on every step cost ~5 us per step)",
+                         "kernel_timing": f"HIP events on the kernel's stream around every {every}-th "
+                                          f"similarity-kernel launch of the timed region ({launches} launches)",
+                         "kernel_le_step": consistent,
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "other_dtypes": variants or None,

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 1
+#define RR_ABI_VERSION 2
 
 /* error codes */
 #define RR_OK             0
@@ -101,8 +101,12 @@ int rr_abi_version(void);
 int rr_get_unique_id(char* out);
 
 /* Join a world of `world` processes as `rank`; this process's single local device holds global
- * shard `rank`. Must precede rr_load / rr_load_shard / rr_fill_synthetic. */
+ * shard `rank`. Must precede rr_load / rr_load_rows / rr_fill_synthetic. Creates the RCCL communicator
+ * for every world size (1 included); every search then exchanges its candidates with ncclAllGather. */
 int rr_init_dist(rr_handle* h, int world, int rank, const char* unique_id);
+
+/* Ranks in the handle's RCCL communicator and this process's rank in it (0 and -1 without one). */
+int rr_dist_info(const rr_handle* h, int* rccl_ranks, int* rccl_rank);
 
 /* ---- corpus ------------------------------------------------------------------------------------ */
 
@@ -151,6 +155,18 @@ int rr_set_queries(rr_handle* h, const float* host_q, int32_t b, int32_t d);
 int rr_search_staged(rr_handle* h, int32_t k);
 int rr_synchronize(rr_handle* h);
 int rr_fetch_results(rr_handle* h, float* out_scores, int64_t* out_idx);
+
+/* Shape of the results rr_fetch_results writes: the batch and k of the last search (0, 0 before any
+ * search or after a reload). out_scores / out_idx must hold b*k elements. */
+int rr_last_shape(const rr_handle* h, int32_t* b, int32_t* k);
+
+/* Pipelined form of rr_search for serving loops: stage the queries through a pinned buffer, enqueue
+ * the H2D copy, the search and the D2H copy of its results, and return at once with a ticket. Up to 4
+ * searches may be in flight; rr_wait(ticket) blocks until that search's results are on the host and
+ * copies them (b*k scores and indices, sorted as rr_search's) into the caller's buffers. Tickets are
+ * waited in any order, each exactly once. */
+int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int32_t k, int32_t* ticket);
+int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx);
 
 /* Queries already on local device 0 (e.g. a torch tensor from the embedding model): device-to-device
  * copy into every local shard's query buffer (skips the reference's .cpu().numpy() round trip,

@@ -11,6 +11,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -75,9 +76,7 @@ struct Shard {
   float* out_scores = nullptr;           // [q_cap][k_cap]
   int64_t* out_idx = nullptr;            // [q_cap][k_cap]
   size_t out_off = 0;
-  float* pin_q = nullptr;                // pinned host staging of the queries (rr_set_queries)
-  size_t pin_q_cap = 0;
-  hipEvent_t pin_q_free = nullptr;       // the last H2D out of pin_q has completed
+  hipEvent_t pin_q_free = nullptr;       // the last H2D out of the handle's pinned query staging completed
   int k_cap = 0;
   // k > RR_FUSED_KMAX path
   uint64_t* full_keys = nullptr;         // [32][max(rows, world*k)]
@@ -96,6 +95,17 @@ struct Shard {
 
 }  // namespace
 
+// One in-flight rr_search_async batch: a pinned buffer that carries its queries to the device and,
+// stream-ordered after the search, its results back.
+struct AsyncSlot {
+  char* pin = nullptr;
+  size_t cap = 0;
+  hipEvent_t done = nullptr;   // results landed in pin
+  int32_t b = 0, k = 0, ticket = -1;
+  bool pending = false;
+};
+constexpr int kAsyncSlots = 4;
+
 struct rr_handle {
   int dtype = RR_DTYPE_F32;
   int metric = RR_METRIC_COSINE;
@@ -108,14 +118,20 @@ struct rr_handle {
   std::vector<Shard> shards;
   int32_t cur_b = 0;    // last staged batch
   int32_t last_k = 0;   // k of the last search
+  int32_t last_b = 0;   // batch of the last search (the shape rr_fetch_results writes)
   bool timing = false;
   int kernel = RR_KERNEL_AUTO;   // rr_set_kernel
   int parity = 0;                // pipelined exchange: buffer set of the next search block
   double t_ms = 0.0;
   int64_t t_count = 0;
-  // pinned host staging for the synchronous search path (rr_set_queries / rr_fetch_results)
+  // pinned host staging for the synchronous search path (rr_set_queries / rr_fetch_results): the queries
+  // are copied into pin_q ONCE per batch and every local shard DMAs them from there
   char* pin_out = nullptr;
   size_t pin_out_cap = 0;
+  float* pin_q = nullptr;
+  size_t pin_q_cap = 0;
+  AsyncSlot aslots[kAsyncSlots];
+  int32_t next_ticket = 0;
 };
 
 namespace {
@@ -161,7 +177,6 @@ int free_shard(Shard& s) {
   for (hipEvent_t e : s.ev) hipEventDestroy(e);
   s.ev.clear();
   if (s.keys_ready) hipEventDestroy(s.keys_ready);
-  if (s.pin_q) hipHostFree(s.pin_q);
   if (s.pin_q_free) hipEventDestroy(s.pin_q_free);
   if (s.copies_done) hipEventDestroy(s.copies_done);
   for (hipEvent_t e : {s.ev_keys[0], s.ev_keys[1], s.ev_xdone[0], s.ev_xdone[1], s.ev_cdone})
@@ -281,8 +296,38 @@ int check_shape(const rr_handle* h, int64_t n, int32_t d) {
   return RR_OK;
 }
 
+// Work buffers are sized for (q_cap, d, k_cap, rows): a reload (possibly with another d or shard size)
+// drops them, and the staged batch / last result shape with them.
+int drop_work_buffers(rr_handle* h) {
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    HIP_TRY(hipStreamSynchronize(s.stream));
+    HIP_TRY(hipStreamSynchronize(s.xstream));
+    void** ptrs[] = {(void**)&s.queries, (void**)&s.cand, (void**)&s.shard_keys, (void**)&s.gathered,
+                     (void**)&s.out_base, (void**)&s.full_keys, (void**)&s.sorted, &s.sort_temp,
+                     (void**)&s.px_keys[0], (void**)&s.px_keys[1], (void**)&s.px_gathered[0],
+                     (void**)&s.px_gathered[1]};
+    for (void** p : ptrs) {
+      if (*p) HIP_TRY(hipFree(*p));
+      *p = nullptr;
+    }
+    s.q_cap = s.k_cap = s.cand_grid = 0;
+    s.full_cap = s.sort_temp_bytes = 0;
+    s.out_scores = nullptr;
+    s.out_idx = nullptr;
+    s.out_off = 0;
+  }
+  h->cur_b = 0;
+  h->last_k = 0;
+  h->last_b = 0;
+  h->parity = 0;
+  h->loaded = false;
+  return RR_OK;
+}
+
 int prepare_ranges(rr_handle* h, int64_t n, int32_t d) {
   if (int rc = check_shape(h, n, d)) return rc;
+  if (int rc = drop_work_buffers(h)) return rc;
   h->n_total = n;
   h->d = d;
   for (size_t i = 0; i < h->shards.size(); ++i) {
@@ -318,13 +363,17 @@ int ensure_buffers(rr_handle* h, int b, int k) {
       s.cand_grid = s.cus;
       if (int rc = dmalloc(&s.cand, (size_t)s.cand_grid * kMaxSlots * RR_FUSED_KMAX * 8)) return rc;
     }
-    if (h->world > 1 && !s.px_keys[0]) {
+    if ((h->world > 1 || h->dist) && !s.px_keys[0]) {
       for (int p = 0; p < 2; ++p) {
         if (int rc = dmalloc(&s.px_keys[p], (size_t)kMaxSlots * RR_FUSED_KMAX * 8)) return rc;
         if (int rc = dmalloc(&s.px_gathered[p], (size_t)h->world * kMaxSlots * RR_FUSED_KMAX * 8)) return rc;
       }
     }
     if (k > RR_FUSED_KMAX) {
+      // hipcub's segmented sort takes an int item count
+      if ((int64_t)rr::kQSlots * std::max<int64_t>(s.rows(), (int64_t)h->world * k) > INT32_MAX)
+        return fail(RR_E_UNSUPPORTED, "k=%d > %d on a shard of %lld rows exceeds the full-sort path's size limit", k,
+                    RR_FUSED_KMAX, (long long)s.rows());
       const size_t need = (size_t)rr::kQSlots * std::max<int64_t>(s.rows(), (int64_t)h->world * k);
       if (need > s.full_cap) {
         if (int rc = dmalloc(&s.full_keys, need * 8)) return rc;
@@ -453,7 +502,7 @@ int block_slots(const rr_handle* h, int b, int k) {
 int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
   const int d = h->d;
   const int kt = rr::fused_kt(k);
-  const bool multi = h->world > 1;
+  const bool multi = h->world > 1 || h->dist;   // an exchange step (RCCL with any world, peer copies)
   const bool local_multi = multi && !h->dist;
   const int p = h->parity;
   for (size_t si = 0; si < h->shards.size(); ++si) {
@@ -627,6 +676,11 @@ void rr_destroy(rr_handle* h) {
   if (!h) return;
   for (Shard& s : h->shards) free_shard(s);
   if (h->pin_out) hipHostFree(h->pin_out);
+  if (h->pin_q) hipHostFree(h->pin_q);
+  for (AsyncSlot& a : h->aslots) {
+    if (a.pin) hipHostFree(a.pin);
+    if (a.done) hipEventDestroy(a.done);
+  }
 
   delete h;
 }
@@ -644,16 +698,30 @@ int rr_init_dist(rr_handle* h, int world, int rank, const char* unique_id) {
   if (h->shards.size() != 1) return fail(RR_E_UNSUPPORTED, "multi-process mode needs exactly one local device");
   if (h->loaded) return fail(RR_E_STATE, "rr_init_dist must precede loading the corpus");
   if (world < 1 || rank < 0 || rank >= world) return fail(RR_E_INVALID, "bad world/rank %d/%d", world, rank);
+  if (h->shards[0].comm) return fail(RR_E_STATE, "rr_init_dist already called on this handle");
+  // A communicator is created for every world size, 1 included: the search then always takes the RCCL
+  // all-gather exchange (with one rank RCCL copies the rank's own candidates), so a 1-GPU box runs the
+  // same data path as a node.
+  Shard& s = h->shards[0];
+  HIP_TRY(hipSetDevice(s.dev));
+  ncclUniqueId id;
+  memcpy(id.internal, unique_id, RR_UNIQUE_ID_BYTES);
+  NCCL_TRY(ncclCommInitRank(&s.comm, world, id, rank));
   h->world = world;
   h->shard_base = rank;
   h->dist = true;
-  if (world > 1) {
-    Shard& s = h->shards[0];
-    HIP_TRY(hipSetDevice(s.dev));
-    ncclUniqueId id;
-    memcpy(id.internal, unique_id, RR_UNIQUE_ID_BYTES);
-    NCCL_TRY(ncclCommInitRank(&s.comm, world, id, rank));
+  return RR_OK;
+}
+
+int rr_dist_info(const rr_handle* h, int* rccl_ranks, int* rccl_rank) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  int n = 0, r = -1;
+  if (h->dist && h->shards[0].comm) {
+    NCCL_TRY(ncclCommCount(h->shards[0].comm, &n));
+    NCCL_TRY(ncclCommUserRank(h->shards[0].comm, &r));
   }
+  if (rccl_ranks) *rccl_ranks = n;
+  if (rccl_rank) *rccl_rank = r;
   return RR_OK;
 }
 
@@ -774,19 +842,22 @@ int rr_set_queries(rr_handle* h, const float* host_q, int32_t b, int32_t d) {
   // stage through a pinned buffer per shard (the copy is then a plain async DMA); a buffer is rewritten
   // only after the previous batch's copy out of it has completed
   const size_t qbytes = (size_t)b * d * 4;
-  for (Shard& s : h->shards) {
+  for (Shard& s : h->shards) {   // every shard's copy out of pin_q has landed before it is rewritten
     HIP_TRY(hipSetDevice(s.dev));
     if (s.pin_q_free) HIP_TRY(hipEventSynchronize(s.pin_q_free));
     else HIP_TRY(hipEventCreateWithFlags(&s.pin_q_free, hipEventDisableTiming));
-    if (qbytes > s.pin_q_cap) {
-      if (s.pin_q) HIP_TRY(hipHostFree(s.pin_q));
-      s.pin_q = nullptr;
-      s.pin_q_cap = 0;
-      HIP_TRY(hipHostMalloc((void**)&s.pin_q, qbytes, hipHostMallocDefault));
-      s.pin_q_cap = qbytes;
-    }
-    memcpy(s.pin_q, host_q, qbytes);
-    HIP_TRY(hipMemcpyAsync(s.queries, s.pin_q, qbytes, hipMemcpyHostToDevice, s.stream));
+  }
+  if (qbytes > h->pin_q_cap) {
+    if (h->pin_q) HIP_TRY(hipHostFree(h->pin_q));
+    h->pin_q = nullptr;
+    h->pin_q_cap = 0;
+    HIP_TRY(hipHostMalloc((void**)&h->pin_q, qbytes, hipHostMallocDefault));
+    h->pin_q_cap = qbytes;
+  }
+  memcpy(h->pin_q, host_q, qbytes);
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    HIP_TRY(hipMemcpyAsync(s.queries, h->pin_q, qbytes, hipMemcpyHostToDevice, s.stream));
     HIP_TRY(hipEventRecord(s.pin_q_free, s.stream));
   }
   h->cur_b = b;
@@ -823,6 +894,14 @@ int rr_search_staged(rr_handle* h, int32_t k) {
     if (int rc = enqueue_block(h, q0, bb, k, slots)) return rc;
   }
   h->last_k = k;
+  h->last_b = b;
+  return RR_OK;
+}
+
+int rr_last_shape(const rr_handle* h, int32_t* b, int32_t* k) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  if (b) *b = h->last_b;
+  if (k) *k = h->last_k;
   return RR_OK;
 }
 
@@ -842,7 +921,7 @@ int rr_fetch_results(rr_handle* h, float* out_scores, int64_t* out_idx) {
   if (int rc = rr_synchronize(h)) return rc;
   Shard& s = h->shards[0];
   HIP_TRY(hipSetDevice(s.dev));
-  const size_t cnt = (size_t)h->cur_b * h->last_k;
+  const size_t cnt = (size_t)h->last_b * h->last_k;
   const size_t span = s.out_off + cnt * 8;
   if (s.out_off > (1u << 20)) {   // capacity grown far beyond this search: two plain copies
     HIP_TRY(hipMemcpy(out_scores, s.out_scores, cnt * 4, hipMemcpyDeviceToHost));
@@ -868,6 +947,63 @@ int rr_search(rr_handle* h, const float* host_q, int32_t b, int32_t d, int32_t k
   if (int rc = rr_set_queries(h, host_q, b, d)) return rc;
   if (int rc = rr_search_staged(h, k)) return rc;
   return rr_fetch_results(h, out_scores, out_idx);
+}
+
+int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int32_t k, int32_t* ticket) {
+  if (!h || !host_q || !ticket) return fail(RR_E_INVALID, "null argument");
+  if (!h->loaded) return fail(RR_E_STATE, "no corpus loaded");
+  if (d != h->d) return fail(RR_E_INVALID, "query dim %d != corpus dim %d", d, h->d);
+  if (b < 1 || k < 1) return fail(RR_E_INVALID, "b=%d k=%d", b, k);
+  const int32_t t = h->next_ticket;
+  AsyncSlot& a = h->aslots[t % kAsyncSlots];
+  if (a.pending) return fail(RR_E_STATE, "%d searches in flight: rr_wait(%d) first", kAsyncSlots, a.ticket);
+  if (int rc = ensure_buffers(h, b, k)) return rc;
+  const size_t qbytes = (size_t)b * d * 4, cnt = (size_t)b * k;
+  const size_t idx_off = (cnt * 4 + 255) & ~(size_t)255;
+  const size_t need = std::max(qbytes, idx_off + cnt * 8);
+  if (need > a.cap) {
+    if (a.pin) HIP_TRY(hipHostFree(a.pin));
+    a.pin = nullptr;
+    a.cap = 0;
+    HIP_TRY(hipHostMalloc((void**)&a.pin, need, hipHostMallocDefault));
+    a.cap = need;
+  }
+  if (!a.done) HIP_TRY(hipEventCreateWithFlags(&a.done, hipEventDisableTiming));
+  memcpy(a.pin, host_q, qbytes);
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    HIP_TRY(hipMemcpyAsync(s.queries, a.pin, qbytes, hipMemcpyHostToDevice, s.stream));
+  }
+  h->cur_b = b;
+  if (int rc = rr_search_staged(h, k)) return rc;
+  // results come back on the stream that wrote them last: the exchange stream when there is an exchange
+  // (the serial k > 32 exchange also orders it after itself), else the compute stream
+  Shard& s0 = h->shards[0];
+  HIP_TRY(hipSetDevice(s0.dev));
+  hipStream_t rs = (h->world > 1 || h->dist) ? s0.xstream : s0.stream;
+  HIP_TRY(hipMemcpyAsync(a.pin, s0.out_scores, cnt * 4, hipMemcpyDeviceToHost, rs));
+  HIP_TRY(hipMemcpyAsync(a.pin + idx_off, s0.out_idx, cnt * 8, hipMemcpyDeviceToHost, rs));
+  HIP_TRY(hipEventRecord(a.done, rs));
+  a.b = b;
+  a.k = k;
+  a.ticket = t;
+  a.pending = true;
+  h->next_ticket = t + 1 < 0x40000000 ? t + 1 : 0;
+  *ticket = t;
+  return RR_OK;
+}
+
+int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx) {
+  if (!h || !out_scores || !out_idx) return fail(RR_E_INVALID, "null argument");
+  if (ticket < 0) return fail(RR_E_INVALID, "bad ticket %d", ticket);
+  AsyncSlot& a = h->aslots[ticket % kAsyncSlots];
+  if (!a.pending || a.ticket != ticket) return fail(RR_E_STATE, "ticket %d is not in flight", ticket);
+  HIP_TRY(hipEventSynchronize(a.done));
+  const size_t cnt = (size_t)a.b * a.k;
+  memcpy(out_scores, a.pin, cnt * 4);
+  memcpy(out_idx, a.pin + ((cnt * 4 + 255) & ~(size_t)255), cnt * 8);
+  a.pending = false;
+  return collect_timing(h);
 }
 
 int rr_set_kernel(rr_handle* h, int kernel) {

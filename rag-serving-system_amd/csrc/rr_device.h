@@ -42,6 +42,13 @@ __device__ __forceinline__ uint64_t make_key(float s, uint32_t gidx) {
 }
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
 
+// Cosine denominator |q|*|d| + 1e-8 with the product rounded BEFORE the add, as the reference computes it
+// (norm_X @ norm_Y.T, then + 1e-8 elementwise; retriever.py:605-607): no FMA contraction here.
+__device__ __forceinline__ float cos_den(float qn, float nd) {
+#pragma clang fp contract(off)
+  return qn * nd + 1e-8f;
+}
+
 // Per-lane sorted (descending) list of the KT best keys, fully in registers (static indexing only).
 template <int KT>
 struct TopK {

@@ -347,7 +347,7 @@ __global__ __launch_bounds__(kThreads) void fused_score_kernel(
         if constexpr (COS) {
           // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
           const float nd = DT == 2 ? wseg[2 * (doc - seg_lo)] : wseg[doc - seg_lo];
-          const float den = qn * nd + 1e-8f;
+          const float den = cos_den(qn, nd);
           if constexpr (MODE == 0) {
             if (valid && s * __builtin_amdgcn_rcpf(den) >= thr) {
               float c = s / den;   // IEEE division, as the reference's elementwise kernel

@@ -123,6 +123,26 @@ __device__ __forceinline__ void split3(const float (&x)[8], bf16x8& b0, bf16x8& 
   b2 = __builtin_bit_cast(bf16x8, p2);
 }
 
+// x = b0 + b1 + r with |r| <= 2^-16 |x| (the first two splits of split3; r dropped). 6 VALU per pair.
+__device__ __forceinline__ void split2(const float (&x)[8], bf16x8& b0, bf16x8& b1) {
+  u32x4 p0, p1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = x[2 * i], b = x[2 * i + 1];
+    p0[i] = cvt_pk_bf16(a, b);
+    const float ra = a - __uint_as_float(p0[i] << 16), rb = b - __uint_as_float(p0[i] & 0xFFFF0000u);
+    p1[i] = cvt_pk_bf16(ra, rb);
+  }
+  b0 = __builtin_bit_cast(bf16x8, p0);
+  b1 = __builtin_bit_cast(bf16x8, p1);
+}
+__device__ __forceinline__ bf16x8 split1(const float (&x)[8]) {
+  u32x4 p0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) p0[i] = cvt_pk_bf16(x[2 * i], x[2 * i + 1]);
+  return __builtin_bit_cast(bf16x8, p0);
+}
+
 // All-ones / all-zeros lane mask the compiler cannot see through, and x AND-ed with it: the loads that
 // feed it are then issued unconditionally (a select on the predicate gets turned into exec-masked branches
 // around each load, which serialises their latencies). Exact zeros, whatever x holds.
@@ -148,6 +168,10 @@ template <int NS>
 struct QFrag<2, NS> { f16x8 hi[NS][2], lo[NS][2]; };          // 2 K-steps of 16 per slab
 template <int NS>
 struct QFrag<3, NS> { bf16x8 c0[NS][2], c1[NS][2], c2[NS][2]; };
+template <int NS>
+struct QFrag<4, NS> { bf16x8 c0[NS][2], c1[NS][2]; };
+template <int NS>
+struct QFrag<5, NS> { bf16x8 c0[NS][2], c1[NS][2]; };
 
 
 // LDS byte offset (within a slot) of 16-byte column position cp of tile row r (swizzled image)
@@ -270,7 +294,8 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
 #pragma unroll
               for (int e = 0; e < 4; ++e) x[4 * u + e] = v[e];
             }
-            split3(x, qf.c0[j][t], qf.c1[j][t], qf.c2[j][t]);
+            if constexpr (DT == 3) split3(x, qf.c0[j][t], qf.c1[j][t], qf.c2[j][t]);
+            else split2(x, qf.c0[j][t], qf.c1[j][t]);
           }
         }
       }
@@ -401,6 +426,17 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
         for (int t = 0; t < 2; ++t) {
           const float x[8] = {a[2 * t].x, a[2 * t].y, a[2 * t].z, a[2 * t].w,
                               a[2 * t + 1].x, a[2 * t + 1].y, a[2 * t + 1].z, a[2 * t + 1].w};
+          if constexpr (DT == 4) {
+            bf16x8 b0, b1;
+            split2(x, b0, b1);
+            for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
+            for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c1[j][t], accs[qh], 0, 0, 0);
+            for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
+          } else if constexpr (DT == 5) {
+            const bf16x8 b0 = split1(x);
+            for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
+            for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c1[j][t], accs[qh], 0, 0, 0);
+          } else {
           bf16x8 b0, b1, b2;
           split3(x, b0, b1, b2);
           for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
@@ -409,6 +445,7 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
           for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qfs[qh].c1[j][t], accs[qh], 0, 0, 0);
           for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c2[j][t], accs[qh], 0, 0, 0);
           for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
+          }
         }
       }
       slot = slot + 1 == RS ? 0 : slot + 1;
@@ -484,7 +521,7 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
       if constexpr (COS) {
         // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
         const float nd = DT == 2 ? seg[2 * li] : seg[li];
-        const float den = qn * nd + 1e-8f;
+        const float den = cos_den(qn, nd);
         if (valid && s * __builtin_amdgcn_rcpf(den) >= thr) {
           float c = s / den;   // IEEE division, as the reference's elementwise kernel
           c = fminf(fmaxf(c, -1.0f), 1.0f);
@@ -600,6 +637,10 @@ hipError_t launch_sk(int sdt, int metric, int kt, int grid, const void* c, const
       case 1: return sk::launch_metric<1, 2, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
       case 2: return sk::launch_metric<2, 2, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
       case 3: return sk::launch_metric<3, 2, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+#ifdef RR_SK_SCREEN_PROBE
+      case 4: return sk::launch_metric<4, 2, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      case 5: return sk::launch_metric<5, 2, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+#endif
       default: return hipErrorInvalidValue;
     }
   }

@@ -38,7 +38,7 @@ RR_UNIQUE_ID_BYTES = 128
 RR_FUSED_KMAX = 32
 RR_KERNEL_AUTO = 0
 RR_KERNEL_FUSED = 1
-RR_ABI_VERSION = 1
+RR_ABI_VERSION = 2
 
 DTYPES = {"fp32": RR_DTYPE_F32, "float32": RR_DTYPE_F32, "f32": RR_DTYPE_F32,
           "bf16": RR_DTYPE_BF16, "bfloat16": RR_DTYPE_BF16, "fp32-split": RR_DTYPE_F32_SPLIT}
@@ -69,6 +69,10 @@ SIGNATURES = {
     "rr_set_kernel": (_c_int, [_vp, _c_int]),
     "rr_set_timing": (_c_int, [_vp, _c_int]),
     "rr_kernel_time": (_c_int, [_vp, ctypes.POINTER(ctypes.c_double), _i64p, _c_int]),
+    "rr_search_async": (_c_int, [_vp, _fp, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_i32)]),
+    "rr_wait": (_c_int, [_vp, _c_i32, _fp, _i64p]),
+    "rr_last_shape": (_c_int, [_vp, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32)]),
+    "rr_dist_info": (_c_int, [_vp, _ip, _ip]),
 }
 
 
@@ -170,6 +174,7 @@ class Index:
         self._h = h
         self.n = 0
         self.d = 0
+        self._tickets = {}
 
     # -- lifecycle ---------------------------------------------------------------------------------
     def close(self) -> None:
@@ -185,6 +190,12 @@ class Index:
 
     def init_dist(self, world: int, rank: int, unique_id: bytes) -> None:
         _check(self._lib.rr_init_dist(self._h, world, rank, unique_id))
+
+    def dist_info(self) -> Tuple[int, int]:
+        """(ranks in the RCCL communicator, this process's rank): (0, -1) without one."""
+        n, r = ctypes.c_int(), ctypes.c_int()
+        _check(self._lib.rr_dist_info(self._h, ctypes.byref(n), ctypes.byref(r)))
+        return n.value, r.value
 
     # -- corpus ------------------------------------------------------------------------------------
     def load(self, corpus: np.ndarray) -> None:
@@ -229,24 +240,49 @@ class Index:
         _check(self._lib.rr_search(self._h, _fptr(q), b, q.shape[1], k, _fptr(scores), _i64ptr(idx)))
         return scores, idx
 
+    def search_async(self, queries: np.ndarray, k: int) -> int:
+        """Enqueue H2D + search + D2H of one batch; returns a ticket for wait() (at most 4 in flight)."""
+        q = np.ascontiguousarray(queries, dtype=np.float32)
+        if q.ndim != 2:
+            raise ValueError("queries must be 2-D")
+        t = _c_i32()
+        _check(self._lib.rr_search_async(self._h, _fptr(q), q.shape[0], q.shape[1], k, ctypes.byref(t)))
+        self._tickets[t.value] = (q.shape[0], k)
+        return t.value
+
+    def wait(self, ticket: int) -> Tuple[np.ndarray, np.ndarray]:
+        b, k = self._tickets.pop(ticket)
+        scores = np.empty((b, k), dtype=np.float32)
+        idx = np.empty((b, k), dtype=np.int64)
+        _check(self._lib.rr_wait(self._h, ticket, _fptr(scores), _i64ptr(idx)))
+        return scores, idx
+
     def set_queries(self, queries: np.ndarray) -> None:
         q = np.ascontiguousarray(queries, dtype=np.float32)
+        if q.ndim != 2:
+            raise ValueError("queries must be 2-D")
         _check(self._lib.rr_set_queries(self._h, _fptr(q), q.shape[0], q.shape[1]))
-        self._staged_b = q.shape[0]
 
     def set_queries_device(self, dev_ptr: int, b: int, d: int) -> None:
         _check(self._lib.rr_set_queries_device(self._h, _vp(dev_ptr), b, d))
-        self._staged_b = b
 
     def search_staged(self, k: int) -> None:
         _check(self._lib.rr_search_staged(self._h, k))
-        self._staged_k = k
 
     def synchronize(self) -> None:
         _check(self._lib.rr_synchronize(self._h))
 
+    def last_shape(self) -> Tuple[int, int]:
+        """(batch, k) of the last search: the shape fetch() returns."""
+        b, k = _c_i32(), _c_i32()
+        _check(self._lib.rr_last_shape(self._h, ctypes.byref(b), ctypes.byref(k)))
+        return b.value, k.value
+
     def fetch(self) -> Tuple[np.ndarray, np.ndarray]:
-        b, k = self._staged_b, self._staged_k
+        """Results of the LAST search (staged or synchronous), sized from the C side's own record."""
+        b, k = self.last_shape()
+        if b < 1 or k < 1:
+            raise HipRetrievalError(RR_E_STATE, "no search has run")
         scores = np.empty((b, k), dtype=np.float32)
         idx = np.empty((b, k), dtype=np.int64)
         _check(self._lib.rr_fetch_results(self._h, _fptr(scores), _i64ptr(idx)))

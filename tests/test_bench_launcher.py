@@ -1,0 +1,24 @@
+"""bench.py as the driver invokes it: `python bench.py --gpus N ...` without torchrun launches one rank per
+GPU itself (CPU dry run: gloo control plane only, no GPU call)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_plain_launch_reaches_timed_loop(n):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--steps", "20",
+                          "--warmup", "5", "--dry-run"], capture_output=True, text=True, timeout=240, env=env,
+                         cwd=REPO)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["dry_run"] and rec["n_gpus"] == n and rec["ranks_seen"] == n
+    assert rec["launched_by"] == ("torch.distributed.run" if n > 1 else "plain")

@@ -1,0 +1,108 @@
+"""C-ABI behaviour beyond the kernels: the RCCL exchange with a 1-rank communicator, reloads, result shapes,
+the pipelined async search."""
+import numpy as np
+import pytest
+
+from oracle.retriever_oracle import canonical_topk, exact_scores
+from parity_helpers import check_topk
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib(hip):
+    import rag_service_amd
+    return rag_service_amd
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_rccl_one_rank_exchange_matches_single_shard(lib, dtype):
+    """rr_init_dist(world=1) creates a real RCCL communicator, so every search takes the all-gather exchange:
+    the pipelined branch (k <= 32, exchange stream, parity buffers) and the serial one (k > 32). Results must be
+    bit-identical to the handle without an exchange, over back-to-back staged searches and mixed k."""
+    rng = np.random.default_rng(3)
+    corpus = rng.standard_normal((7001, 1024)).astype(np.float32)
+    q = rng.standard_normal((45, 1024)).astype(np.float32)     # two query blocks
+    plain = lib.Index(devices=[0], dtype=dtype, metric="cosine")
+    plain.load(corpus)
+    rc = lib.Index(devices=[0], dtype=dtype, metric="cosine")
+    rc.init_dist(1, 0, lib.get_unique_id())
+    assert rc.dist_info() == (1, 0)
+    assert plain.dist_info() == (0, -1)
+    rc.load(corpus)
+    for k in (5, 40, 8, 32, 33, 1):
+        want = plain.search(q, k)
+        got = rc.search(q, k)
+        assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), k
+    rc.set_queries(q)
+    for k in (5, 40, 5, 5):
+        for _ in range(3):
+            rc.search_staged(k)
+        s, i = rc.fetch()
+        want = plain.search(q, k)
+        assert np.array_equal(i, want[1]) and np.array_equal(s, want[0]), k
+    plain.close()
+    rc.close()
+
+
+def test_reload_with_other_dim_and_size(lib):
+    """A handle reloaded with a different d / row count drops its work buffers (they were sized for the old
+    corpus): searches after the reload are correct, and the staged batch does not survive the reload."""
+    rng = np.random.default_rng(4)
+    ix = lib.Index(dtype="fp32", metric="cosine")
+    c1 = rng.standard_normal((300, 64)).astype(np.float32)
+    q1 = rng.standard_normal((70, 64)).astype(np.float32)
+    ix.load(c1)
+    ix.search(q1, 5)
+    c2 = rng.standard_normal((5000, 1024)).astype(np.float32)
+    q2 = rng.standard_normal((40, 1024)).astype(np.float32)
+    ix.load(c2)
+    with pytest.raises(lib.HipRetrievalError):
+        ix.search_staged(5)                         # the 64-d batch staged before the reload is gone
+    s, i = ix.search(q2, 7)
+    _, cidx = canonical_topk(exact_scores(c2, q2, "cosine"), 7)
+    check_topk(i, s, cidx, c2, q2, "cosine", near_tie=1e-5 * 32, score_tol=1e-3)
+    ix.load(c1)                                     # and back to the small one
+    s, i = ix.search(q1, 3)
+    _, cidx = canonical_topk(exact_scores(c1, q1, "cosine"), 3)
+    check_topk(i, s, cidx, c1, q1, "cosine", near_tie=1e-5 * 8, score_tol=1e-3)
+    ix.close()
+
+
+def test_fetch_returns_the_last_search_shape(lib):
+    rng = np.random.default_rng(5)
+    corpus = rng.standard_normal((2000, 256)).astype(np.float32)
+    ix = lib.Index(dtype="fp32", metric="dot")
+    ix.load(corpus)
+    ix.set_queries(corpus[:1])
+    ix.search_staged(1)
+    assert ix.last_shape() == (1, 1)
+    q = rng.standard_normal((64, 256)).astype(np.float32)
+    s, i = ix.search(q, 100)                        # synchronous search after a staged one
+    assert ix.last_shape() == (64, 100)
+    s2, i2 = ix.fetch()
+    assert s2.shape == (64, 100) and np.array_equal(i2, i) and np.array_equal(s2, s)
+    ix.close()
+
+
+@pytest.mark.parametrize("shards", [1, 3])
+def test_async_pipeline_matches_sync(lib, shards):
+    rng = np.random.default_rng(6)
+    corpus = rng.standard_normal((9000, 512)).astype(np.float32)
+    ix = lib.Index(devices=[0] * shards, dtype="fp32", metric="cosine")
+    ix.load(corpus)
+    batches = [(rng.standard_normal((b, 512)).astype(np.float32), k)
+               for b, k in [(32, 5), (7, 40), (64, 10), (1, 1), (33, 32), (32, 5)]]
+    want = [ix.search(q, k) for q, k in batches]
+    tickets = [ix.search_async(q, k) for q, k in batches[:4]]
+    with pytest.raises(lib.HipRetrievalError):
+        ix.search_async(*batches[4])                # four already in flight
+    got = [ix.wait(t) for t in tickets[:2]]
+    tickets += [ix.search_async(q, k) for q, k in batches[4:]]
+    got += [ix.wait(t) for t in tickets[2:]]
+    for (ws, wi), (gs, gi) in zip(want, got):
+        assert np.array_equal(wi, gi) and np.array_equal(ws, gs)
+    with pytest.raises(lib.HipRetrievalError):     # a ticket is waited exactly once
+        lib._lib._check(ix._lib.rr_wait(ix._h, tickets[0], gs.ctypes.data_as(lib._lib._fp),
+                                        gi.ctypes.data_as(lib._lib._i64p)))
+    ix.close()

@@ -5,6 +5,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I rag-serving-system_amd/csrc \
 //         tools/kbench.hip -o tools/kbench && tools/kbench [n_docs] [rounds]
 #define RR_SK_RING3 1
+#define RR_SK_SCREEN_PROBE 1
 #include "../rag-serving-system_amd/csrc/rr_kernels.hip"
 #include "../rag-serving-system_amd/csrc/rr_sk.hip"
 
@@ -15,6 +16,7 @@
 #include <functional>
 #include <string>
 #include <vector>
+#include <unistd.h>
 
 #define CK(x)                                                                       \
   do {                                                                              \
@@ -360,6 +362,37 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(stream_lin, dim3(grid * 4), dim3(512), 0, s, (const u32x4*)c, n * d / 4, sink);
         return hipGetLastError(); }, {}},
   };
+  if (argc > 3 && strcmp(argv[3], "transient") == 0) {
+    // Per-launch durations from an idle GPU: each variant after `idle` seconds without work, `count`
+    // launches timed one by one (HIP events), so the clock/power transient shows per kernel form.
+    const int count = argc > 4 ? atoi(argv[4]) : 40;
+    const int idle_ms = argc > 5 ? atoi(argv[5]) : 3000;
+    CK(hipFuncSetAttribute((const void*)stream_sk<3, 1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 3 * 4096));
+    std::vector<Variant> tv = {VK(3, 0, 1, 2), VK(4, 0, 1, 2), VK(5, 0, 1, 2), VK(2, 2, 1, 2), streams[9],
+                               VK(4, 0, 1, 2), VK(3, 0, 1, 2)};
+    std::vector<hipEvent_t> ev(2 * count);
+    for (auto& e : ev) CK(hipEventCreate(&e));
+    for (auto& v : tv) {
+      const void* c = v.dtype == 1 ? (const void*)c16 : v.dtype == 2 ? (const void*)csplit : (const void*)c32;
+      CK(hipStreamSynchronize(s));
+      usleep(idle_ms * 1000);
+      for (int i = 0; i < count; ++i) {
+        CK(hipEventRecord(ev[2 * i], s));
+        CK(v.run(c, cand));
+        CK(hipEventRecord(ev[2 * i + 1], s));
+      }
+      CK(hipStreamSynchronize(s));
+      printf("{\"transient\": \"%s\", \"us\": [", v.name.c_str());
+      for (int i = 0; i < count; ++i) {
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
+        printf("%s%.0f", i ? ", " : "", ms * 1e3);
+      }
+      printf("]}\n");
+      fflush(stdout);
+    }
+    return 0;
+  }
   CK(hipFuncSetAttribute((const void*)stream_glds<16, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 16 * 1024));
   CK(hipFuncSetAttribute((const void*)stream_sk<3, 1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 3 * 4096));
   CK(hipFuncSetAttribute((const void*)stream_sk<3, 1, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 3 * 4096));
