@@ -177,12 +177,22 @@ int rr_set_queries_device(rr_handle* h, const float* dev_q, int32_t b, int32_t d
 
 #define RR_KERNEL_AUTO  0   /* split-K LDS-DMA kernel where the shape allows it (d*elem/8 a multiple of
                                128 bytes, at most 512 bytes; 64 queries per corpus pass for bf16 /
-                               fp32-split at k <= 16), else the register-streaming kernel */
+                               fp32-split at k <= 16), else the register-streaming kernel. fp32 storage at
+                               k <= 29: the screened search (an f16 screening pass of upper bounds, exact
+                               rescoring of the candidates, an exact full pass when the bound cannot prove
+                               completeness) — results identical to RR_KERNEL_EXACT */
 #define RR_KERNEL_FUSED 1   /* always the register-streaming kernel (fp32: f32 MFMA) */
+#define RR_KERNEL_EXACT 2   /* split-K kernel, fp32 storage scored exactly in one pass (no screening) */
+#define RR_KERNEL_SCREEN_FALLBACK 3   /* test hook: screened search whose verify always reports the block
+                                         incomplete, so the exact fallback pass produces the results */
 
 /* Choose the similarity kernel for k <= RR_FUSED_KMAX searches on this handle. Results of the two kernels
  * differ only by fp32 summation order. */
 int rr_set_kernel(rr_handle* h, int kernel);
+
+/* Screened-search counters since the corpus was (re)loaded: search blocks screened (summed over local
+ * shards) and how many of them needed the exact fallback pass. Synchronises the handle's streams. */
+int rr_screen_stats(rr_handle* h, int64_t* blocks, int64_t* fallbacks);
 
 /* ---- timing (benchmarks) ----------------------------------------------------------------------- */
 

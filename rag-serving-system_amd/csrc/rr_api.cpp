@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -61,6 +62,7 @@ struct Shard {
   int q_cap = 0;
   uint64_t* cand = nullptr;              // [grid][32][32] fused per-workgroup candidates
   int cand_grid = 0;
+  int* scount = nullptr;                 // screened search: blocks this shard flagged for the exact pass
   uint64_t* shard_keys = nullptr;        // [32][k_cap] this shard's top-k (all-gather send buffer)
   uint64_t* gathered = nullptr;          // [world][32][k_cap] (all-gather receive buffer)
   // pipelined exchange (k <= RR_FUSED_KMAX, world > 1): the exchange of search i (all-gather + final
@@ -72,7 +74,7 @@ struct Shard {
   hipEvent_t ev_keys[2] = {nullptr, nullptr};   // compute stream: px_keys[p] written
   hipEvent_t ev_xdone[2] = {nullptr, nullptr};  // xstream: exchange of parity p finished (buffers free)
   hipEvent_t ev_cdone = nullptr;                // compute stream: a serial (k > KMAX) exchange finished
-  char* out_base = nullptr;              // one allocation: scores at 0, indices at out_off
+  char* out_base = nullptr;              // one allocation: flag word at 0, scores at kOutHead, indices at out_off
   float* out_scores = nullptr;           // [q_cap][k_cap]
   int64_t* out_idx = nullptr;            // [q_cap][k_cap]
   size_t out_off = 0;
@@ -103,6 +105,8 @@ struct AsyncSlot {
   hipEvent_t done = nullptr;   // results landed in pin
   int32_t b = 0, k = 0, ticket = -1;
   bool pending = false;
+  bool screened = false;   // the search ran screened blocks, the first with sequence number seq0
+  int seq0 = 0;
 };
 constexpr int kAsyncSlots = 4;
 
@@ -132,6 +136,13 @@ struct rr_handle {
   size_t pin_q_cap = 0;
   AsyncSlot aslots[kAsyncSlots];
   int32_t next_ticket = 0;
+  // screened search (fp32 storage): allowed when every stored |x| < 2^15 (the screen reads x as f16)
+  bool screen_ok = false;
+  int screen_seq = 0;
+  int64_t screen_blocks = 0;
+  int64_t screen_reruns = 0;
+  bool last_screened = false;   // the last search (rr_search_staged) ran screened blocks
+  int last_seq0 = 0;            // ... and its first block's sequence number
 };
 
 namespace {
@@ -141,6 +152,10 @@ size_t elem_bytes(int dtype) { return dtype == RR_DTYPE_BF16 ? 2 : 4; }
 // Query slots per corpus pass, at most (the split-K kernel serves 64 queries per pass for bf16 and
 // fp32-split storage; every other path 32).
 constexpr int kMaxSlots = 64;
+// Result buffer head (the screened-search flag word, then padding) and the words each exchanged candidate list
+// carries after its keys (word 0: the shard's flag).
+constexpr size_t kOutHead = 64;
+constexpr int kXTail = 8;
 
 // How each public corpus dtype is stored and multiplied (rr_internal.h KDT_*).
 int kdt_of(int dtype) {
@@ -170,7 +185,7 @@ int dmalloc(T** p, size_t bytes) {
 
 int free_shard(Shard& s) {
   hipSetDevice(s.dev);
-  void* ptrs[] = {s.corpus, s.norms, s.rscale, s.queries, s.cand, s.shard_keys, s.gathered, s.out_base,
+  void* ptrs[] = {s.corpus, s.norms, s.rscale, s.queries, s.cand, s.scount, s.shard_keys, s.gathered, s.out_base,
                   s.full_keys, s.sorted, s.sort_temp, s.px_keys[0], s.px_keys[1], s.px_gathered[0], s.px_gathered[1]};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -203,12 +218,40 @@ int alloc_corpus(rr_handle* h, Shard& s) {
   return RR_OK;
 }
 
-int finish_corpus(rr_handle* h, Shard& s) {
+// Per-row norms (cosine, and the screened search's bound for fp32 storage) and, for fp32 storage, whether
+// every value fits the screen's f16 reading (|x| < 2^15). Returns the shard's verdict in *screen_ok.
+int finish_corpus(rr_handle* h, Shard& s, bool* screen_ok) {
   HIP_TRY(hipSetDevice(s.dev));
+  const bool f32 = kdt_of(h->dtype) == rr::KDT_F32_MFMA;
   // split-f16 rows got their norms (of the fp32 values) during the split
-  if (h->metric == RR_METRIC_COSINE && s.rows() > 0 && kdt_of(h->dtype) != rr::KDT_F32_SPLIT)
+  if ((h->metric == RR_METRIC_COSINE || f32) && s.rows() > 0 && kdt_of(h->dtype) != rr::KDT_F32_SPLIT)
     HIP_TRY(rr::launch_row_norms(h->dtype == RR_DTYPE_BF16 ? 1 : 0, s.corpus, s.rows(), h->d, s.norms, s.stream));
+  *screen_ok = false;
+  if (f32) {
+    float* dmax = nullptr;
+    HIP_TRY(hipMalloc((void**)&dmax, sizeof(float)));
+    hipError_t e = hipMemsetAsync(dmax, 0, sizeof(float), s.stream);
+    if (e == hipSuccess && s.rows() > 0) e = rr::launch_absmax((const float*)s.corpus, s.rows() * h->d, dmax, s.stream);
+    float m = 0.f;
+    if (e == hipSuccess) e = hipMemcpyAsync(&m, dmax, sizeof(float), hipMemcpyDeviceToHost, s.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+    hipFree(dmax);
+    if (e != hipSuccess) return fail(RR_E_HIP, "corpus range check failed: %s", hipGetErrorString(e));
+    *screen_ok = m < 32768.0f;   // also false for NaN
+  }
   HIP_TRY(hipStreamSynchronize(s.stream));
+  return RR_OK;
+}
+
+// Finish every local shard; the screened search is allowed only when every shard's range allows it.
+int finish_all(rr_handle* h) {
+  bool ok = true;
+  for (Shard& s : h->shards) {
+    bool sok = false;
+    if (int rc = finish_corpus(h, s, &sok)) return rc;
+    ok = ok && sok;
+  }
+  h->screen_ok = ok;
   return RR_OK;
 }
 
@@ -303,7 +346,7 @@ int drop_work_buffers(rr_handle* h) {
     HIP_TRY(hipSetDevice(s.dev));
     HIP_TRY(hipStreamSynchronize(s.stream));
     HIP_TRY(hipStreamSynchronize(s.xstream));
-    void** ptrs[] = {(void**)&s.queries, (void**)&s.cand, (void**)&s.shard_keys, (void**)&s.gathered,
+    void** ptrs[] = {(void**)&s.queries, (void**)&s.cand, (void**)&s.scount, (void**)&s.shard_keys, (void**)&s.gathered,
                      (void**)&s.out_base, (void**)&s.full_keys, (void**)&s.sorted, &s.sort_temp,
                      (void**)&s.px_keys[0], (void**)&s.px_keys[1], (void**)&s.px_gathered[0],
                      (void**)&s.px_gathered[1]};
@@ -321,6 +364,9 @@ int drop_work_buffers(rr_handle* h) {
   h->last_k = 0;
   h->last_b = 0;
   h->parity = 0;
+  h->screen_blocks = 0;   // the flagged-block counters (scount) were freed above
+  h->screen_reruns = 0;
+  h->last_screened = false;
   h->loaded = false;
   return RR_OK;
 }
@@ -349,9 +395,10 @@ int ensure_buffers(rr_handle* h, int b, int k) {
         HIP_TRY(hipMemset(s.queries, 0, (size_t)((qc + kMaxSlots - 1) / kMaxSlots * kMaxSlots) * h->d * 4));
       }
       // scores and indices in one allocation, so a search's results come back in ONE D2H copy
-      s.out_off = ((size_t)qc * kc * 4 + 255) & ~(size_t)255;
+      s.out_off = (kOutHead + (size_t)qc * kc * 4 + 255) & ~(size_t)255;
       if (int rc = dmalloc(&s.out_base, s.out_off + (size_t)qc * kc * 8)) return rc;
-      s.out_scores = (float*)s.out_base;
+      HIP_TRY(hipMemset(s.out_base, 0, kOutHead));   // the screened-search flag word starts at 0
+      s.out_scores = (float*)(s.out_base + kOutHead);
       s.out_idx = (int64_t*)(s.out_base + s.out_off);
       const int kk = std::max(kc, RR_FUSED_KMAX);
       if (int rc = dmalloc(&s.shard_keys, (size_t)rr::kQSlots * kk * 8)) return rc;
@@ -362,11 +409,16 @@ int ensure_buffers(rr_handle* h, int b, int k) {
     if (!s.cand) {
       s.cand_grid = s.cus;
       if (int rc = dmalloc(&s.cand, (size_t)s.cand_grid * kMaxSlots * RR_FUSED_KMAX * 8)) return rc;
+      if (int rc = dmalloc(&s.scount, sizeof(int))) return rc;
+      HIP_TRY(hipMemset(s.scount, 0, sizeof(int)));
     }
     if ((h->world > 1 || h->dist) && !s.px_keys[0]) {
       for (int p = 0; p < 2; ++p) {
-        if (int rc = dmalloc(&s.px_keys[p], (size_t)kMaxSlots * RR_FUSED_KMAX * 8)) return rc;
-        if (int rc = dmalloc(&s.px_gathered[p], (size_t)h->world * kMaxSlots * RR_FUSED_KMAX * 8)) return rc;
+        // each exchanged list carries its shard's screened-search flag word after the keys
+        const size_t per = (size_t)kMaxSlots * RR_FUSED_KMAX + kXTail;
+        if (int rc = dmalloc(&s.px_keys[p], per * 8)) return rc;
+        if (int rc = dmalloc(&s.px_gathered[p], (size_t)h->world * per * 8)) return rc;
+        HIP_TRY(hipMemset(s.px_keys[p], 0, per * 8));
       }
     }
     if (k > RR_FUSED_KMAX) {
@@ -405,6 +457,28 @@ int sk_dtype_of(int dtype) {
 bool use_sk(const rr_handle* h) {
   if (h->kernel == RR_KERNEL_FUSED) return false;
   return rr::sk_slabs(sk_dtype_of(h->dtype), h->d) != 0;
+}
+
+// Screened search (rr_sk.hip "Screened search"): list width for k (>= k + 3 spare, 2k + 2 when it fits),
+// 0 when k is too large for it.
+int screen_kt(int k) {
+  const int want = std::max(2 * k + 2, k + 3);
+  if (want <= RR_FUSED_KMAX) return rr::fused_kt(want);
+  return k + 3 <= RR_FUSED_KMAX ? RR_FUSED_KMAX : 0;
+}
+
+// Error bound of the screen (rr_sk.hip): eps = kScreenEpsA |x||q| + kScreenEpsB (sqrt(d) |x| + sum|q|).
+//   f16(x): <= 2^-11 |x| + 2^-25 per element; q - c0 - c1: <= 2^-22 |q| + 2^-24.99;
+//   fp32 accumulation, any order, of the screen (<= 16 MFMAs x 17 roundings + 8 per score) and of the exact
+//   DT 3 score (48 x 17 + 8, plus its dropped split terms <= 4 x 2^-24 |xq|): <= 1.7e-5 and 4.9e-5 of
+//   sum |x_k q_k| <= |x||q|.  Sum: 5.54e-4 |x||q| + 2^-24.9 (sum|x| + sum|q|), sum|x| <= sqrt(d) |x|; with
+//   an 8 % margin on each.
+constexpr float kScreenEpsA = 6.0e-4f;
+constexpr float kScreenEpsB = 4.0e-8f;
+
+bool screened(const rr_handle* h, int k, int slots) {
+  return (h->kernel == RR_KERNEL_AUTO || h->kernel == RR_KERNEL_SCREEN_FALLBACK) && h->dtype == RR_DTYPE_F32 &&
+         h->screen_ok && slots == rr::kQSlots && screen_kt(k) != 0 && use_sk(h);
 }
 
 int fused_grid(const Shard& s) {
@@ -466,7 +540,7 @@ int local_gather(rr_handle* h, int kk) {
 // while the compute stream goes on with the next block. px_keys[p] is rewritten two blocks later and only
 // after ev_xdone[p] of every shard that read it (enqueue_block).
 int enqueue_exchange_px(rr_handle* h, int p, int q0, int bb, int k, int kt, int slots) {
-  const size_t slot = (size_t)slots * kt;
+  const size_t slot = (size_t)slots * kt + kXTail;   // keys + the shard's flag word
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
     HIP_TRY(hipEventRecord(s.ev_keys[p], s.stream));
@@ -485,7 +559,8 @@ int enqueue_exchange_px(rr_handle* h, int p, int q0, int bb, int k, int kt, int 
       }
     }
     HIP_TRY(rr::launch_merge(kt, dst.px_gathered[p], h->world, kt, bb, k, nullptr, dst.out_scores + (size_t)q0 * k,
-                             dst.out_idx + (size_t)q0 * k, dst.xstream, slots));
+                             dst.out_idx + (size_t)q0 * k, dst.xstream, slots, (int64_t)slot,
+                             (uint64_t*)dst.out_base));
     HIP_TRY(hipEventRecord(dst.ev_xdone[p], dst.xstream));
   }
   return RR_OK;
@@ -498,13 +573,33 @@ int block_slots(const rr_handle* h, int b, int k) {
   return rr::kQSlots;
 }
 
+// Kernel arguments common to every split-K launch on this shard.
+rr::SkArgs sk_base(const rr_handle* h, const Shard& s, const float* qb, int bb) {
+  rr::SkArgs a{};
+  a.corpus = (const char*)s.corpus;
+  a.norms = s.norms;
+  a.rscale = s.rscale;
+  a.queries = qb;
+  a.n = s.rows();
+  a.d = h->d;
+  a.b = bb;
+  a.idx_base = (uint32_t)s.row_begin;
+  return a;
+}
+
 // Enqueue the device pipeline for query block [q0, q0 + bb) (bb <= slots) on every local shard.
 int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
   const int d = h->d;
-  const int kt = rr::fused_kt(k);
+  const bool scr = screened(h, k, slots);
+  const int kt = scr ? screen_kt(k) : rr::fused_kt(k);
   const bool multi = h->world > 1 || h->dist;   // an exchange step (RCCL with any world, peer copies)
   const bool local_multi = multi && !h->dist;
   const int p = h->parity;
+  if (scr) {
+    ++h->screen_seq;
+    ++h->screen_blocks;
+  }
+  const int seq = h->screen_seq;
   for (size_t si = 0; si < h->shards.size(); ++si) {
     Shard& s = h->shards[si];
     HIP_TRY(hipSetDevice(s.dev));
@@ -528,14 +623,47 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
     float* osc = s.out_scores + (size_t)q0 * k;
     int64_t* oix = s.out_idx + (size_t)q0 * k;
     const uint32_t base = (uint32_t)s.row_begin;
-    if (kt) {
-      int grid = fused_grid(s);
-      hipEvent_t e0 = nullptr, e1 = nullptr;
-      const bool timed = h->timing && si == 0;
-      if (timed) {
-        if (int rc = next_event_pair(s, &e0, &e1)) return rc;
-        HIP_TRY(hipEventRecord(e0, s.stream));
+    const bool timed = h->timing && si == 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (timed)
+      if (int rc = next_event_pair(s, &e0, &e1)) return rc;
+    if (scr) {
+      // screened search: screen (upper bounds) -> verify (exact DT 3 scores of the KT candidates, results;
+      // raises the block's flag word when the bound cannot prove completeness: settle_screen re-runs then)
+      if (multi) HIP_TRY(wait_px(p));
+      if (s.rows() > 0) {
+        const int sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(s.cand_grid, (s.rows() + 31) / 32));
+        rr::SkArgs a = sk_base(h, s, qb, bb);
+        a.out = s.cand;
+        a.eps_a = kScreenEpsA;
+        a.eps_b = kScreenEpsB;
+        a.sqrt_d = sqrtf((float)d) * (1.0f + 0x1p-20f);
+        if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
+        HIP_TRY(rr::launch_sk_args(rr::KDT_SCREEN, h->metric, kt, 0, sgrid, rr::kQSlots, a, s.stream));
+        if (timed) HIP_TRY(hipEventRecord(e1, s.stream));
+        rr::SkArgs v = sk_base(h, s, qb, bb);
+        v.vin = s.cand;
+        v.nlists = sgrid;
+        v.k_out = k;
+        v.out_scores = multi ? nullptr : osc;
+        v.out_idx = multi ? nullptr : oix;
+        v.out_keys = multi ? s.px_keys[p] : nullptr;
+        // the block's flag word: the result buffer's head, or (exchange) the word after this shard's keys
+        v.flag = multi ? s.px_keys[p] + (size_t)slots * kt : (uint64_t*)s.out_base;
+        v.count = s.scount;
+        v.seq = seq;
+        v.force_incomplete = h->kernel == RR_KERNEL_SCREEN_FALLBACK;
+        HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 1, rr::kQSlots, rr::kQSlots, v, s.stream));
+      } else {   // a shard without rows contributes empty lists
+        if (timed) {
+          HIP_TRY(hipEventRecord(e0, s.stream));
+          HIP_TRY(hipEventRecord(e1, s.stream));
+        }
+        HIP_TRY(hipMemsetAsync(s.px_keys[p], 0, (size_t)slots * kt * 8, s.stream));
       }
+    } else if (kt) {
+      int grid = fused_grid(s);
+      if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
       if (s.rows() > 0) {
         if (use_sk(h)) {
           const int sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(s.cand_grid, (s.rows() + 31) / 32));
@@ -560,6 +688,7 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
       // k > RR_FUSED_KMAX: all keys of this shard, segmented radix sort, keep the first k. The exchange
       // is serial on the compute stream, after every pipelined exchange still writing results.
       const int64_t rows = s.rows();
+      if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
       if (multi) {
         HIP_TRY(wait_px(0));
         HIP_TRY(wait_px(1));
@@ -570,9 +699,12 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
         const int grid = fused_grid(s);
         HIP_TRY(rr::launch_full_keys(kdt_of(h->dtype), h->metric, grid, s.corpus, s.norms, s.rscale, qb, rows, d,
                                      bb, base, s.full_keys, s.stream));
+        if (timed) HIP_TRY(hipEventRecord(e1, s.stream));
         size_t tb = s.sort_temp_bytes;
         HIP_TRY(rr::segmented_sort_desc(s.sort_temp, &tb, s.full_keys, s.sorted, bb, rows, s.stream));
         HIP_TRY(rr::launch_take_prefix(s.sorted, bb, rows, k, s.shard_keys, s.stream));
+      } else if (timed) {
+        HIP_TRY(hipEventRecord(e1, s.stream));
       }
       if (!multi) HIP_TRY(rr::launch_decode(s.shard_keys, bb, k, osc, oix, s.stream));
     }
@@ -728,11 +860,10 @@ int rr_dist_info(const rr_handle* h, int* rccl_ranks, int* rccl_rank) {
 int rr_load(rr_handle* h, const float* host_corpus, int64_t n, int32_t d) {
   if (!h || !host_corpus) return fail(RR_E_INVALID, "null argument");
   if (int rc = prepare_ranges(h, n, d)) return rc;
-  for (Shard& s : h->shards) {
+  for (Shard& s : h->shards)
     if (s.rows() > 0)
       if (int rc = upload_rows(h, s, host_corpus + s.row_begin * (int64_t)d, 0, s.rows())) return rc;
-    if (int rc = finish_corpus(h, s)) return rc;
-  }
+  if (int rc = finish_all(h)) return rc;
   h->loaded = true;
   return RR_OK;
 }
@@ -747,8 +878,8 @@ int rr_load_rows(rr_handle* h, const float* host_rows, int64_t row_begin, int64_
                   (long long)(row_begin + n_rows), (long long)s.row_begin, (long long)s.row_end);
     if (s.rows() > 0)
       if (int rc = upload_rows(h, s, host_rows + (s.row_begin - row_begin) * (int64_t)d, 0, s.rows())) return rc;
-    if (int rc = finish_corpus(h, s)) return rc;
   }
+  if (int rc = finish_all(h)) return rc;
   h->loaded = true;
   return RR_OK;
 }
@@ -777,8 +908,8 @@ int rr_fill_synthetic(rr_handle* h, int kind, uint64_t seed, int64_t n_total, in
       }
       hipFree(tmp);
     }
-    if (int rc = finish_corpus(h, s)) return rc;
   }
+  if (int rc = finish_all(h)) return rc;
   h->loaded = true;
   return RR_OK;
 }
@@ -889,6 +1020,8 @@ int rr_search_staged(rr_handle* h, int32_t k) {
   const int b = h->cur_b;
   if (int rc = ensure_buffers(h, b, k)) return rc;
   const int slots = block_slots(h, b, k);
+  h->last_screened = screened(h, k, slots);
+  h->last_seq0 = h->screen_seq + 1;
   for (int q0 = 0; q0 < b; q0 += slots) {
     const int bb = std::min(slots, b - q0);
     if (int rc = enqueue_block(h, q0, bb, k, slots)) return rc;
@@ -905,8 +1038,9 @@ int rr_last_shape(const rr_handle* h, int32_t* b, int32_t* k) {
   return RR_OK;
 }
 
-int rr_synchronize(rr_handle* h) {
-  if (!h) return fail(RR_E_INVALID, "null handle");
+namespace {
+
+int sync_streams(rr_handle* h) {
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
     HIP_TRY(hipStreamSynchronize(s.stream));
@@ -915,30 +1049,75 @@ int rr_synchronize(rr_handle* h) {
   return collect_timing(h);
 }
 
+// Screened search, last step: `flag` is the last search's flag word (shard 0's result head, which after an
+// exchange holds the largest flag of every shard, so every rank sees the same value). When a block of that
+// search was flagged, re-run the search — its queries are still staged — with the one-pass exact kernel.
+int settle_screen(rr_handle* h, uint64_t flag, bool* rerun) {
+  *rerun = false;
+  if (!h->last_screened || flag < (uint64_t)h->last_seq0) return RR_OK;
+  const int saved = h->kernel;
+  h->kernel = RR_KERNEL_EXACT;
+  const int rc = rr_search_staged(h, h->last_k);
+  h->kernel = saved;
+  if (rc) return rc;
+  ++h->screen_reruns;
+  *rerun = true;
+  return sync_streams(h);
+}
+
+int read_flag(rr_handle* h, uint64_t* flag) {
+  Shard& s = h->shards[0];
+  *flag = 0;
+  if (!s.out_base) return RR_OK;
+  HIP_TRY(hipSetDevice(s.dev));
+  HIP_TRY(hipMemcpy(flag, s.out_base, sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return RR_OK;
+}
+
+}  // namespace
+
+int rr_synchronize(rr_handle* h) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  if (int rc = sync_streams(h)) return rc;
+  if (!h->last_screened) return RR_OK;
+  uint64_t flag = 0;
+  if (int rc = read_flag(h, &flag)) return rc;
+  bool rerun = false;
+  return settle_screen(h, flag, &rerun);
+}
+
 int rr_fetch_results(rr_handle* h, float* out_scores, int64_t* out_idx) {
   if (!h || !out_scores || !out_idx) return fail(RR_E_INVALID, "null argument");
   if (h->last_k < 1) return fail(RR_E_STATE, "no search has run");
-  if (int rc = rr_synchronize(h)) return rc;
+  if (int rc = sync_streams(h)) return rc;
   Shard& s = h->shards[0];
-  HIP_TRY(hipSetDevice(s.dev));
   const size_t cnt = (size_t)h->last_b * h->last_k;
   const size_t span = s.out_off + cnt * 8;
-  if (s.out_off > (1u << 20)) {   // capacity grown far beyond this search: two plain copies
-    HIP_TRY(hipMemcpy(out_scores, s.out_scores, cnt * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(out_idx, s.out_idx, cnt * 8, hipMemcpyDeviceToHost));
-    return RR_OK;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    HIP_TRY(hipSetDevice(s.dev));
+    uint64_t flag = 0;
+    if (s.out_off > (1u << 20)) {   // capacity grown far beyond this search: plain copies
+      HIP_TRY(hipMemcpy(out_scores, s.out_scores, cnt * 4, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(out_idx, s.out_idx, cnt * 8, hipMemcpyDeviceToHost));
+      if (int rc = read_flag(h, &flag)) return rc;
+    } else {
+      if (span > h->pin_out_cap) {
+        if (h->pin_out) HIP_TRY(hipHostFree(h->pin_out));
+        h->pin_out = nullptr;
+        h->pin_out_cap = 0;
+        HIP_TRY(hipHostMalloc((void**)&h->pin_out, span, hipHostMallocDefault));
+        h->pin_out_cap = span;
+      }
+      // one pinned D2H of [flag word | scores | pad | indices] (the streams are idle)
+      HIP_TRY(hipMemcpy(h->pin_out, s.out_base, span, hipMemcpyDeviceToHost));
+      memcpy(&flag, h->pin_out, sizeof flag);
+      memcpy(out_scores, h->pin_out + kOutHead, cnt * 4);
+      memcpy(out_idx, h->pin_out + s.out_off, cnt * 8);
+    }
+    bool rerun = false;
+    if (int rc = settle_screen(h, flag, &rerun)) return rc;
+    if (!rerun) return RR_OK;
   }
-  if (span > h->pin_out_cap) {
-    if (h->pin_out) HIP_TRY(hipHostFree(h->pin_out));
-    h->pin_out = nullptr;
-    h->pin_out_cap = 0;
-    HIP_TRY(hipHostMalloc((void**)&h->pin_out, span, hipHostMallocDefault));
-    h->pin_out_cap = span;
-  }
-  // one pinned D2H of [scores | pad | indices] (the stream is idle: rr_synchronize above)
-  HIP_TRY(hipMemcpy(h->pin_out, s.out_base, span, hipMemcpyDeviceToHost));
-  memcpy(out_scores, h->pin_out, cnt * 4);
-  memcpy(out_idx, h->pin_out + s.out_off, cnt * 8);
   return RR_OK;
 }
 
@@ -958,9 +1137,11 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
   AsyncSlot& a = h->aslots[t % kAsyncSlots];
   if (a.pending) return fail(RR_E_STATE, "%d searches in flight: rr_wait(%d) first", kAsyncSlots, a.ticket);
   if (int rc = ensure_buffers(h, b, k)) return rc;
+  // pinned slot: [queries | flag word | scores | pad | indices]; the queries stay for a possible re-run
   const size_t qbytes = (size_t)b * d * 4, cnt = (size_t)b * k;
-  const size_t idx_off = (cnt * 4 + 255) & ~(size_t)255;
-  const size_t need = std::max(qbytes, idx_off + cnt * 8);
+  const size_t res_off = (qbytes + 255) & ~(size_t)255;
+  const size_t idx_off = res_off + ((kOutHead + cnt * 4 + 255) & ~(size_t)255);
+  const size_t need = idx_off + cnt * 8;
   if (need > a.cap) {
     if (a.pin) HIP_TRY(hipHostFree(a.pin));
     a.pin = nullptr;
@@ -981,12 +1162,15 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
   Shard& s0 = h->shards[0];
   HIP_TRY(hipSetDevice(s0.dev));
   hipStream_t rs = (h->world > 1 || h->dist) ? s0.xstream : s0.stream;
-  HIP_TRY(hipMemcpyAsync(a.pin, s0.out_scores, cnt * 4, hipMemcpyDeviceToHost, rs));
+  HIP_TRY(hipMemcpyAsync(a.pin + res_off, s0.out_base, kOutHead, hipMemcpyDeviceToHost, rs));
+  HIP_TRY(hipMemcpyAsync(a.pin + res_off + kOutHead, s0.out_scores, cnt * 4, hipMemcpyDeviceToHost, rs));
   HIP_TRY(hipMemcpyAsync(a.pin + idx_off, s0.out_idx, cnt * 8, hipMemcpyDeviceToHost, rs));
   HIP_TRY(hipEventRecord(a.done, rs));
   a.b = b;
   a.k = k;
   a.ticket = t;
+  a.screened = h->last_screened;
+  a.seq0 = h->last_seq0;
   a.pending = true;
   h->next_ticket = t + 1 < 0x40000000 ? t + 1 : 0;
   *ticket = t;
@@ -999,16 +1183,53 @@ int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx) {
   AsyncSlot& a = h->aslots[ticket % kAsyncSlots];
   if (!a.pending || a.ticket != ticket) return fail(RR_E_STATE, "ticket %d is not in flight", ticket);
   HIP_TRY(hipEventSynchronize(a.done));
-  const size_t cnt = (size_t)a.b * a.k;
-  memcpy(out_scores, a.pin, cnt * 4);
-  memcpy(out_idx, a.pin + ((cnt * 4 + 255) & ~(size_t)255), cnt * 8);
   a.pending = false;
+  const size_t qbytes = (size_t)a.b * h->d * 4, cnt = (size_t)a.b * a.k;
+  const size_t res_off = (qbytes + 255) & ~(size_t)255;
+  const size_t idx_off = res_off + ((kOutHead + cnt * 4 + 255) & ~(size_t)255);
+  uint64_t flag = 0;
+  memcpy(&flag, a.pin + res_off, sizeof flag);
+  if (a.screened && flag >= (uint64_t)a.seq0) {
+    // a block needed the exact pass: this batch again, exactly (every rank of an exchange sees the same
+    // flag here, so all re-run it together)
+    if (int rc = sync_streams(h)) return rc;
+    for (Shard& s : h->shards) {
+      HIP_TRY(hipSetDevice(s.dev));
+      HIP_TRY(hipMemcpyAsync(s.queries, a.pin, qbytes, hipMemcpyHostToDevice, s.stream));
+    }
+    h->cur_b = a.b;
+    const int saved = h->kernel;
+    h->kernel = RR_KERNEL_EXACT;
+    const int rc = rr_search_staged(h, a.k);
+    h->kernel = saved;
+    if (rc) return rc;
+    ++h->screen_reruns;
+    return rr_fetch_results(h, out_scores, out_idx);
+  }
+  memcpy(out_scores, a.pin + res_off + kOutHead, cnt * 4);
+  memcpy(out_idx, a.pin + idx_off, cnt * 8);
   return collect_timing(h);
+}
+
+int rr_screen_stats(rr_handle* h, int64_t* blocks, int64_t* fallbacks) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  if (int rc = rr_synchronize(h)) return rc;
+  int64_t fb = 0;
+  for (Shard& s : h->shards) {
+    if (!s.scount) continue;
+    int f = 0;
+    HIP_TRY(hipSetDevice(s.dev));
+    HIP_TRY(hipMemcpy(&f, s.scount, sizeof f, hipMemcpyDeviceToHost));
+    fb += f;
+  }
+  if (blocks) *blocks = h->screen_blocks * (int64_t)h->shards.size();
+  if (fallbacks) *fallbacks = fb;
+  return RR_OK;
 }
 
 int rr_set_kernel(rr_handle* h, int kernel) {
   if (!h) return fail(RR_E_INVALID, "null handle");
-  if (kernel != RR_KERNEL_AUTO && kernel != RR_KERNEL_FUSED) return fail(RR_E_INVALID, "bad kernel %d", kernel);
+  if (kernel < RR_KERNEL_AUTO || kernel > RR_KERNEL_SCREEN_FALLBACK) return fail(RR_E_INVALID, "bad kernel %d", kernel);
   h->kernel = kernel;
   return RR_OK;
 }

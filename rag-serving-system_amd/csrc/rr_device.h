@@ -74,14 +74,43 @@ struct TopK {
   }
 };
 
+// ------------------------------------------------------------------------------------------------
+// cross-lane max of 64-bit keys with DPP (row ops take a VALU slot each; no LDS round trip as the
+// ds_swizzle / ds_bpermute forms of __shfl_xor do): the high words first, then the low words of the
+// lanes that hold the high maximum.
+// ------------------------------------------------------------------------------------------------
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ uint32_t dpp_max_u32(uint32_t v) {
+  const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROW_MASK, 0xF, false);
+  return v > t ? v : t;
+}
+// max over aligned groups of G lanes (G = 2, 4, 8, 16), every lane of the group gets it
+template <int G>
+__device__ __forceinline__ uint32_t group_max_u32(uint32_t v) {
+  static_assert(G == 2 || G == 4 || G == 8 || G == 16, "DPP row groups");
+  v = dpp_max_u32<0xB1>(v);                        // quad_perm [1,0,3,2]
+  if constexpr (G >= 4) v = dpp_max_u32<0x4E>(v);  // quad_perm [2,3,0,1]
+  if constexpr (G >= 8) v = dpp_max_u32<0x141>(v); // row_half_mirror
+  if constexpr (G >= 16) v = dpp_max_u32<0x140>(v); // row_mirror
+  return v;
+}
+// max over the 64 lanes, returned in every lane
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = group_max_u32<16>(v);
+  v = dpp_max_u32<0x142, 0xA>(v);                   // row_bcast:15 into rows 1, 3
+  v = dpp_max_u32<0x143, 0xC>(v);                   // row_bcast:31 into rows 2, 3: lane 63 has the max
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+template <int G>
+__device__ __forceinline__ uint64_t group_max_u64(uint64_t x) {
+  const uint32_t hi = group_max_u32<G>((uint32_t)(x >> 32));
+  const uint32_t lo = group_max_u32<G>((uint32_t)(x >> 32) == hi ? (uint32_t)x : 0u);
+  return ((uint64_t)hi << 32) | lo;
+}
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, off, 64);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), off, 64);
-    x = umax64(x, ((uint64_t)hi << 32) | lo);
-  }
-  return x;
+  const uint32_t hi = wave_max_u32((uint32_t)(x >> 32));
+  const uint32_t lo = wave_max_u32((uint32_t)(x >> 32) == hi ? (uint32_t)x : 0u);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 }  // namespace rr

@@ -25,6 +25,9 @@ constexpr int KDT_F32_SPLIT = 2;
 //   KDT_F32_X3   : fp32 rows, each value split exactly into three bf16 in registers, 6 bf16 MFMAs
 //                  (split-K kernel only; rr_sk.hip)
 constexpr int KDT_F32_X3 = 3;
+//   KDT_SCREEN   : fp32 rows read as f16 against the query's f16 hi + lo: an upper bound of the KDT_F32_X3
+//                  score for the screened search (split-K kernel only; rr_sk.hip "Screened search")
+constexpr int KDT_SCREEN = 6;
 
 // Smallest fused-kernel list width KT >= k (4, 8, 16, 32); 0 if k > RR_FUSED_KMAX.
 int fused_kt(int k);
@@ -38,6 +41,30 @@ size_t fused_lds_bytes(int d, int kt, int kdt);
 hipError_t launch_fused(int kdt, int metric, int kt, int grid, const void* corpus, const float* norms,
                         const float* rscale, const float* queries, int64_t n, int d, int b, uint32_t idx_base,
                         uint64_t* cand, hipStream_t s);
+
+// Arguments of the split-K kernel (rr_sk.hip), all modes.
+struct SkArgs {
+  const char* corpus;      // this shard's rows in the storage layout
+  const float* norms;      // [rows] |row| (cosine; and the screen's bound)
+  const float* rscale;     // [rows] split-f16 row scales
+  const float* queries;    // [slots][d] fp32
+  int64_t n;               // rows of this shard
+  int d, b;                // dimension, queries in this block
+  uint32_t idx_base;       // global index of local row 0
+  uint64_t* out;           // MODE 0: [grid][slots][KT] candidate keys
+  // screen (KDT_SCREEN): upper bound u = s~ + eps_a |x||q| + eps_b (sqrt_d |x| + sum|q|)
+  float eps_a, eps_b, sqrt_d;
+  // MODE 1 (verify, one workgroup per query slot)
+  const uint64_t* vin;     // [nlists][slots][KT] screen keys
+  int nlists, k_out;
+  float* out_scores;       // [b][k_out] (may be null)
+  int64_t* out_idx;        // [b][k_out]
+  uint64_t* out_keys;      // [slots][KT] exact keys (may be null)
+  uint64_t* flag;          // MODE 1: raised (atomic max) to seq when the block needs the exact pass
+  int* count;              // MODE 1: blocks flagged so far (statistics)
+  int seq;                 // this search block's sequence number (> every earlier one)
+  int force_incomplete;    // MODE 1 test hook: report the block incomplete
+};
 
 // Split-K streaming kernel (rr_sk.hip): same output contract as launch_fused. sdt = KDT_* (0..3).
 // sk_slabs(sdt, d) = 128-byte slabs per wave per row (1..4; bf16 1..2), 0 if d is not supported.
@@ -53,11 +80,21 @@ size_t sk_lds_bytes(int sdt, bool cos, int ring, int qslots);
 hipError_t launch_sk(int sdt, int metric, int kt, int grid, const void* corpus, const float* norms,
                      const float* rscale, const float* queries, int64_t n, int d, int b, uint32_t idx_base,
                      uint64_t* cand, hipStream_t s, int ring = 0, int qslots = 32);
+// Any mode: mode 0 (top-KT per workgroup; sdt KDT_SCREEN = the screen), mode 1 (verify, grid = 32).
+hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int qslots, const SkArgs& a,
+                          hipStream_t s, int ring = 0);
 
 // Merge nlists candidate lists laid out [nlists][slots][in_kt] into the top-kt per query.
 // out_keys [slots][kt] (may be null); out_scores/out_idx [b][k_out] (may be null).
+// list_stride: elements between consecutive lists (0: slots * in_kt). flag_out: when non-null, raised
+// (max) to the largest of the words at in[l * list_stride + slots * in_kt] over the lists — the exchanged
+// screened-search flags of every shard.
 hipError_t launch_merge(int kt, const uint64_t* in, int nlists, int in_kt, int b, int k_out,
-                        uint64_t* out_keys, float* out_scores, int64_t* out_idx, hipStream_t s, int slots = 32);
+                        uint64_t* out_keys, float* out_scores, int64_t* out_idx, hipStream_t s, int slots = 32,
+                        int64_t list_stride = 0, uint64_t* flag_out = nullptr);
+
+// Largest |x| of n values (non-negative float bits compared as ints) into *out (device, pre-zeroed).
+hipError_t launch_absmax(const float* x, int64_t n, float* out, hipStream_t s);
 
 // Full-score path for k > RR_FUSED_KMAX: keys [b][n] for every (query, doc) pair.
 hipError_t launch_full_keys(int kdt, int metric, int grid, const void* corpus, const float* norms,

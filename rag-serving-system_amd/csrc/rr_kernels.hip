@@ -459,20 +459,27 @@ template <int KT>
 __global__ __launch_bounds__(256) void merge_kernel(const uint64_t* __restrict__ in, int nlists, int slots, int b,
                                                     int k_out, uint64_t* __restrict__ out_keys,
                                                     float* __restrict__ out_scores,
-                                                    int64_t* __restrict__ out_idx) {
+                                                    int64_t* __restrict__ out_idx, int64_t stride,
+                                                    uint64_t* __restrict__ flag_out) {
   const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (flag_out && q == 0 && tid < 64) {   // the shards' screened-search flags (one word after each list)
+    uint64_t f = 0;
+    for (int l = tid; l < nlists; l += 64) f = umax64(f, in[(size_t)l * stride + (size_t)slots * KT]);
+    f = wave_max_u64(f);
+    if (tid == 0 && f > *flag_out) *flag_out = f;   // the word only grows; stream order serialises writers
+  }
   __shared__ uint64_t L[256][KT];
   __shared__ uint64_t W[4 * KT];
   TopK<KT> tk;
   if (tid < nlists) {
-    const uint64_t* src = in + ((size_t)tid * slots + q) * KT;
+    const uint64_t* src = in + (size_t)tid * stride + (size_t)q * KT;
 #pragma unroll
     for (int i = 0; i < KT; ++i) tk.v[i] = src[i];
   } else {
     tk.init();
   }
   for (int l = tid + 256; l < nlists; l += 256) {
-    const uint64_t* src = in + ((size_t)l * slots + q) * KT;
+    const uint64_t* src = in + (size_t)l * stride + (size_t)q * KT;
     for (int i = 0; i < KT; ++i) {
       const uint64_t key = src[i];
       if (key <= tk.last()) break;            // sorted input: nothing further can enter
@@ -815,16 +822,18 @@ hipError_t launch_full_keys(int kdt, int metric, int grid, const void* c, const 
 }
 
 hipError_t launch_merge(int kt, const uint64_t* in, int nlists, int in_kt, int b, int k_out, uint64_t* out_keys,
-                        float* out_scores, int64_t* out_idx, hipStream_t s, int slots) {
+                        float* out_scores, int64_t* out_idx, hipStream_t s, int slots, int64_t list_stride,
+                        uint64_t* flag_out) {
+  if (list_stride == 0) list_stride = (int64_t)slots * in_kt;
   if (in_kt != kt) return hipErrorInvalidValue;   // lists are always produced at the kernel's KT
   // Rows >= b of out_keys are still produced (from the zero-filled slots) so the buffer is uniform.
   if (b > slots) return hipErrorInvalidValue;
   const int grid = out_keys ? slots : b;
   switch (kt) {
-    case 4: hipLaunchKernelGGL(merge_kernel<4>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx); break;
-    case 8: hipLaunchKernelGGL(merge_kernel<8>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx); break;
-    case 16: hipLaunchKernelGGL(merge_kernel<16>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx); break;
-    case 32: hipLaunchKernelGGL(merge_kernel<32>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx); break;
+    case 4: hipLaunchKernelGGL(merge_kernel<4>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out); break;
+    case 8: hipLaunchKernelGGL(merge_kernel<8>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out); break;
+    case 16: hipLaunchKernelGGL(merge_kernel<16>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out); break;
+    case 32: hipLaunchKernelGGL(merge_kernel<32>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -900,6 +909,20 @@ hipError_t launch_row_norms(int dtype, const void* corpus, int64_t n, int d, flo
   const unsigned grid = (unsigned)((n + 3) / 4);
   if (dtype == 0) hipLaunchKernelGGL(row_norms_kernel<0>, dim3(grid), dim3(256), 0, s, corpus, n, d, norms);
   else hipLaunchKernelGGL(row_norms_kernel<1>, dim3(grid), dim3(256), 0, s, corpus, n, d, norms);
+  return hipGetLastError();
+}
+
+__global__ void absmax_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
+  float m = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(x[i]));
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax((int*)out, __float_as_int(m));   // non-negative: int order = float order
+}
+
+hipError_t launch_absmax(const float* x, int64_t n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(absmax_kernel, dim3(1024), dim3(256), 0, s, x, n, out);
   return hipGetLastError();
 }
 

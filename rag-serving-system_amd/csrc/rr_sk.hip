@@ -30,7 +30,27 @@
 //     partial product is exact in fp32 and the dropped terms (b1c2, b2c1, b2c2) are below 2^-23 |x q|
 //     (unbiased), the size of one fp32 rounding per product, so a score carries fp32 summation error
 //     only. Half of DT 0's matrix-core cycles (and no f32-MFMA clock throttling).
+//   6 SCREEN over fp32 rows: x rounded to f16 (one v_cvt_pk_f16_f32 per pair), q = c0 + c1 in f16, two f16
+//     MFMAs per K-step. Not a score: the key is an UPPER BOUND u >= the DT 3 score (see "Screened search").
 // The K order inside a wave's slice is a permutation applied identically to both operands.
+//
+// Screened search (fp32 storage, k <= 29; rr_api.cpp enqueue_block):
+//   1. MODE 0, DT 6 over the shard: per doc and query an upper bound u = s~ + eps of the exact DT 3 score
+//      (cosine: of the clipped quotient), eps = eps_a |x||q| + eps_b (sqrt(d) |x| + sum|q|) from the
+//      f16 rounding of x (<= 2^-11 |x| + 2^-25 per element), of the query split (<= 2^-22 |q| + 2^-24.9) and
+//      generous fp32 accumulation bounds for both computations (rr_api.cpp kScreenEpsA/B); top-KT
+//      (KT >= k + 3) by u per workgroup. At half the matrix-core work and a tenth of the vector work of
+//      DT 3 it streams at the LDS-DMA rate, also while the GPU's power management throttles the core
+//      clock during its first ~40 launches out of idle (profiles/r02/kbench_transient_screen.log).
+//   2. MODE 1, DT 3, one workgroup per query slot: merges the screen's lists into the global top-KT by u,
+//      gathers those KT rows and scores them with EXACTLY the DT 3 arithmetic (same K split, MFMA order
+//      and wave-reduction order: bit-identical to a full DT 3 pass), keeps the exact top-k. Complete
+//      when the exact k-th score is strictly above the KT-th upper bound (every other doc's exact score
+//      is at most its u, which is at most that bound) — or when the shard has fewer than KT docs.
+//   3. Otherwise (rare: > KT - k docs inside the bound's window) the verify raises the block's flag word
+//      (a monotonic sequence number; exchanged with the candidates when shards exchange) and the host
+//      re-runs that search with the exact one-pass kernel when it collects the results (rr_api.cpp).
+//   Either way the results are those of the exact DT 3 path, for every shard layout.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "rr_device.h"
@@ -123,26 +143,6 @@ __device__ __forceinline__ void split3(const float (&x)[8], bf16x8& b0, bf16x8& 
   b2 = __builtin_bit_cast(bf16x8, p2);
 }
 
-// x = b0 + b1 + r with |r| <= 2^-16 |x| (the first two splits of split3; r dropped). 6 VALU per pair.
-__device__ __forceinline__ void split2(const float (&x)[8], bf16x8& b0, bf16x8& b1) {
-  u32x4 p0, p1;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float a = x[2 * i], b = x[2 * i + 1];
-    p0[i] = cvt_pk_bf16(a, b);
-    const float ra = a - __uint_as_float(p0[i] << 16), rb = b - __uint_as_float(p0[i] & 0xFFFF0000u);
-    p1[i] = cvt_pk_bf16(ra, rb);
-  }
-  b0 = __builtin_bit_cast(bf16x8, p0);
-  b1 = __builtin_bit_cast(bf16x8, p1);
-}
-__device__ __forceinline__ bf16x8 split1(const float (&x)[8]) {
-  u32x4 p0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) p0[i] = cvt_pk_bf16(x[2 * i], x[2 * i + 1]);
-  return __builtin_bit_cast(bf16x8, p0);
-}
-
 // All-ones / all-zeros lane mask the compiler cannot see through, and x AND-ed with it: the loads that
 // feed it are then issued unconditionally (a select on the predicate gets turned into exec-masked branches
 // around each load, which serialises their latencies). Exact zeros, whatever x holds.
@@ -169,27 +169,77 @@ struct QFrag<2, NS> { f16x8 hi[NS][2], lo[NS][2]; };          // 2 K-steps of 16
 template <int NS>
 struct QFrag<3, NS> { bf16x8 c0[NS][2], c1[NS][2], c2[NS][2]; };
 template <int NS>
-struct QFrag<4, NS> { bf16x8 c0[NS][2], c1[NS][2]; };
-template <int NS>
-struct QFrag<5, NS> { bf16x8 c0[NS][2], c1[NS][2]; };
+struct QFrag<6, NS> { f16x8 c0[NS][2], c1[NS][2]; };          // screen: q = c0 + c1 (+ <= 2^-22 |q|)
 
 
 // LDS byte offset (within a slot) of 16-byte column position cp of tile row r (swizzled image)
 __device__ __forceinline__ int slab_off(int r, int cp) { return (r >> 3) * 1024 + (r & 7) * 128 + ((cp ^ (r & 7)) << 4); }
 
+// Verify stage (MODE 1): the screen's [nlists][QS][KT] upper-bound lists -> this query's global top-KT by u
+// in akeys[] (LDS), KT rounds of a wave-wide max per wave, then one wave merges the 8 wave lists.
+template <int KT>
+__device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict__ in, int nlists, int qslots, int q,
+                                                      uint64_t* W, uint64_t* akeys) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  TopK<KT> tk;
+  if (tid < nlists) {
+    const uint64_t* src = in + ((size_t)tid * qslots + q) * KT;
+#pragma unroll
+    for (int i = 0; i < KT; ++i) tk.v[i] = src[i];
+  } else {
+    tk.init();
+  }
+  for (int l = tid + kThreads; l < nlists; l += kThreads) {   // lists beyond 512 folded in (sorted input)
+    const uint64_t* src = in + ((size_t)l * qslots + q) * KT;
+    for (int i = 0; i < KT; ++i) {
+      const uint64_t key = src[i];
+      if (key <= tk.last()) break;
+      tk.insert(key);
+    }
+  }
+  for (int rnd = 0; rnd < KT; ++rnd) {
+    const uint64_t m = wave_max_u64(tk.v[0]);
+    if (lane == 0) W[wid * KT + rnd] = m;
+    if (m != 0 && tk.v[0] == m) tk.pop();   // keys are unique: exactly one owner
+  }
+  __syncthreads();
+  if (wid == 0) {
+    constexpr int PER = (kWaves * KT + 63) / 64;   // per-wave winners held per lane
+    uint64_t e[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) e[i] = lane + 64 * i < kWaves * KT ? W[lane + 64 * i] : 0;
+    for (int rnd = 0; rnd < KT; ++rnd) {
+      uint64_t best = 0;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) best = umax64(best, e[i]);
+      best = wave_max_u64(best);
+#pragma unroll
+      for (int i = 0; i < PER; ++i) e[i] = (best != 0 && e[i] == best) ? 0 : e[i];
+      if (lane == 0) akeys[rnd] = best;
+    }
+  }
+  __syncthreads();
+}
+
 // QH = query halves: 32 * QH query slots per pass (64 for the batch-64 configs: one corpus pass serves
 // them all; each A fragment then feeds the MFMAs of both halves).
-template <int DT, int NS, int KT, bool COS, int RS, int QH>
-__global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict__ corpus,
-                                                          const float* __restrict__ norms,
-                                                          const float* __restrict__ rscale,
-                                                          const float* __restrict__ queries, int64_t n, int d,
-                                                          int b, uint32_t idx_base, uint64_t* __restrict__ out) {
+// MODE 0: top-KT per query over this workgroup's rows (DT 6: by upper bound).
+// MODE 1: verify (DT 3, QH 1): block q = query slot q; see "Screened search" above.
+template <int DT, int NS, int KT, bool COS, int RS, int QH, int MODE>
+__global__ __launch_bounds__(512, 1) void sk_score_kernel(const SkArgs a) {
   static_assert(RS == 2 || RS == 3, "ring depth 2 or 3 (the tail waits are written for these)");
   static_assert(QH == 1 || QH == 2, "32 or 64 query slots");
+  static_assert(MODE == 0 || (DT == 3 && QH == 1), "the verify stage runs the exact fp32 arithmetic");
   constexpr int QS = 32 * QH;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   SK_PROBE(0);
+  const char* __restrict__ corpus = a.corpus;
+  const float* __restrict__ norms = a.norms;
+  const float* __restrict__ rscale = a.rscale;
+  const float* __restrict__ queries = a.queries;
+  const int64_t n = a.n;
+  const int d = a.d, b = a.b;
+  const uint32_t idx_base = a.idx_base;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
@@ -199,17 +249,36 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
   const int p0 = w * (KS / 16);                                 // first 16-byte storage unit of the slice
 
   float* red = (float*)(smem + ring_bytes(RS));
-  constexpr int SW = (COS ? 1 : 0) + (DT == 2 ? 1 : 0);          // per-doc floats in the segment
+  constexpr int SW = (COS || DT == 6 ? 1 : 0) + (DT == 2 ? 1 : 0);   // per-doc floats in the segment
   float* seg = (float*)(smem + ring_bytes(RS) + red_bytes(RS, QH));
-  float* qinfo = seg + kSegRows * (SW > 0 ? SW : 1);            // [QS] |q|, [QS] 2^-e (split), [QS] int e
+  float* qinfo = seg + kSegRows * (SW > 0 ? SW : 1);            // [QS] |q|, [QS] 2^-e / sum|q| / max|q|, [QS] int e
   int* qexp = (int*)(qinfo + 2 * QS);
 
-  // ---- this workgroup's rows ----------------------------------------------------------------------------
+  // ---- MODE 1: the candidate rows of query slot vq ---------------------------------------------------------
+  // (LDS after qexp: merge scratch W [8][KT], akeys [KT], grow [32], gnorm [32], gvalid [32], xk [KT])
+  const int vq = MODE == 1 ? (int)blockIdx.x : 0;
+  uint64_t* vW = (uint64_t*)(qexp + QS);
+  uint64_t* akeys = vW + kWaves * KT;
+  int* grow = (int*)(akeys + KT);
+  float* gnorm = (float*)(grow + 32);
+  int* gvalid = (int*)(gnorm + 32);
+  uint64_t* xk = (uint64_t*)(gvalid + 32);
+  // MODE 1 reads its 32 gathered rows straight into registers (all loads issued at once: one latency), the
+  // exact fragments the LDS image would give: lane (r, h) takes 16-byte units 4(i>>1) + 2h + (i&1) of slab j
+  f32x4 vrow[MODE == 1 ? NS : 1][4];
+  if constexpr (MODE == 1) {
+    if (vq >= b) {   // padding slot: keep the exchange buffer uniform
+      if (a.out_keys && tid < KT) a.out_keys[(size_t)vq * KT + tid] = 0;
+      return;
+    }
+  }
+
+  // ---- this workgroup's rows (MODE 0) ------------------------------------------------------------------------
   const int64_t G = gridDim.x, g = blockIdx.x;
   const int64_t per = n / G, rem = n % G;
-  const int64_t r0 = g * per + (g < rem ? g : rem);
-  const int64_t r1 = r0 + per + (g < rem ? 1 : 0);
-  const int64_t ntile = (r1 - r0 + 31) / 32;
+  const int64_t r0 = MODE == 1 ? 0 : g * per + (g < rem ? g : rem);
+  const int64_t r1 = MODE == 1 ? 32 : r0 + per + (g < rem ? 1 : 0);
+  const int64_t ntile = MODE == 1 ? 1 : (r1 - r0 + 31) / 32;
 
   // LDS-DMA lane mapping: instruction i of a slab covers tile rows 8i + lane/8, 16-byte column
   // (lane % 8) ^ (lane / 8) of the slab — so the image holds column c of row r at c ^ (r & 7)
@@ -228,10 +297,12 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
   };
 
   const int64_t total = ntile * NS;                   // slabs this wave consumes
-  // prologue: the first RS - 1 slabs (slab p = tile p / NS, column block p % NS, slot p)
+  if constexpr (MODE == 0) {
+    // prologue: the first RS - 1 slabs (slab p = tile p / NS, column block p % NS, slot p)
 #pragma unroll
-  for (int p = 0; p < RS - 1; ++p)
-    if (p < total) issue(p / NS, p % NS, p);
+    for (int p = 0; p < RS - 1; ++p)
+      if (p < total) issue(p / NS, p % NS, p);
+  }
   // ---- query side: this wave's K-slice of every query as MFMA B operands, |q| and split exponents.
   // Runs while the prologue slabs above are in flight (their latency overlaps the query loads).
   QFrag<DT, NS> qfs[QH];
@@ -294,18 +365,27 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
 #pragma unroll
               for (int e = 0; e < 4; ++e) x[4 * u + e] = v[e];
             }
-            if constexpr (DT == 3) split3(x, qf.c0[j][t], qf.c1[j][t], qf.c2[j][t]);
-            else split2(x, qf.c0[j][t], qf.c1[j][t]);
+            if constexpr (DT == 3) {
+              split3(x, qf.c0[j][t], qf.c1[j][t], qf.c2[j][t]);
+            } else {   // DT 6: q = c0 + c1 in f16 (RNE), residual exact in fp32
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const _Float16 c0 = (_Float16)x[e];
+                qf.c0[j][t][e] = c0;
+                qf.c1[j][t][e] = (_Float16)(x[e] - (float)c0);
+              }
+            }
           }
         }
       }
     }
   };
   if constexpr (DT != 2) build_frags();
-  // ---- per-query scalars: |q| (cosine, fp32 as cp.linalg.norm, retriever.py:602) and split exponents.
-  // All loads of a group of 4 queries are issued before any is used (one L2/HBM latency per group, not
-  // one per query); the sums are the same lane-strided fmaf chains + xor tree in the same order.
-  if (COS || DT == 2) {
+  // ---- per-query scalars: |q| (cosine, fp32 as cp.linalg.norm, retriever.py:602), split exponents (DT 2),
+  // sum |q| (DT 6 bound), max |q| (MODE 1: the screen's f16 range). All loads of a group of 4 queries are
+  // issued before any is used (one L2/HBM latency per group, not one per query); the sums are the same
+  // lane-strided fmaf chains + xor tree in the same order.
+  if (COS || DT == 2 || DT == 6 || MODE == 1) {
     const int nc = d >> 2;                      // float4 per row (d <= 1024 on this kernel: <= 4 per lane)
 #pragma unroll
     for (int g4 = 0; g4 < QH; ++g4) {
@@ -323,26 +403,28 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
 #pragma unroll
       for (int qi = 0; qi < 4; ++qi) {
         const int q = w * 4 * QH + 4 * g4 + qi;
-        float ss = 0.f, m = 0.f;
+        float ss = 0.f, m = 0.f, sa = 0.f;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           if (lane + 64 * c < nc) {
             const f32x4 x = v[qi][c];
             ss = fmaf(x.x, x.x, ss); ss = fmaf(x.y, x.y, ss); ss = fmaf(x.z, x.z, ss); ss = fmaf(x.w, x.w, ss);
             m = fmaxf(m, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+            if constexpr (DT == 6) sa += (fabsf(x.x) + fabsf(x.y)) + (fabsf(x.z) + fabsf(x.w));
           }
         }
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
           ss += __shfl_xor(ss, off, 64);
           m = fmaxf(m, __shfl_xor(m, off, 64));
+          if constexpr (DT == 6) sa += __shfl_xor(sa, off, 64);
         }
         int E = 0;
         if (m > 0.f) frexpf(m, &E);
         const int ex = m > 0.f ? 15 - E : 0;
         if (lane == 0) {
           qinfo[q] = sqrtf(ss);
-          qinfo[QS + q] = ldexpf(1.0f, -ex);
+          qinfo[QS + q] = DT == 2 ? ldexpf(1.0f, -ex) : DT == 6 ? sa * (1.0f + 0x1p-20f) : m;
           qexp[q] = ex;
         }
       }
@@ -352,13 +434,40 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
 
   if constexpr (DT == 2) build_frags();
 
+  // ---- MODE 1: this query's candidates (the queries' fragments and scalars above are already built, so
+  // their loads overlapped the list loads), then their rows straight into registers ---------------------------
+  if constexpr (MODE == 1) {
+    SK_PROBE(6);
+    merge_lists_for_query<KT>(a.vin, a.nlists, QS, vq, vW, akeys);
+    SK_PROBE(7);
+    if (tid < 32) {
+      const uint64_t k0 = akeys[0];
+      const uint64_t key = tid < KT ? akeys[tid] : 0;
+      const int64_t first = k0 ? (int64_t)(0xFFFFFFFFu - (uint32_t)k0) - idx_base : 0;
+      const int64_t row = key ? (int64_t)(0xFFFFFFFFu - (uint32_t)key) - idx_base : first;
+      grow[tid] = (int)row;
+      gvalid[tid] = key != 0;
+      gnorm[tid] = COS ? norms[row] : 0.f;
+    }
+    __syncthreads();
+    SK_PROBE(3);
+    const char* src = corpus + (int64_t)grow[r] * row_bytes + (size_t)w * KS;
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        vrow[j][i] = *(const f32x4*)(src + j * kSlabRowBytes + ((4 * (i >> 1) + 2 * h + (i & 1)) << 4));
+  }
+
+
   // epilogue lane mapping: wave w owns queries 4·QH·w + [0, 4·QH); LPQ lanes per query, each with DPL
   // consecutive tile rows (QH 1: 16 lanes x 2 rows, QH 2: 8 lanes x 4 rows)
   constexpr int LPQ = 16 / QH, DPL = 2 * QH;
   const int qe = 4 * QH * w + lane / LPQ, er = DPL * (lane % LPQ);
-  const bool qev = qe < b;
-  const float qn = COS ? qinfo[qe] : 0.f;
+  const bool qev = MODE == 1 ? qe == vq : qe < b;
+  const float qn = COS || DT == 6 ? qinfo[qe] : 0.f;
   const float qs = DT == 2 ? qinfo[QS + qe] : 1.f;
+  const float qsa = DT == 6 ? qinfo[QS + qe] : 0.f;
 
   TopK<KT> tk;
   tk.init();
@@ -380,7 +489,9 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
       const int64_t tn = tile + jn / NS;
       int nslot = slot + RS - 1;
       nslot -= nslot >= RS ? RS : 0;
-      if (tn < ntile) {
+      if constexpr (MODE == 1) {
+        // registers: hipcc waits for its own loads
+      } else if (tn < ntile) {
         issue(tn, jn % NS, nslot);
         wait_vm<4 * (RS - 1)>();
       } else if (RS == 3 && tile * NS + j + 2 == total) {   // tail: one younger slab still in flight
@@ -390,20 +501,20 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
       }
       const char* sl = ring + slot * kSlabBytes;
       if constexpr (DT == 0) {
-        f32x4 a[4];
+        f32x4 av[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a[i] = *(const f32x4*)(sl + slab_off(r, 4 * h + i));
+        for (int i = 0; i < 4; ++i) av[i] = *(const f32x4*)(sl + slab_off(r, 4 * h + i));
 #pragma unroll
         for (int m = 0; m < 16; ++m)
-          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m >> 2][m & 3], qfs[qh].v[j][m], accs[qh], 0, 0, 0);
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m >> 2][m & 3], qfs[qh].v[j][m], accs[qh], 0, 0, 0);
       } else if constexpr (DT == 1) {
-        bf16x8 a[4];
+        bf16x8 av[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) a[t] = *(const bf16x8*)(sl + slab_off(r, 2 * t + h));
+        for (int t = 0; t < 4; ++t) av[t] = *(const bf16x8*)(sl + slab_off(r, 2 * t + h));
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], qfs[qh].hi[j][t], accs[qh], 0, 0, 0);
-          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], qfs[qh].lo[j][t], accs[qh], 0, 0, 0);
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[t], qfs[qh].hi[j][t], accs[qh], 0, 0, 0);
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[t], qfs[qh].lo[j][t], accs[qh], 0, 0, 0);
         }
       } else if constexpr (DT == 2) {
         f16x8 ah[2], al[2];
@@ -419,32 +530,29 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
           for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[t], qfs[qh].hi[j][t], accs[qh], 0, 0, 0);
         }
       } else {
-        f32x4 a[4];
+        f32x4 av[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a[i] = *(const f32x4*)(sl + slab_off(r, 4 * (i >> 1) + 2 * h + (i & 1)));
+        for (int i = 0; i < 4; ++i)
+          av[i] = MODE == 1 ? vrow[MODE == 1 ? j : 0][i] : *(const f32x4*)(sl + slab_off(r, 4 * (i >> 1) + 2 * h + (i & 1)));
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const float x[8] = {a[2 * t].x, a[2 * t].y, a[2 * t].z, a[2 * t].w,
-                              a[2 * t + 1].x, a[2 * t + 1].y, a[2 * t + 1].z, a[2 * t + 1].w};
-          if constexpr (DT == 4) {
-            bf16x8 b0, b1;
-            split2(x, b0, b1);
+          const float x[8] = {av[2 * t].x, av[2 * t].y, av[2 * t].z, av[2 * t].w,
+                              av[2 * t + 1].x, av[2 * t + 1].y, av[2 * t + 1].z, av[2 * t + 1].w};
+          if constexpr (DT == 3) {
+            bf16x8 b0, b1, b2;
+            split3(x, b0, b1, b2);
             for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
             for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c1[j][t], accs[qh], 0, 0, 0);
             for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
-          } else if constexpr (DT == 5) {
-            const bf16x8 b0 = split1(x);
-            for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
-            for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c1[j][t], accs[qh], 0, 0, 0);
-          } else {
-          bf16x8 b0, b1, b2;
-          split3(x, b0, b1, b2);
-          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
-          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c1[j][t], accs[qh], 0, 0, 0);
-          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
-          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qfs[qh].c1[j][t], accs[qh], 0, 0, 0);
-          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c2[j][t], accs[qh], 0, 0, 0);
-          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
+            for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qfs[qh].c1[j][t], accs[qh], 0, 0, 0);
+            for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[qh].c2[j][t], accs[qh], 0, 0, 0);
+            for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
+          } else {   // DT 6: x rounded to f16 (RNE), two f16 MFMAs
+            f16x8 hx;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) hx[e] = (_Float16)x[e];
+            for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(hx, qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
+            for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(hx, qfs[qh].c1[j][t], accs[qh], 0, 0, 0);
           }
         }
       }
@@ -465,7 +573,7 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
       }
     lds_barrier();
     const int64_t tb = r0 + tile * 32;
-    if constexpr (SW > 0) {
+    if constexpr (SW > 0 && MODE == 0) {
       if (tb < seg_lo || tb + 32 > seg_lo + kSegRows) {   // workgroup-uniform: refill the per-doc factors
         seg_lo = tb;
         for (int i = tid; i < kSegRows; i += kThreads) {
@@ -474,7 +582,7 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
           if constexpr (COS && DT == 2) {
             seg[2 * i] = norms[row];
             seg[2 * i + 1] = rscale[row];
-          } else if constexpr (COS) {
+          } else if constexpr (COS || DT == 6) {
             seg[i] = norms[row];
           } else {
             seg[i] = rscale[row];
@@ -504,7 +612,7 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
     // few that pass pay the exact IEEE division (the list only grows inside the loop: the threshold
     // taken here is conservative).
     float thr = -INFINITY;
-    if constexpr (COS) {
+    if constexpr (COS && DT != 6) {
       const uint64_t last = tk.last();
       if (last != 0) {
         const float t = float_of_ord((uint32_t)(last >> 32));
@@ -513,14 +621,39 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
     }
 #pragma unroll
     for (int e = 0; e < DPL; ++e) {
-      const int64_t row = tb + er + e;
+      int64_t row;
+      bool valid;
+      float nd = 1.f;
       float s = sv[e];
-      const int64_t li = row - seg_lo;
-      if constexpr (DT == 2) s = s * (COS ? seg[2 * li + 1] : seg[li]) * qs;   // exact 2^e rescales
-      const bool valid = qev && row < r1;
-      if constexpr (COS) {
+      if constexpr (MODE == 1) {
+        row = grow[er + e];
+        valid = qev && gvalid[er + e];
+        if constexpr (COS) nd = gnorm[er + e];
+      } else {
+        row = tb + er + e;
+        const int64_t li = row - seg_lo;
+        valid = qev && row < r1;
+        if constexpr (DT == 2) s = s * (COS ? seg[2 * li + 1] : seg[li]) * qs;   // exact 2^e rescales
+        if constexpr (COS || DT == 6) nd = DT == 2 ? seg[2 * li] : seg[li];
+      }
+      if constexpr (DT == 6) {
+        // upper bound of the exact (DT 3) score, see "Screened search"; the relative bumps cover the
+        // roundings of the bound's own arithmetic and of the reciprocal (<= 1 ulp)
+        const float eps = fmaf(a.eps_a * nd, qn, a.eps_b * fmaf(a.sqrt_d, nd, qsa));
+        float v = s + eps;
+        v += fabsf(v) * 0x1p-22f;
+        float u;
+        if constexpr (COS) {
+          u = v * __builtin_amdgcn_rcpf(cos_den(qn, nd));
+          u += fabsf(u) * 0x1p-20f + 0x1p-126f;
+          u = fminf(fmaxf(u, -1.0f), 1.0f);   // the exact score is clipped to [-1, 1] (retriever.py:609)
+        } else {
+          u = v;
+        }
+        const uint64_t key = make_key(u, idx_base + (uint32_t)row);
+        if (valid && key > tk.last()) tk.insert(key);
+      } else if constexpr (COS) {
         // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
-        const float nd = DT == 2 ? seg[2 * li] : seg[li];
         const float den = cos_den(qn, nd);
         if (valid && s * __builtin_amdgcn_rcpf(den) >= thr) {
           float c = s / den;   // IEEE division, as the reference's elementwise kernel
@@ -534,78 +667,103 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const char* __restrict
       }
     }
     if (tile == 0) SK_PROBE(2);
-    if (tile == 1) SK_PROBE(3);
+    if (MODE == 0 && tile == 1) SK_PROBE(3);
   }
   SK_PROBE(4);
 
   // ---- per query: merge its LPQ lane lists (KT rounds of an LPQ-lane max; keys are unique) -------------
-  uint64_t* dst = out + ((size_t)g * QS + qe) * KT;
+  if constexpr (MODE == 0) {
+    uint64_t* dst = a.out + ((size_t)g * QS + qe) * KT;
 #pragma unroll 1
-  for (int rnd = 0; rnd < KT; ++rnd) {
-    uint64_t m = tk.v[0];
-#pragma unroll
-    for (int off = LPQ / 2; off >= 1; off >>= 1) {
-      const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)m, off, 64);
-      const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(m >> 32), off, 64);
-      m = umax64(m, ((uint64_t)hi << 32) | lo);
+    for (int rnd = 0; rnd < KT; ++rnd) {
+      const uint64_t m = group_max_u64<LPQ>(tk.v[0]);
+      if (m != 0 && tk.v[0] == m) tk.pop();
+      if (lane % LPQ == 0) dst[rnd] = m;
     }
-    if (m != 0 && tk.v[0] == m) tk.pop();
-    if (lane % LPQ == 0) dst[rnd] = m;
+  } else {
+    if (w != vq / 4) return;   // the wave that owns query slot vq (QH 1: queries 4w..4w+3)
+#pragma unroll 1
+    for (int rnd = 0; rnd < KT; ++rnd) {
+      const uint64_t m = group_max_u64<LPQ>(tk.v[0]);
+      if (m != 0 && tk.v[0] == m) tk.pop();
+      if (qe == vq && lane % LPQ == 0) xk[rnd] = m;
+    }
+    if (qe != vq || lane % LPQ != 0) return;
+    // leader of query slot vq: completeness, then the results
+    const uint64_t ukt = akeys[KT - 1];          // the KT-th upper bound (0: fewer than KT docs here)
+    const uint64_t ek = xk[a.k_out - 1];         // the exact k-th key
+    bool complete = ukt == 0 || (ek != 0 && (uint32_t)(ek >> 32) > (uint32_t)(ukt >> 32));
+    complete = complete && qinfo[QS + vq] < 32768.0f && !a.force_incomplete;   // f16 range of the screen
+    if (!complete) {   // the first query slot to flag the block also counts it
+      if (__hip_atomic_fetch_max(a.flag, (uint64_t)a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+          (uint64_t)a.seq)
+        __hip_atomic_fetch_add(a.count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (a.out_keys)
+      for (int i = 0; i < KT; ++i) a.out_keys[(size_t)vq * KT + i] = xk[i];
+    if (a.out_scores)
+      for (int i = 0; i < a.k_out; ++i) {
+        const uint64_t key = xk[i];
+        a.out_scores[(size_t)vq * a.k_out + i] = key ? float_of_ord((uint32_t)(key >> 32)) : -INFINITY;
+        a.out_idx[(size_t)vq * a.k_out + i] = key ? (int64_t)(0xFFFFFFFFu - (uint32_t)key) : -1;
+      }
   }
   SK_PROBE(5);
 }
 
-template <int DT, int NS, int KT, bool COS, int RS, int QH>
-hipError_t launch_t(int grid, const void* c, const float* nr, const float* rs, const float* q, int64_t n, int d,
-                    int b, uint32_t base, uint64_t* out, hipStream_t s) {
-  auto kern = sk_score_kernel<DT, NS, KT, COS, RS, QH>;
+template <int DT, int NS, int KT, bool COS, int RS, int QH, int MODE>
+hipError_t launch_t(int grid, const SkArgs& a, hipStream_t s) {
+  auto kern = sk_score_kernel<DT, NS, KT, COS, RS, QH, MODE>;
+  static bool attr_set = false;   // the dynamic-LDS ceiling is a per-function attribute: set it once
   const size_t lds = sk_lds_bytes(DT, COS, RS, 32 * QH);
-  if (hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds))
-    return e;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, (const char*)c, nr, rs, q, n, d, b, base, out);
+  if (!attr_set) {
+    if (hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds))
+      return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, a);
   return hipGetLastError();
 }
 
-template <int DT, int NS, bool COS, int RS, int QH>
-hipError_t launch_kt(int kt, int grid, const void* c, const float* nr, const float* rs, const float* q, int64_t n,
-                     int d, int b, uint32_t base, uint64_t* out, hipStream_t s) {
+template <int DT, int NS, bool COS, int RS, int QH, int MODE>
+hipError_t launch_kt(int kt, int grid, const SkArgs& a, hipStream_t s) {
   switch (kt) {
-    case 4: return launch_t<DT, NS, 4, COS, RS, QH>(grid, c, nr, rs, q, n, d, b, base, out, s);
-    case 8: return launch_t<DT, NS, 8, COS, RS, QH>(grid, c, nr, rs, q, n, d, b, base, out, s);
-    case 16: return launch_t<DT, NS, 16, COS, RS, QH>(grid, c, nr, rs, q, n, d, b, base, out, s);
-    case 32: if constexpr (QH == 1) return launch_t<DT, NS, 32, COS, RS, QH>(grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 4: return launch_t<DT, NS, 4, COS, RS, QH, MODE>(grid, a, s);
+    case 8: return launch_t<DT, NS, 8, COS, RS, QH, MODE>(grid, a, s);
+    case 16: return launch_t<DT, NS, 16, COS, RS, QH, MODE>(grid, a, s);
+    case 32: if constexpr (QH == 1) return launch_t<DT, NS, 32, COS, RS, QH, MODE>(grid, a, s);
              else return hipErrorInvalidValue;   // 64 slots x KT 32 spills: served as two 32-slot passes
     default: return hipErrorInvalidValue;
   }
 }
 
-template <int DT, bool COS, int RS, int QH>
-hipError_t launch_ns(int ns, int kt, int grid, const void* c, const float* nr, const float* rs, const float* q,
-                     int64_t n, int d, int b, uint32_t base, uint64_t* out, hipStream_t s) {
+template <int DT, bool COS, int RS, int QH, int MODE>
+hipError_t launch_ns(int ns, int kt, int grid, const SkArgs& a, hipStream_t s) {
   switch (ns) {
-    case 1: return launch_kt<DT, 1, COS, RS, QH>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
-    case 2: return launch_kt<DT, 2, COS, RS, QH>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
-    case 3: if constexpr (DT != 1) return launch_kt<DT, 3, COS, RS, QH>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 1: return launch_kt<DT, 1, COS, RS, QH, MODE>(kt, grid, a, s);
+    case 2: return launch_kt<DT, 2, COS, RS, QH, MODE>(kt, grid, a, s);
+    case 3: if constexpr (DT != 1) return launch_kt<DT, 3, COS, RS, QH, MODE>(kt, grid, a, s);
             else return hipErrorInvalidValue;
-    case 4: if constexpr (DT != 1) return launch_kt<DT, 4, COS, RS, QH>(kt, grid, c, nr, rs, q, n, d, b, base, out, s);
+    case 4: if constexpr (DT != 1) return launch_kt<DT, 4, COS, RS, QH, MODE>(kt, grid, a, s);
             else return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }
 
-template <int DT, int RS, int QH>
-hipError_t launch_metric(int metric, int ns, int kt, int grid, const void* c, const float* nr, const float* rs,
-                         const float* q, int64_t n, int d, int b, uint32_t base, uint64_t* out, hipStream_t s) {
-  return metric ? launch_ns<DT, true, RS, QH>(ns, kt, grid, c, nr, rs, q, n, d, b, base, out, s)
-                : launch_ns<DT, false, RS, QH>(ns, kt, grid, c, nr, rs, q, n, d, b, base, out, s);
+template <int DT, int RS, int QH, int MODE = 0>
+hipError_t launch_metric(int metric, int ns, int kt, int grid, const SkArgs& a, hipStream_t s) {
+  return metric ? launch_ns<DT, true, RS, QH, MODE>(ns, kt, grid, a, s)
+                : launch_ns<DT, false, RS, QH, MODE>(ns, kt, grid, a, s);
 }
 
 }  // namespace sk
 
 size_t sk_lds_bytes(int sdt, bool cos, int ring, int qslots) {
-  const int sw = (cos ? 1 : 0) + (sdt == 2 ? 1 : 0);
+  const int sw = (cos || sdt == 6 ? 1 : 0) + (sdt == 2 ? 1 : 0);
+  // + MODE 1 scratch: W [8][32] + akeys [32] keys, grow / gnorm / gvalid [32], xk [32] keys
+  const size_t verify = (size_t)(kWaves * 32 + 32 + 32) * 8 + 3 * 32 * 4;
   return sk::ring_bytes(ring) + sk::red_bytes(ring, qslots / 32) + (size_t)sk::kSegRows * (sw > 0 ? sw : 1) * 4 +
-         3 * qslots * 4;
+         3 * qslots * 4 + verify;
 }
 
 bool sk_supports_64(int sdt) { return sdt == KDT_BF16 || sdt == KDT_F32_SPLIT; }
@@ -617,44 +775,63 @@ int sk_slabs(int sdt, int d) {
   return (ns >= 1 && ns <= (sdt == 1 ? 2 : 4)) ? ns : 0;
 }
 
-hipError_t launch_sk(int sdt, int metric, int kt, int grid, const void* c, const float* nr, const float* rs,
-                     const float* q, int64_t n, int d, int b, uint32_t base, uint64_t* cand, hipStream_t s, int ring,
-                     int qslots) {
-  const int ns = sk_slabs(sdt, d);
-  if (!ns || b < 1 || b > qslots || n < 1 || (qslots != 32 && qslots != 64)) return hipErrorInvalidValue;
+hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int qslots, const SkArgs& a,
+                          hipStream_t s, int ring) {
+  const int ns = sk_slabs(sdt == KDT_SCREEN ? KDT_F32_X3 : sdt, a.d);
+  if (!ns || a.b < 1 || a.b > qslots || a.n < 1 || (qslots != 32 && qslots != 64)) return hipErrorInvalidValue;
   if (ring == 0) ring = kSkRing;
+  if (mode == 1) {   // verify: exact fp32 arithmetic, 32 slots, one workgroup per query slot
+    if (sdt != KDT_F32_X3 || qslots != 32 || ring != 2 || grid != 32) return hipErrorInvalidValue;
+    return sk::launch_metric<3, 2, 1, 1>(metric, ns, kt, grid, a, s);
+  }
+  if (sdt == KDT_SCREEN) {
+    if (qslots != 32 || ring != 2) return hipErrorInvalidValue;
+    return sk::launch_metric<6, 2, 1>(metric, ns, kt, grid, a, s);
+  }
   if (qslots == 64) {   // one corpus pass for up to 64 queries: bf16 and fp32-split storage, ring 2
     if (ring != 2) return hipErrorInvalidValue;
     switch (sdt) {
-      case 1: return sk::launch_metric<1, 2, 2>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-      case 2: return sk::launch_metric<2, 2, 2>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      case 1: return sk::launch_metric<1, 2, 2>(metric, ns, kt, grid, a, s);
+      case 2: return sk::launch_metric<2, 2, 2>(metric, ns, kt, grid, a, s);
       default: return hipErrorInvalidValue;
     }
   }
   if (ring == 2) {
     switch (sdt) {
-      case 0: return sk::launch_metric<0, 2, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-      case 1: return sk::launch_metric<1, 2, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-      case 2: return sk::launch_metric<2, 2, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-      case 3: return sk::launch_metric<3, 2, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-#ifdef RR_SK_SCREEN_PROBE
-      case 4: return sk::launch_metric<4, 2, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-      case 5: return sk::launch_metric<5, 2, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-#endif
+      case 0: return sk::launch_metric<0, 2, 1>(metric, ns, kt, grid, a, s);
+      case 1: return sk::launch_metric<1, 2, 1>(metric, ns, kt, grid, a, s);
+      case 2: return sk::launch_metric<2, 2, 1>(metric, ns, kt, grid, a, s);
+      case 3: return sk::launch_metric<3, 2, 1>(metric, ns, kt, grid, a, s);
       default: return hipErrorInvalidValue;
     }
   }
 #ifdef RR_SK_RING3   // A/B builds only (tools/kbench.hip): measured no faster, see kSkRing
   if (ring == 3) {   // (the f32-MFMA form DT 0 is a kbench reference only: ring 2)
     switch (sdt) {
-      case 1: return sk::launch_metric<1, 3, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-      case 2: return sk::launch_metric<2, 3, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
-      case 3: return sk::launch_metric<3, 3, 1>(metric, ns, kt, grid, c, nr, rs, q, n, d, b, base, cand, s);
+      case 1: return sk::launch_metric<1, 3, 1>(metric, ns, kt, grid, a, s);
+      case 2: return sk::launch_metric<2, 3, 1>(metric, ns, kt, grid, a, s);
+      case 3: return sk::launch_metric<3, 3, 1>(metric, ns, kt, grid, a, s);
       default: return hipErrorInvalidValue;
     }
   }
 #endif
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_sk(int sdt, int metric, int kt, int grid, const void* c, const float* nr, const float* rs,
+                     const float* q, int64_t n, int d, int b, uint32_t base, uint64_t* cand, hipStream_t s, int ring,
+                     int qslots) {
+  SkArgs a{};
+  a.corpus = (const char*)c;
+  a.norms = nr;
+  a.rscale = rs;
+  a.queries = q;
+  a.n = n;
+  a.d = d;
+  a.b = b;
+  a.idx_base = base;
+  a.out = cand;
+  return launch_sk_args(sdt, metric, kt, 0, grid, qslots, a, s, ring);
 }
 
 }  // namespace rr

@@ -38,6 +38,8 @@ RR_UNIQUE_ID_BYTES = 128
 RR_FUSED_KMAX = 32
 RR_KERNEL_AUTO = 0
 RR_KERNEL_FUSED = 1
+RR_KERNEL_EXACT = 2
+RR_KERNEL_SCREEN_FALLBACK = 3
 RR_ABI_VERSION = 2
 
 DTYPES = {"fp32": RR_DTYPE_F32, "float32": RR_DTYPE_F32, "f32": RR_DTYPE_F32,
@@ -71,6 +73,7 @@ SIGNATURES = {
     "rr_kernel_time": (_c_int, [_vp, ctypes.POINTER(ctypes.c_double), _i64p, _c_int]),
     "rr_search_async": (_c_int, [_vp, _fp, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_i32)]),
     "rr_wait": (_c_int, [_vp, _c_i32, _fp, _i64p]),
+    "rr_screen_stats": (_c_int, [_vp, _i64p, _i64p]),
     "rr_last_shape": (_c_int, [_vp, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32)]),
     "rr_dist_info": (_c_int, [_vp, _ip, _ip]),
 }
@@ -288,9 +291,20 @@ class Index:
         _check(self._lib.rr_fetch_results(self._h, _fptr(scores), _i64ptr(idx)))
         return scores, idx
 
+    KERNELS = {"auto": RR_KERNEL_AUTO, "fused": RR_KERNEL_FUSED, "exact": RR_KERNEL_EXACT,
+               "screen-fallback": RR_KERNEL_SCREEN_FALLBACK}
+
     def set_kernel(self, kernel: str) -> None:
-        """'auto' (split-K LDS-DMA kernel where the shape allows) or 'fused' (register-streaming kernel)."""
-        _check(self._lib.rr_set_kernel(self._h, {"auto": RR_KERNEL_AUTO, "fused": RR_KERNEL_FUSED}[kernel]))
+        """'auto' (split-K LDS-DMA kernel where the shape allows; fp32 storage: the screened search),
+        'exact' (split-K, fp32 scored exactly in one pass), 'fused' (register-streaming kernel) or
+        'screen-fallback' (test hook: the screened search's exact fallback pass always runs)."""
+        _check(self._lib.rr_set_kernel(self._h, self.KERNELS[kernel]))
+
+    def screen_stats(self) -> Tuple[int, int]:
+        """(screened search blocks, blocks that needed the exact fallback pass)."""
+        b, f = _c_i64(), _c_i64()
+        _check(self._lib.rr_screen_stats(self._h, ctypes.byref(b), ctypes.byref(f)))
+        return b.value, f.value
 
     def set_timing(self, enable: bool) -> None:
         _check(self._lib.rr_set_timing(self._h, 1 if enable else 0))

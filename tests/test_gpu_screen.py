@@ -1,0 +1,163 @@
+"""The screened search (fp32 storage, rr_sk.hip "Screened search"): an f16 screening pass of upper bounds,
+exact rescoring of the KT candidates with the DT 3 arithmetic, and an exact fallback pass when the bound cannot
+prove completeness. Its results must be BIT-IDENTICAL to the one-pass exact kernel (RR_KERNEL_EXACT) in every
+case — screened, forced fallback, shards, cosine and dot — and match the oracle."""
+import numpy as np
+import pytest
+
+from oracle import synth
+from oracle.retriever_oracle import canonical_topk, exact_scores
+from parity_helpers import check_topk
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def Index(hip):
+    from rag_service_amd import Index as _Index
+    return _Index
+
+
+CASES = [  # (n, d, b, k)
+    (1, 256, 1, 1), (5, 256, 3, 5), (40, 1024, 32, 29), (1000, 512, 32, 8), (4099, 1024, 32, 5),
+    (12345, 1024, 20, 16), (2049, 768, 7, 2), (70000, 1024, 32, 10), (33, 256, 45, 3),
+]
+
+
+@pytest.mark.parametrize("n,d,b,k", CASES)
+@pytest.mark.parametrize("metric", ["cosine", "dot"])
+def test_screened_equals_exact(Index, n, d, b, k, metric):
+    rng = np.random.default_rng(n + d + b + k)
+    corpus = rng.standard_normal((n, d)).astype(np.float32) * rng.uniform(0.5, 2, size=(n, 1)).astype(np.float32)
+    q = rng.standard_normal((b, d)).astype(np.float32)
+    ix = Index(dtype="fp32", metric=metric)
+    ix.load(corpus)
+    got = ix.search(q, k)
+    blocks, fallbacks = ix.screen_stats()
+    assert blocks == -(-b // 32)
+    ix.set_kernel("exact")
+    want = ix.search(q, k)
+    ix.set_kernel("screen-fallback")
+    forced = ix.search(q, k)
+    assert ix.screen_stats()[1] == fallbacks + blocks          # every forced block took the exact pass
+    for s, i in (got, forced):
+        assert np.array_equal(i, want[1]) and np.array_equal(s, want[0])
+    _, cidx = canonical_topk(exact_scores(corpus, q, metric), k)
+    tol = 1e-3 * (np.sqrt(d) if metric == "dot" else 1.0)
+    check_topk(got[1], got[0], cidx, corpus, q, metric, near_tie=1e-5 * np.sqrt(d), score_tol=tol)
+    ix.close()
+
+
+def test_screen_rarely_falls_back_on_unit_norm_data(Index):
+    """The headline's data (unit-norm rows): with a list of 2k + 2 the bound proves completeness for every
+    block (at k near the list width, 29 of 32, a block may need the exact pass; the results are exact
+    either way)."""
+    corpus = synth.unit_norm_gaussian(1234, 65536, 1024)
+    q = synth.unit_norm_gaussian(5678, 32, 1024)
+    ix = Index(dtype="fp32", metric="cosine")
+    ix.load(corpus)
+    for k in (1, 5, 10, 15):
+        ix.search(q, k)
+    assert ix.screen_stats() == (4, 0)
+    ix.set_kernel("exact")
+    want = ix.search(q, 29)
+    ix.set_kernel("auto")
+    got = ix.search(q, 29)
+    assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
+    ix.close()
+
+
+def test_screen_ties_take_the_exact_pass(Index):
+    """40 copies of one row spread over the corpus, queried with that row: 40 exactly tied top scores, more
+    than the screen's candidate list holds, so the bound cannot prove completeness and the search is re-run
+    exactly; the result is the canonical order (equal scores by ascending index), bit-identical to the
+    one-pass exact kernel, for cosine and dot."""
+    corpus = synth.unit_norm_gaussian(77, 65536, 1024)
+    dup = np.arange(40) * 1601 + 7
+    corpus[dup] = corpus[123]
+    q = np.concatenate([corpus[123:124], synth.unit_norm_gaussian(78, 31, 1024)])
+    for metric in ("cosine", "dot"):
+        ix = Index(dtype="fp32", metric=metric)
+        ix.load(corpus)
+        got = ix.search(q, 5)
+        assert ix.screen_stats() == (1, 1)
+        assert sorted(got[1][0]) == sorted(np.sort(np.append(dup, 123))[:5])
+        ix.set_kernel("exact")
+        want = ix.search(q, 5)
+        assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
+        val, cidx = canonical_topk(exact_scores(corpus, q, metric), 5)
+        assert np.array_equal(got[1], cidx)
+        ix.close()
+
+
+def test_screen_guards_f16_range(Index):
+    """Values the screen's f16 reading cannot hold: a corpus element >= 2^15 turns screening off for the
+    handle; a query element >= 2^15 makes its block take the exact pass. Both still give exact results."""
+    rng = np.random.default_rng(9)
+    corpus = rng.standard_normal((3000, 256)).astype(np.float32)
+    q = rng.standard_normal((8, 256)).astype(np.float32)
+    q[3, 17] = 40000.0
+    ix = Index(dtype="fp32", metric="dot")
+    ix.load(corpus)
+    got = ix.search(q, 6)
+    assert ix.screen_stats() == (1, 1)
+    ix.set_kernel("exact")
+    want = ix.search(q, 6)
+    assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
+    big = corpus.copy()
+    big[5, 3] = 1e5
+    ix.set_kernel("auto")
+    ix.load(big)
+    ix.search(q[:2], 4)
+    assert ix.screen_stats() == (0, 0)                          # counters restart at the load; nothing screened
+    ix.close()
+
+
+@pytest.mark.parametrize("shards", [2, 8])
+def test_screened_sharded_equals_single(Index, shards):
+    """Shards screen and verify independently (each with its own fallback decision) before the exchange:
+    results equal the one-shard exact ones, for the pipelined (staged) loop too."""
+    rng = np.random.default_rng(shards)
+    corpus = rng.standard_normal((20011, 1024)).astype(np.float32)
+    corpus /= np.linalg.norm(corpus, axis=1, keepdims=True)
+    q = rng.standard_normal((45, 1024)).astype(np.float32)
+    one = Index(devices=[0], dtype="fp32", metric="cosine")
+    one.load(corpus)
+    one.set_kernel("exact")
+    many = Index(devices=[0] * shards, dtype="fp32", metric="cosine")
+    many.load(corpus)
+    for k in (5, 10, 29, 40):
+        want = one.search(q, k)
+        got = many.search(q, k)
+        assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), k
+    many.set_queries(q)
+    for _ in range(5):
+        many.search_staged(5)
+    s, i = many.fetch()
+    want = one.search(q, 5)
+    assert np.array_equal(i, want[1]) and np.array_equal(s, want[0])
+    many.set_kernel("screen-fallback")
+    got = many.search(q, 7)
+    want = one.search(q, 7)
+    assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
+    one.close()
+    many.close()
+
+
+def test_screened_rccl_one_rank(Index):
+    from rag_service_amd import get_unique_id
+    rng = np.random.default_rng(12)
+    corpus = rng.standard_normal((9000, 512)).astype(np.float32)
+    q = rng.standard_normal((32, 512)).astype(np.float32)
+    ref = Index(dtype="fp32", metric="cosine")
+    ref.load(corpus)
+    ref.set_kernel("exact")
+    rc = Index(dtype="fp32", metric="cosine")
+    rc.init_dist(1, 0, get_unique_id())
+    rc.load(corpus)
+    for k in (3, 12):
+        want = ref.search(q, k)
+        got = rc.search(q, k)
+        assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), k
+    ref.close()
+    rc.close()

@@ -1,0 +1,83 @@
+// verify_probe.hip — per-phase timestamps of the screened search's verify kernel (development probe).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DRR_SK_PROBE -I include -I rag-serving-system_amd/csrc \
+//         tools/verify_probe.hip -o tools/verify_probe && tools/verify_probe [n_docs]
+#include "../rag-serving-system_amd/csrc/rr_kernels.hip"
+#include "../rag-serving-system_amd/csrc/rr_sk.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                                     \
+  do {                                                                                            \
+    hipError_t e_ = (x);                                                                          \
+    if (e_ != hipSuccess) {                                                                       \
+      fprintf(stderr, "%s failed: %s (line %d)\n", #x, hipGetErrorString(e_), __LINE__);          \
+      exit(2);                                                                                    \
+    }                                                                                             \
+  } while (0)
+
+using namespace rr;
+
+int main(int argc, char** argv) {
+  const int64_t n = argc > 1 ? atoll(argv[1]) : 1000000;
+  const int d = 1024, b = 32, k = 5, kt = 16;
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  float *tmp, *c32, *norms, *q, *osc;
+  int64_t* oix;
+  uint64_t *cand, *flag;
+  int* count;
+  CK(hipMalloc(&tmp, (size_t)n * d * 4));
+  CK(hipMalloc(&c32, (size_t)n * d * 4));
+  CK(hipMalloc(&norms, (size_t)(n + 64) * 4));
+  CK(hipMalloc(&q, (size_t)b * d * 4));
+  CK(hipMalloc(&osc, b * k * 4));
+  CK(hipMalloc(&oix, b * k * 8));
+  CK(hipMalloc(&cand, (size_t)cus * 32 * 32 * 8));
+  CK(hipMalloc(&flag, 64));
+  CK(hipMalloc(&count, 64));
+  CK(hipMemset(flag, 0, 64));
+  CK(launch_synth(1, 1234, 0, n, d, tmp, s));
+  CK(launch_permute_f32(tmp, c32, n, d, 0, s));
+  CK(launch_row_norms(0, c32, n, d, norms, s));
+  CK(launch_synth(1, 99, 0, b, d, q, s));
+  CK(hipStreamSynchronize(s));
+  SkArgs a{};
+  a.corpus = (const char*)c32; a.norms = norms; a.queries = q; a.n = n; a.d = d; a.b = b; a.out = cand;
+  a.eps_a = 6e-4f; a.eps_b = 4e-8f; a.sqrt_d = 32.0f;
+  SkArgs v = a;
+  v.vin = cand; v.nlists = cus; v.k_out = k; v.out_scores = osc; v.out_idx = oix; v.flag = flag; v.count = count;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<unsigned long long> h((size_t)32 * 8);
+  for (int rep = 0; rep < 6; ++rep) {
+    v.seq = rep + 1;
+    CK(launch_sk_args(KDT_SCREEN, 1, kt, 0, cus, 32, a, s));
+    CK(hipEventRecord(e0, s));
+    CK(launch_sk_args(KDT_F32_X3, 1, kt, 1, 32, 32, v, s));
+    CK(hipEventRecord(e1, s));
+    CK(hipStreamSynchronize(s));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    CK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(rr::sk::probe), h.size() * 8));
+    unsigned long long t0 = ~0ull;
+    for (int g = 0; g < 32; ++g) t0 = std::min(t0, h[g * 8]);
+    printf("{\"rep\": %d, \"verify_event_us\": %.1f", rep, ms * 1e3);
+    const int order[] = {0, 6, 7, 3, 1, 2, 4};
+    const char* nm[] = {"start", "frags_norms", "merged", "rows_known", "loop_start", "tile_done", "loop_end"};
+    for (int i = 0; i < 7; ++i) {
+      std::vector<double> x;
+      for (int g = 0; g < 32; ++g)
+        if (order[i] != 5 || g < 4) x.push_back((h[g * 8 + order[i]] - t0) / 100.0);
+      std::sort(x.begin(), x.end());
+      printf(", \"%s_us\": [%.2f, %.2f]", nm[i], x[x.size() / 2], x.back());
+    }
+    printf("}\n");
+  }
+  return 0;
+}
