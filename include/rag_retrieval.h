@@ -190,6 +190,11 @@ int rr_set_queries_device(rr_handle* h, const float* dev_q, int32_t b, int32_t d
  * differ only by fp32 summation order. */
 int rr_set_kernel(rr_handle* h, int kernel);
 
+/* Work schedule of the split-K kernels: 1 (default) = dynamic — each workgroup takes its first chunk of
+ * tiles, then the next free one from a device counter, so workgroups on faster CUs take more; 0 = static
+ * (chunks dealt round-robin). Results are identical; for A/B measurements. */
+int rr_set_schedule(rr_handle* h, int dynamic);
+
 /* Screened-search counters since the corpus was (re)loaded: search blocks screened (summed over local
  * shards) and how many of them needed the exact fallback pass. Synchronises the handle's streams. */
 int rr_screen_stats(rr_handle* h, int64_t* blocks, int64_t* fallbacks);

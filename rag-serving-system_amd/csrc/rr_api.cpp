@@ -58,11 +58,15 @@ struct Shard {
   void* corpus = nullptr;                // [rows][d] fp32 or bf16
   float* norms = nullptr;                // [round_up(rows, 32) + 32] |row| (pad = 1)
   float* rscale = nullptr;               // [same] split-f16 row scale 2^-e (pad = 1)
-  float* queries = nullptr;              // [q_cap][d] fp32
+  float* qbuf[2] = {nullptr, nullptr};   // staged queries, double-buffered ([q_cap][d] fp32 each): a new
+                                         // batch is copied into one while verifies may still read the other
+  hipEvent_t ev_qread[2] = {nullptr, nullptr};   // xstream: the last verify reading qbuf[i] has finished
+  hipEvent_t ev_scr[2] = {nullptr, nullptr};     // compute stream: the screen of parity p has written cand[p]
   int q_cap = 0;
-  uint64_t* cand = nullptr;              // [grid][32][32] fused per-workgroup candidates
-  int cand_grid = 0;
+  uint64_t* cand = nullptr;              // 2 x [grid][64][32] per-workgroup candidates (the screened search
+  int cand_grid = 0;                     // alternates the halves by parity; the other paths use half 0)
   int* scount = nullptr;                 // screened search: blocks this shard flagged for the exact pass
+  uint32_t* ctr = nullptr;               // split-K chunk counter (dynamic schedule), 0 between launches
   uint64_t* shard_keys = nullptr;        // [32][k_cap] this shard's top-k (all-gather send buffer)
   uint64_t* gathered = nullptr;          // [world][32][k_cap] (all-gather receive buffer)
   // pipelined exchange (k <= RR_FUSED_KMAX, world > 1): the exchange of search i (all-gather + final
@@ -143,6 +147,10 @@ struct rr_handle {
   int64_t screen_reruns = 0;
   bool last_screened = false;   // the last search (rr_search_staged) ran screened blocks
   int last_seq0 = 0;            // ... and its first block's sequence number
+  bool last_settled = true;     // ... and its completeness has been checked (settle_screen)
+  int last_qpar = 0;            // ... and the query buffer it read
+  int qpar = 0;                 // the staged queries live in every shard's qbuf[qpar]
+  int dyn_sched = 1;            // split-K kernels: dynamic chunk schedule (rr_set_schedule)
 };
 
 namespace {
@@ -166,6 +174,9 @@ int kdt_of(int dtype) {
   }
 }
 
+// Elements of one half of a shard's candidate buffer: [grid][64 slots][32] keys.
+size_t cand_half(const Shard& s) { return (size_t)s.cand_grid * kMaxSlots * RR_FUSED_KMAX; }
+
 void shard_range(int64_t n, int world, int g, int64_t* b, int64_t* e) {
   const int64_t per = (n + world - 1) / world;
   *b = std::min<int64_t>(n, (int64_t)g * per);
@@ -185,7 +196,7 @@ int dmalloc(T** p, size_t bytes) {
 
 int free_shard(Shard& s) {
   hipSetDevice(s.dev);
-  void* ptrs[] = {s.corpus, s.norms, s.rscale, s.queries, s.cand, s.scount, s.shard_keys, s.gathered, s.out_base,
+  void* ptrs[] = {s.corpus, s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.ctr, s.shard_keys, s.gathered, s.out_base,
                   s.full_keys, s.sorted, s.sort_temp, s.px_keys[0], s.px_keys[1], s.px_gathered[0], s.px_gathered[1]};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -194,7 +205,8 @@ int free_shard(Shard& s) {
   if (s.keys_ready) hipEventDestroy(s.keys_ready);
   if (s.pin_q_free) hipEventDestroy(s.pin_q_free);
   if (s.copies_done) hipEventDestroy(s.copies_done);
-  for (hipEvent_t e : {s.ev_keys[0], s.ev_keys[1], s.ev_xdone[0], s.ev_xdone[1], s.ev_cdone})
+  for (hipEvent_t e : {s.ev_keys[0], s.ev_keys[1], s.ev_xdone[0], s.ev_xdone[1], s.ev_cdone, s.ev_qread[0],
+                       s.ev_qread[1], s.ev_scr[0], s.ev_scr[1]})
     if (e) hipEventDestroy(e);
   if (s.xstream) hipStreamDestroy(s.xstream);
   if (s.comm) ncclCommDestroy(s.comm);
@@ -346,7 +358,7 @@ int drop_work_buffers(rr_handle* h) {
     HIP_TRY(hipSetDevice(s.dev));
     HIP_TRY(hipStreamSynchronize(s.stream));
     HIP_TRY(hipStreamSynchronize(s.xstream));
-    void** ptrs[] = {(void**)&s.queries, (void**)&s.cand, (void**)&s.scount, (void**)&s.shard_keys, (void**)&s.gathered,
+    void** ptrs[] = {(void**)&s.qbuf[0], (void**)&s.qbuf[1], (void**)&s.cand, (void**)&s.scount, (void**)&s.ctr, (void**)&s.shard_keys, (void**)&s.gathered,
                      (void**)&s.out_base, (void**)&s.full_keys, (void**)&s.sorted, &s.sort_temp,
                      (void**)&s.px_keys[0], (void**)&s.px_keys[1], (void**)&s.px_gathered[0],
                      (void**)&s.px_gathered[1]};
@@ -367,6 +379,8 @@ int drop_work_buffers(rr_handle* h) {
   h->screen_blocks = 0;   // the flagged-block counters (scount) were freed above
   h->screen_reruns = 0;
   h->last_screened = false;
+  h->last_settled = true;
+  h->qpar = 0;
   h->loaded = false;
   return RR_OK;
 }
@@ -391,8 +405,11 @@ int ensure_buffers(rr_handle* h, int b, int k) {
     if (b > s.q_cap || k > s.k_cap) {
       const int qc = std::max(b, s.q_cap), kc = std::max(k, s.k_cap);
       if (b > s.q_cap) {
-        if (int rc = dmalloc(&s.queries, (size_t)((qc + kMaxSlots - 1) / kMaxSlots * kMaxSlots) * h->d * 4)) return rc;
-        HIP_TRY(hipMemset(s.queries, 0, (size_t)((qc + kMaxSlots - 1) / kMaxSlots * kMaxSlots) * h->d * 4));
+        const size_t qb = (size_t)((qc + kMaxSlots - 1) / kMaxSlots * kMaxSlots) * h->d * 4;
+        for (int i = 0; i < 2; ++i) {
+          if (int rc = dmalloc(&s.qbuf[i], qb)) return rc;
+          HIP_TRY(hipMemset(s.qbuf[i], 0, qb));
+        }
       }
       // scores and indices in one allocation, so a search's results come back in ONE D2H copy
       s.out_off = (kOutHead + (size_t)qc * kc * 4 + 255) & ~(size_t)255;
@@ -408,9 +425,11 @@ int ensure_buffers(rr_handle* h, int b, int k) {
     }
     if (!s.cand) {
       s.cand_grid = s.cus;
-      if (int rc = dmalloc(&s.cand, (size_t)s.cand_grid * kMaxSlots * RR_FUSED_KMAX * 8)) return rc;
+      if (int rc = dmalloc(&s.cand, 2 * cand_half(s) * 8)) return rc;
       if (int rc = dmalloc(&s.scount, sizeof(int))) return rc;
       HIP_TRY(hipMemset(s.scount, 0, sizeof(int)));
+      if (int rc = dmalloc(&s.ctr, sizeof(uint32_t))) return rc;
+      HIP_TRY(hipMemset(s.ctr, 0, sizeof(uint32_t)));
     }
     if ((h->world > 1 || h->dist) && !s.px_keys[0]) {
       for (int p = 0; p < 2; ++p) {
@@ -539,11 +558,11 @@ int local_gather(rr_handle* h, int kk) {
 // process per GPU, peer copies within one process) into px_gathered[p] and merges it into the results,
 // while the compute stream goes on with the next block. px_keys[p] is rewritten two blocks later and only
 // after ev_xdone[p] of every shard that read it (enqueue_block).
-int enqueue_exchange_px(rr_handle* h, int p, int q0, int bb, int k, int kt, int slots) {
+int enqueue_exchange_px(rr_handle* h, int p, int q0, int bb, int k, int kt, int slots, bool keys_on_x) {
   const size_t slot = (size_t)slots * kt + kXTail;   // keys + the shard's flag word
-  for (Shard& s : h->shards) {
+  for (Shard& s : h->shards) {   // px_keys[p] is written: by the compute stream, or by the verify on xstream
     HIP_TRY(hipSetDevice(s.dev));
-    HIP_TRY(hipEventRecord(s.ev_keys[p], s.stream));
+    HIP_TRY(hipEventRecord(s.ev_keys[p], keys_on_x ? s.xstream : s.stream));
   }
   for (Shard& dst : h->shards) {
     HIP_TRY(hipSetDevice(dst.dev));
@@ -584,6 +603,8 @@ rr::SkArgs sk_base(const rr_handle* h, const Shard& s, const float* qb, int bb) 
   a.d = h->d;
   a.b = bb;
   a.idx_base = (uint32_t)s.row_begin;
+  a.ctr = s.ctr;
+  a.dyn = h->dyn_sched;
   return a;
 }
 
@@ -619,7 +640,7 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
           if (hipError_t e = hipStreamWaitEvent(s.stream, o.ev_xdone[par], 0)) return e;
       return hipSuccess;
     };
-    const float* qb = s.queries + (size_t)q0 * d;
+    const float* qb = s.qbuf[h->qpar] + (size_t)q0 * d;
     float* osc = s.out_scores + (size_t)q0 * k;
     int64_t* oix = s.out_idx + (size_t)q0 * k;
     const uint32_t base = (uint32_t)s.row_begin;
@@ -628,21 +649,28 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
     if (timed)
       if (int rc = next_event_pair(s, &e0, &e1)) return rc;
     if (scr) {
-      // screened search: screen (upper bounds) -> verify (exact DT 3 scores of the KT candidates, results;
-      // raises the block's flag word when the bound cannot prove completeness: settle_screen re-runs then)
-      if (multi) HIP_TRY(wait_px(p));
+      // screened search. Compute stream: the screen (upper bounds) into cand[p], once the verify of the block
+      // two back has read that half. Exchange stream: the verify (exact DT 3 scores of the KT candidates;
+      // results, or this shard's exact keys for the exchange; raises the block's flag word when the bound
+      // cannot prove completeness: settle_screen re-runs then), overlapping the next block's screen.
+      HIP_TRY(wait_px(p));
+      uint64_t* candp = s.cand + (size_t)p * cand_half(s);
+      const int sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(s.cand_grid, (s.rows() + 31) / 32));
+      if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
       if (s.rows() > 0) {
-        const int sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(s.cand_grid, (s.rows() + 31) / 32));
         rr::SkArgs a = sk_base(h, s, qb, bb);
-        a.out = s.cand;
+        a.out = candp;
         a.eps_a = kScreenEpsA;
         a.eps_b = kScreenEpsB;
         a.sqrt_d = sqrtf((float)d) * (1.0f + 0x1p-20f);
-        if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
         HIP_TRY(rr::launch_sk_args(rr::KDT_SCREEN, h->metric, kt, 0, sgrid, rr::kQSlots, a, s.stream));
-        if (timed) HIP_TRY(hipEventRecord(e1, s.stream));
+      }
+      if (timed) HIP_TRY(hipEventRecord(e1, s.stream));
+      HIP_TRY(hipEventRecord(s.ev_scr[p], s.stream));
+      HIP_TRY(hipStreamWaitEvent(s.xstream, s.ev_scr[p], 0));
+      if (s.rows() > 0) {
         rr::SkArgs v = sk_base(h, s, qb, bb);
-        v.vin = s.cand;
+        v.vin = candp;
         v.nlists = sgrid;
         v.k_out = k;
         v.out_scores = multi ? nullptr : osc;
@@ -653,22 +681,22 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
         v.count = s.scount;
         v.seq = seq;
         v.force_incomplete = h->kernel == RR_KERNEL_SCREEN_FALLBACK;
-        HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 1, rr::kQSlots, rr::kQSlots, v, s.stream));
+        HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 1, rr::kQSlots, rr::kQSlots, v, s.xstream));
       } else {   // a shard without rows contributes empty lists
-        if (timed) {
-          HIP_TRY(hipEventRecord(e0, s.stream));
-          HIP_TRY(hipEventRecord(e1, s.stream));
-        }
-        HIP_TRY(hipMemsetAsync(s.px_keys[p], 0, (size_t)slots * kt * 8, s.stream));
+        HIP_TRY(hipMemsetAsync(s.px_keys[p], 0, (size_t)slots * kt * 8, s.xstream));
       }
+      HIP_TRY(hipEventRecord(s.ev_qread[h->qpar], s.xstream));
+      if (!multi) HIP_TRY(hipEventRecord(s.ev_xdone[p], s.xstream));
     } else if (kt) {
       int grid = fused_grid(s);
+      HIP_TRY(wait_px(0));   // no screened verify still reads cand or writes the results
+      HIP_TRY(wait_px(1));
       if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
       if (s.rows() > 0) {
         if (use_sk(h)) {
           const int sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(s.cand_grid, (s.rows() + 31) / 32));
           HIP_TRY(rr::launch_sk(sk_dtype_of(h->dtype), h->metric, kt, sgrid, s.corpus, s.norms, s.rscale, qb,
-                                s.rows(), d, bb, base, s.cand, s.stream, 0, slots));
+                                s.rows(), d, bb, base, s.cand, s.stream, 0, slots, h->dyn_sched ? s.ctr : nullptr));
           grid = sgrid;
         } else {
           HIP_TRY(rr::launch_fused(kdt_of(h->dtype), h->metric, kt, grid, s.corpus, s.norms, s.rscale, qb,
@@ -689,10 +717,8 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
       // is serial on the compute stream, after every pipelined exchange still writing results.
       const int64_t rows = s.rows();
       if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
-      if (multi) {
-        HIP_TRY(wait_px(0));
-        HIP_TRY(wait_px(1));
-      }
+      HIP_TRY(wait_px(0));   // no pipelined exchange or screened verify still uses the buffers
+      HIP_TRY(wait_px(1));
       HIP_TRY(wait_copies());
       HIP_TRY(hipMemsetAsync(s.shard_keys, 0, (size_t)rr::kQSlots * k * 8, s.stream));
       if (rows > 0) {
@@ -709,9 +735,12 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
       if (!multi) HIP_TRY(rr::launch_decode(s.shard_keys, bb, k, osc, oix, s.stream));
     }
   }
-  if (!multi) return RR_OK;
+  if (!multi) {
+    if (scr) h->parity ^= 1;
+    return RR_OK;
+  }
   if (kt) {
-    if (int rc = enqueue_exchange_px(h, p, q0, bb, k, kt, slots)) return rc;
+    if (int rc = enqueue_exchange_px(h, p, q0, bb, k, kt, slots, scr)) return rc;
     h->parity ^= 1;
     return RR_OK;
   }
@@ -739,6 +768,21 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
     HIP_TRY(hipEventRecord(s.ev_cdone, s.stream));
     HIP_TRY(hipStreamWaitEvent(s.xstream, s.ev_cdone, 0));
   }
+  return RR_OK;
+}
+
+// A new batch goes into the query buffer the last search did not read (that search's verifies may still be
+// running on the exchange streams). The last screened search can be re-run only while its buffer is intact,
+// so it is settled first when its buffer is the one about to be rewritten (two batches staged, no search).
+int begin_stage(rr_handle* h, int* nq) {
+  const int t = h->qpar ^ 1;
+  if (h->last_screened && !h->last_settled && h->last_qpar == t)
+    if (int rc = rr_synchronize(h)) return rc;
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    HIP_TRY(hipStreamWaitEvent(s.stream, s.ev_qread[t], 0));
+  }
+  *nq = t;
   return RR_OK;
 }
 
@@ -793,7 +837,8 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.keys_ready, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.copies_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.xstream, hipStreamNonBlocking);
-    for (hipEvent_t* ev : {&s.ev_keys[0], &s.ev_keys[1], &s.ev_xdone[0], &s.ev_xdone[1], &s.ev_cdone})
+    for (hipEvent_t* ev : {&s.ev_keys[0], &s.ev_keys[1], &s.ev_xdone[0], &s.ev_xdone[1], &s.ev_cdone, &s.ev_qread[0],
+                           &s.ev_qread[1], &s.ev_scr[0], &s.ev_scr[1]})
       if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e != hipSuccess) {
       rr_destroy(h);
@@ -986,11 +1031,14 @@ int rr_set_queries(rr_handle* h, const float* host_q, int32_t b, int32_t d) {
     h->pin_q_cap = qbytes;
   }
   memcpy(h->pin_q, host_q, qbytes);
+  int nq = 0;
+  if (int rc = begin_stage(h, &nq)) return rc;
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
-    HIP_TRY(hipMemcpyAsync(s.queries, h->pin_q, qbytes, hipMemcpyHostToDevice, s.stream));
+    HIP_TRY(hipMemcpyAsync(s.qbuf[nq], h->pin_q, qbytes, hipMemcpyHostToDevice, s.stream));
     HIP_TRY(hipEventRecord(s.pin_q_free, s.stream));
   }
+  h->qpar = nq;
   h->cur_b = b;
   return RR_OK;
 }
@@ -1002,13 +1050,16 @@ int rr_set_queries_device(rr_handle* h, const float* dev_q, int32_t b, int32_t d
   if (b < 1) return fail(RR_E_INVALID, "b=%d", b);
   if (int rc = ensure_buffers(h, b, 1)) return rc;
   const int src_dev = h->shards[0].dev;
+  int nq = 0;
+  if (int rc = begin_stage(h, &nq)) return rc;
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
     if (s.dev == src_dev)
-      HIP_TRY(hipMemcpyAsync(s.queries, dev_q, (size_t)b * d * 4, hipMemcpyDeviceToDevice, s.stream));
+      HIP_TRY(hipMemcpyAsync(s.qbuf[nq], dev_q, (size_t)b * d * 4, hipMemcpyDeviceToDevice, s.stream));
     else
-      HIP_TRY(hipMemcpyPeerAsync(s.queries, s.dev, dev_q, src_dev, (size_t)b * d * 4, s.stream));
+      HIP_TRY(hipMemcpyPeerAsync(s.qbuf[nq], s.dev, dev_q, src_dev, (size_t)b * d * 4, s.stream));
   }
+  h->qpar = nq;
   h->cur_b = b;
   return RR_OK;
 }
@@ -1022,6 +1073,8 @@ int rr_search_staged(rr_handle* h, int32_t k) {
   const int slots = block_slots(h, b, k);
   h->last_screened = screened(h, k, slots);
   h->last_seq0 = h->screen_seq + 1;
+  h->last_settled = !h->last_screened;
+  h->last_qpar = h->qpar;
   for (int q0 = 0; q0 < b; q0 += slots) {
     const int bb = std::min(slots, b - q0);
     if (int rc = enqueue_block(h, q0, bb, k, slots)) return rc;
@@ -1054,11 +1107,19 @@ int sync_streams(rr_handle* h) {
 // search was flagged, re-run the search — its queries are still staged — with the one-pass exact kernel.
 int settle_screen(rr_handle* h, uint64_t flag, bool* rerun) {
   *rerun = false;
-  if (!h->last_screened || flag < (uint64_t)h->last_seq0) return RR_OK;
-  const int saved = h->kernel;
+  if (!h->last_screened || h->last_settled) return RR_OK;
+  h->last_settled = true;
+  if (flag < (uint64_t)h->last_seq0) return RR_OK;
+  // the search's own queries (begin_stage keeps its buffer intact until it is settled); a batch staged
+  // since stays staged
+  const int saved_kernel = h->kernel, saved_qpar = h->qpar, saved_b = h->cur_b;
   h->kernel = RR_KERNEL_EXACT;
+  h->qpar = h->last_qpar;
+  h->cur_b = h->last_b;
   const int rc = rr_search_staged(h, h->last_k);
-  h->kernel = saved;
+  h->kernel = saved_kernel;
+  h->qpar = saved_qpar;
+  h->cur_b = saved_b;
   if (rc) return rc;
   ++h->screen_reruns;
   *rerun = true;
@@ -1151,17 +1212,20 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
   }
   if (!a.done) HIP_TRY(hipEventCreateWithFlags(&a.done, hipEventDisableTiming));
   memcpy(a.pin, host_q, qbytes);
+  int nq = 0;
+  if (int rc = begin_stage(h, &nq)) return rc;
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
-    HIP_TRY(hipMemcpyAsync(s.queries, a.pin, qbytes, hipMemcpyHostToDevice, s.stream));
+    HIP_TRY(hipMemcpyAsync(s.qbuf[nq], a.pin, qbytes, hipMemcpyHostToDevice, s.stream));
   }
+  h->qpar = nq;
   h->cur_b = b;
   if (int rc = rr_search_staged(h, k)) return rc;
   // results come back on the stream that wrote them last: the exchange stream when there is an exchange
   // (the serial k > 32 exchange also orders it after itself), else the compute stream
   Shard& s0 = h->shards[0];
   HIP_TRY(hipSetDevice(s0.dev));
-  hipStream_t rs = (h->world > 1 || h->dist) ? s0.xstream : s0.stream;
+  hipStream_t rs = (h->world > 1 || h->dist || h->last_screened) ? s0.xstream : s0.stream;
   HIP_TRY(hipMemcpyAsync(a.pin + res_off, s0.out_base, kOutHead, hipMemcpyDeviceToHost, rs));
   HIP_TRY(hipMemcpyAsync(a.pin + res_off + kOutHead, s0.out_scores, cnt * 4, hipMemcpyDeviceToHost, rs));
   HIP_TRY(hipMemcpyAsync(a.pin + idx_off, s0.out_idx, cnt * 8, hipMemcpyDeviceToHost, rs));
@@ -1193,10 +1257,13 @@ int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx) {
     // a block needed the exact pass: this batch again, exactly (every rank of an exchange sees the same
     // flag here, so all re-run it together)
     if (int rc = sync_streams(h)) return rc;
+    int nq = 0;
+    if (int rc = begin_stage(h, &nq)) return rc;
     for (Shard& s : h->shards) {
       HIP_TRY(hipSetDevice(s.dev));
-      HIP_TRY(hipMemcpyAsync(s.queries, a.pin, qbytes, hipMemcpyHostToDevice, s.stream));
+      HIP_TRY(hipMemcpyAsync(s.qbuf[nq], a.pin, qbytes, hipMemcpyHostToDevice, s.stream));
     }
+    h->qpar = nq;
     h->cur_b = a.b;
     const int saved = h->kernel;
     h->kernel = RR_KERNEL_EXACT;
@@ -1231,6 +1298,13 @@ int rr_set_kernel(rr_handle* h, int kernel) {
   if (!h) return fail(RR_E_INVALID, "null handle");
   if (kernel < RR_KERNEL_AUTO || kernel > RR_KERNEL_SCREEN_FALLBACK) return fail(RR_E_INVALID, "bad kernel %d", kernel);
   h->kernel = kernel;
+  return RR_OK;
+}
+
+int rr_set_schedule(rr_handle* h, int dynamic) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  if (int rc = sync_streams(h)) return rc;   // no launch in flight uses the counter
+  h->dyn_sched = dynamic ? 1 : 0;
   return RR_OK;
 }
 

@@ -52,6 +52,8 @@ struct SkArgs {
   int d, b;                // dimension, queries in this block
   uint32_t idx_base;       // global index of local row 0
   uint64_t* out;           // MODE 0: [grid][slots][KT] candidate keys
+  uint32_t* ctr;           // MODE 0, dyn: the shard's chunk counter (0 between launches; the kernel resets it)
+  int dyn;                 // MODE 0: 1 = dynamic chunk schedule (ctr), 0 = static (chunks g, g + grid, ...)
   // screen (KDT_SCREEN): upper bound u = s~ + eps_a |x||q| + eps_b (sqrt_d |x| + sum|q|)
   float eps_a, eps_b, sqrt_d;
   // MODE 1 (verify, one workgroup per query slot)
@@ -68,9 +70,9 @@ struct SkArgs {
 
 // Split-K streaming kernel (rr_sk.hip): same output contract as launch_fused. sdt = KDT_* (0..3).
 // sk_slabs(sdt, d) = 128-byte slabs per wave per row (1..4; bf16 1..2), 0 if d is not supported.
-// ring = LDS slab slots per wave (0 = kSkRing). Shipped: 2. A third slot (builds with RR_SK_RING3) needs a
-// single-buffered K-partial block and a second barrier per tile; on MI355X it ran 5 % slower for fp32
-// storage and within 1 % for bf16 / fp32-split (profiles/r01/kbench_ring.log).
+// ring = LDS slab slots per wave (0 = kSkRing): 2. (A third slot ran 5 % slower for fp32 storage and within
+// 1 % for bf16 / fp32-split, profiles/r01/kbench_ring.log, and no better from an idle GPU,
+// profiles/r02/kbench_transient_ring.log; removed.)
 constexpr int kSkRing = 2;
 // qslots = query slots per corpus pass (32, or 64 where sk_supports_64: bf16 / fp32-split storage, KT <= 16);
 // cand is then [grid][qslots][KT].
@@ -79,7 +81,7 @@ bool sk_supports_64(int sdt);
 size_t sk_lds_bytes(int sdt, bool cos, int ring, int qslots);
 hipError_t launch_sk(int sdt, int metric, int kt, int grid, const void* corpus, const float* norms,
                      const float* rscale, const float* queries, int64_t n, int d, int b, uint32_t idx_base,
-                     uint64_t* cand, hipStream_t s, int ring = 0, int qslots = 32);
+                     uint64_t* cand, hipStream_t s, int ring = 0, int qslots = 32, uint32_t* ctr = nullptr);
 // Any mode: mode 0 (top-KT per workgroup; sdt KDT_SCREEN = the screen), mode 1 (verify, grid = 32).
 hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int qslots, const SkArgs& a,
                           hipStream_t s, int ring = 0);

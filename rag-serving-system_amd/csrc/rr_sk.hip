@@ -76,7 +76,6 @@ __device__ unsigned long long probe[4096 * 8];
 constexpr int kSlabRowBytes = 128;                // contiguous bytes of one row per slab
 constexpr int kSlabBytes = 32 * kSlabRowBytes;    // 4 KiB
 constexpr int kRedStride = 36;                    // floats per (wave, query) block of 32 rows (+4 pad)
-constexpr int kSegRows = 1024;                    // rows of per-doc factors held in LDS at a time
 
 // Ring of RS slab slots per wave: RS - 1 slabs stay in flight while one is multiplied. With RS = 2 the
 // K-partial block is double-buffered (one barrier per tile); with RS = 3 (2 x 32 KiB more ring) it is
@@ -108,6 +107,25 @@ __device__ __forceinline__ void glds16(const void* src, unsigned lds) {
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+// s_waitcnt vmcnt(n) for the n the issue sequence leaves (workgroup- or wave-uniform): 0, or one slab (4)
+// plus up to two single-instruction extras of wave 0 (per-row factors, chunk counter)
+__device__ __forceinline__ void wait_vm_n(int n) {
+  switch (n) {
+    case 0: wait_vm<0>(); break;
+    case 4: wait_vm<4>(); break;
+    case 5: wait_vm<5>(); break;
+    default: wait_vm<6>(); break;
+  }
+}
+// One 4-byte-per-lane LDS-DMA load (the per-row factors of a tile: 64 lanes x 4 B), default policy.
+__device__ __forceinline__ void glds4(const void* src, unsigned lds) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
 }
 
 // LDS writes of this wave visible, then the workgroup barrier (no vmcnt: slabs stay in flight across it)
@@ -225,11 +243,12 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
 // them all; each A fragment then feeds the MFMAs of both halves).
 // MODE 0: top-KT per query over this workgroup's rows (DT 6: by upper bound).
 // MODE 1: verify (DT 3, QH 1): block q = query slot q; see "Screened search" above.
-template <int DT, int NS, int KT, bool COS, int RS, int QH, int MODE>
-__global__ __launch_bounds__(512, 1) void sk_score_kernel(const SkArgs a) {
-  static_assert(RS == 2 || RS == 3, "ring depth 2 or 3 (the tail waits are written for these)");
+template <int DT, int NS, int KT, bool COS, int RS, int QH, int MODE, int SCHED>
+__global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const SkArgs a) {
+  static_assert(RS == 2, "two slab slots per wave: one in flight while one is multiplied (the waits assume it)");
   static_assert(QH == 1 || QH == 2, "32 or 64 query slots");
   static_assert(MODE == 0 || (DT == 3 && QH == 1), "the verify stage runs the exact fp32 arithmetic");
+  static_assert(SCHED == 0 || (MODE == 0 && QH == 1), "the scheduler wave serves the 32-slot streaming pass");
   constexpr int QS = 32 * QH;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   SK_PROBE(0);
@@ -249,9 +268,11 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const SkArgs a) {
   const int p0 = w * (KS / 16);                                 // first 16-byte storage unit of the slice
 
   float* red = (float*)(smem + ring_bytes(RS));
-  constexpr int SW = (COS || DT == 6 ? 1 : 0) + (DT == 2 ? 1 : 0);   // per-doc floats in the segment
-  float* seg = (float*)(smem + ring_bytes(RS) + red_bytes(RS, QH));
-  float* qinfo = seg + kSegRows * (SW > 0 ? SW : 1);            // [QS] |q|, [QS] 2^-e / sum|q| / max|q|, [QS] int e
+  constexpr int SW = (COS || DT == 6 ? 1 : 0) + (DT == 2 ? 1 : 0);   // per-row factors (norm, split scale)
+  constexpr int FX = SW > 0 ? 1 : 0;                            // LDS-DMA instructions per tile for them
+  float* trow = (float*)(smem + ring_bytes(RS) + red_bytes(RS, QH));   // [3 tiles][2 factors][32 rows]
+  int* nxt = (int*)(trow + 3 * 64);                             // [2] next chunk (dynamic schedule), + pad
+  float* qinfo = (float*)(nxt + 4);                             // [QS] |q|, [QS] 2^-e / sum|q| / max|q|, [QS] int e
   int* qexp = (int*)(qinfo + 2 * QS);
 
   // ---- MODE 1: the candidate rows of query slot vq ---------------------------------------------------------
@@ -273,35 +294,72 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const SkArgs a) {
     }
   }
 
-  // ---- this workgroup's rows (MODE 0) ------------------------------------------------------------------------
+  // ---- MODE 0 work: 32-row tiles in chunks of CT tiles (about 8 slabs, 256 KiB of corpus per workgroup).
+  // Workgroup g takes chunk g, then (SCHED) the next free chunk from a device counter — workgroups on CUs that
+  // get a larger share of the HBM bandwidth take more chunks, so all of them finish together — or (static)
+  // chunks g + G, g + 2G, ...
+  constexpr int CT = NS >= 4 ? 2 : NS == 3 ? 3 : NS == 2 ? 4 : 8;
   const int64_t G = gridDim.x, g = blockIdx.x;
-  const int64_t per = n / G, rem = n % G;
-  const int64_t r0 = MODE == 1 ? 0 : g * per + (g < rem ? g : rem);
-  const int64_t r1 = MODE == 1 ? 32 : r0 + per + (g < rem ? 1 : 0);
-  const int64_t ntile = MODE == 1 ? 1 : (r1 - r0 + 31) / 32;
+  const int64_t T = (n + 31) / 32, C = (T + CT - 1) / CT;
 
   // LDS-DMA lane mapping: instruction i of a slab covers tile rows 8i + lane/8, 16-byte column
   // (lane % 8) ^ (lane / 8) of the slab — so the image holds column c of row r at c ^ (r & 7)
   const int rl = lane >> 3, cl = lane & 7;
   const unsigned ring_lds = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(smem + (size_t)w * RS * kSlabBytes));
+  const unsigned trow_lds = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)trow);
   const char* ring = smem + (size_t)w * RS * kSlabBytes;
   const char* lane_src = corpus + (size_t)w * KS + ((cl ^ rl) << 4);
 
-  auto issue = [&](int64_t tile, int j, int slot) {
+  auto issue = [&](int64_t base, int j, int slot) {   // slab j (this wave's K-slice) of the tile at row base
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int64_t row = r0 + tile * 32 + 8 * i + rl;
-      row = row < r1 ? row : r1 - 1;                  // partial last tile: re-read a valid row
+      int64_t row = base + 8 * i + rl;
+      row = row < n ? row : n - 1;                    // partial last tile: re-read a valid row
       glds16(lane_src + row * row_bytes + j * kSlabRowBytes, ring_lds + slot * kSlabBytes + i * 1024);
     }
   };
+  // wave 0: the per-row factors of the tile at row base into factor slot ts (lanes 0-31: the norm, or the
+  // split scale when there is no norm; lanes 32-63: the split scale next to a norm)
+  auto issue_factors = [&](int64_t base, int ts) {
+    int64_t row = base + (lane & 31);
+    row = row < n ? row : n - 1;
+    const float* src = ((SW == 2 && lane >= 32) || (DT == 2 && !COS)) ? rscale : norms;
+    glds4(src + row, trow_lds + ts * 256);
+  };
 
-  const int64_t total = ntile * NS;                   // slabs this wave consumes
+  if constexpr (SCHED) {
+    if (w == kWaves) {
+      // The scheduler wave (a 9th wave: no corpus, no query, no inline-asm loads, so hipcc's own waits around
+      // its atomic drain nothing else). Per chunk it takes the next free chunk from the counter and publishes
+      // it in nxt[] before the chunk's first reduction barrier; the streaming waves read it at the chunk's last
+      // step. It passes exactly the barriers the streaming waves pass: one after the query scalars, one per tile.
+      __syncthreads();
+      int64_t ck = g;
+      int cp = 0;
+      while (ck < C) {
+        const int tic = (int)(C - ck == 1 ? T - ck * CT : CT);
+        if (ck != C - 1 && lane == 0) {   // every chunk but the last asks once: C - 1 dequeues per launch
+          const uint32_t old = __hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const int64_t nc = G + (int64_t)old;
+          nxt[cp] = (int)(nc < C ? nc : C);
+          // the launch's last dequeue resets the counter for the next launch on this stream
+          if ((int64_t)old == C - 2) __hip_atomic_store(a.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        for (int t = 0; t < tic; ++t) lds_barrier();
+        if (ck == C - 1) break;
+        ck = nxt[cp];
+        cp ^= 1;
+      }
+      return;
+    }
+  }
+
+  int64_t chunk = g, base = chunk * CT * 32;
   if constexpr (MODE == 0) {
-    // prologue: the first RS - 1 slabs (slab p = tile p / NS, column block p % NS, slot p)
-#pragma unroll
-    for (int p = 0; p < RS - 1; ++p)
-      if (p < total) issue(p / NS, p % NS, p);
+    if (chunk < C) {   // prologue: the first tile's factors and slab 0
+      if (FX && w == 0) issue_factors(base, 0);
+      issue(base, 0, 0);
+    }
   }
   // ---- query side: this wave's K-slice of every query as MFMA B operands, |q| and split exponents.
   // Runs while the prologue slabs above are in flight (their latency overlaps the query loads).
@@ -311,7 +369,9 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const SkArgs a) {
 #pragma unroll
     for (int qh = 0; qh < QH; ++qh) {
       QFrag<DT, NS>& qf = qfs[qh];
-      const int rq = r + 32 * qh;
+      // MODE 1 puts query vq in every column: each output element depends only on its own column's operands,
+      // so column vq's scores are bit-identical to a full pass's, and every lane loads the same 4 KB
+      const int rq = MODE == 1 ? vq : r + 32 * qh;
       const bool qv = rq < b;
       const float* qrow = queries + (size_t)(qv ? rq : 0) * d;
       const uint32_t qmask = opaque_mask(qv);
@@ -385,7 +445,36 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const SkArgs a) {
   // sum |q| (DT 6 bound), max |q| (MODE 1: the screen's f16 range). All loads of a group of 4 queries are
   // issued before any is used (one L2/HBM latency per group, not one per query); the sums are the same
   // lane-strided fmaf chains + xor tree in the same order.
-  if (COS || DT == 2 || DT == 6 || MODE == 1) {
+  if constexpr (MODE == 1) {   // |q| and max |q| of query vq only, by wave 0
+    if (w == 0) {
+      const int nc = d >> 2;
+      f32x4 v[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int cc = lane + 64 * c;
+        v[c] = zero_unless(((const f32x4*)queries)[(size_t)vq * nc + (cc < nc ? cc : 0)], opaque_mask(cc < nc));
+      }
+      float ss = 0.f, m = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (lane + 64 * c < nc) {
+          const f32x4 x = v[c];
+          ss = fmaf(x.x, x.x, ss); ss = fmaf(x.y, x.y, ss); ss = fmaf(x.z, x.z, ss); ss = fmaf(x.w, x.w, ss);
+          m = fmaxf(m, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+        }
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {   // the same xor tree as the full pass's |q|
+        ss += __shfl_xor(ss, off, 64);
+        m = fmaxf(m, __shfl_xor(m, off, 64));
+      }
+      if (lane == 0) {
+        qinfo[vq] = sqrtf(ss);
+        qinfo[QS + vq] = m;
+      }
+    }
+    __syncthreads();
+  } else if (COS || DT == 2 || DT == 6) {
     const int nc = d >> 2;                      // float4 per row (d <= 1024 on this kernel: <= 4 per lane)
 #pragma unroll
     for (int g4 = 0; g4 < QH; ++g4) {
@@ -473,9 +562,13 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const SkArgs a) {
   tk.init();
 
   SK_PROBE(1);
-  int64_t seg_lo = INT64_MIN / 2;
-  int slot = 0;                                       // slot of the slab being consumed
-  for (int64_t tile = 0; tile < ntile; ++tile) {
+  int slot = 0, ti = 0, cpar = 0, ts = 0;   // ring slot, tile of the chunk, nxt parity, factor slot
+  int64_t tcount = 0;                       // tiles done (reduction buffer parity)
+  bool run = MODE == 1 || chunk < C;
+  while (run) {
+    const int tic = MODE == 1 ? 1 : (int)(C - chunk == 1 ? T - chunk * CT : CT);   // tiles in this chunk
+    const bool last_in_chunk = ti + 1 == tic;
+    int64_t next_chunk = C, next_base = -1;
     f32x16 accs[QH];
 #pragma unroll
     for (int qh = 0; qh < QH; ++qh)
@@ -483,21 +576,32 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const SkArgs a) {
       for (int i = 0; i < 16; ++i) accs[qh][i] = 0.f;
     static_for<0, NS>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      // keep RS - 1 slabs in flight: issue slab s + RS - 1 into the slot consumed last, then wait for
-      // slab s (4 LDS-DMA instructions per slab; the younger ones stay outstanding)
-      constexpr int jn = j + RS - 1;
-      const int64_t tn = tile + jn / NS;
-      int nslot = slot + RS - 1;
-      nslot -= nslot >= RS ? RS : 0;
-      if constexpr (MODE == 1) {
-        // registers: hipcc waits for its own loads
-      } else if (tn < ntile) {
-        issue(tn, jn % NS, nslot);
-        wait_vm<4 * (RS - 1)>();
-      } else if (RS == 3 && tile * NS + j + 2 == total) {   // tail: one younger slab still in flight
-        wait_vm<4>();
-      } else {
-        wait_vm<0>();
+      if constexpr (MODE == 0) {
+        // keep one slab in flight: issue the next slab (of this tile, or slab 0 of the next tile with wave 0
+        // issuing that tile's factors first) into the slot consumed last, then wait for this one. Wave 0's
+        // counted wait includes its single-instruction extras issued after this slab (factors, counter).
+        int nw = 0, extra0 = 0;
+        if (j + 1 < NS) {
+          issue(base, j + 1, slot ^ 1);
+          nw = 4;
+        } else {
+          if (!last_in_chunk) {
+            next_base = base + 32;
+          } else {
+            next_chunk = !SCHED ? chunk + G : chunk == C - 1 ? C : (int64_t)nxt[cpar];
+            next_base = next_chunk < C ? next_chunk * CT * 32 : -1;
+          }
+          if (next_base >= 0) {
+            if (FX && w == 0) {
+              issue_factors(next_base, ts == 2 ? 0 : ts + 1);
+              extra0 += 1;
+            }
+            issue(next_base, 0, slot ^ 1);
+            nw = 4;
+          }
+        }
+        if (nw) nw += w == 0 ? extra0 : 0;
+        wait_vm_n(nw);
       }
       const char* sl = ring + slot * kSlabBytes;
       if constexpr (DT == 0) {
@@ -556,13 +660,13 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const SkArgs a) {
           }
         }
       }
-      slot = slot + 1 == RS ? 0 : slot + 1;
+      slot ^= 1;
     });
 
     // ---- sum the 8 K-partials of this tile (fixed order), then the metric epilogue --------------------
-    float* rb = red + (red_bufs(RS, QH) == 2 ? (size_t)(tile & 1) * kWaves * QS * kRedStride : 0);
+    float* rb = red + (red_bufs(RS, QH) == 2 ? (size_t)(tcount & 1) * kWaves * QS * kRedStride : 0);
     if constexpr (red_bufs(RS, QH) == 1) {
-      if (tile > 0) lds_barrier();   // every wave has read the previous tile's partials
+      if (tcount > 0) lds_barrier();   // every wave has read the previous tile's partials
     }
 #pragma unroll
     for (int qh = 0; qh < QH; ++qh)
@@ -571,26 +675,7 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const SkArgs a) {
         const f32x4 v = {accs[qh][4 * a4], accs[qh][4 * a4 + 1], accs[qh][4 * a4 + 2], accs[qh][4 * a4 + 3]};
         *(f32x4*)(rb + (w * QS + 32 * qh + r) * kRedStride + 8 * a4 + 4 * h) = v;
       }
-    lds_barrier();
-    const int64_t tb = r0 + tile * 32;
-    if constexpr (SW > 0 && MODE == 0) {
-      if (tb < seg_lo || tb + 32 > seg_lo + kSegRows) {   // workgroup-uniform: refill the per-doc factors
-        seg_lo = tb;
-        for (int i = tid; i < kSegRows; i += kThreads) {
-          int64_t row = tb + i;
-          row = row < r1 ? row : r1 - 1;
-          if constexpr (COS && DT == 2) {
-            seg[2 * i] = norms[row];
-            seg[2 * i + 1] = rscale[row];
-          } else if constexpr (COS || DT == 6) {
-            seg[i] = norms[row];
-          } else {
-            seg[i] = rscale[row];
-          }
-        }
-        lds_barrier();
-      }
-    }
+    lds_barrier();   // (also publishes wave 0's LDS-DMA factors and its next-chunk word)
     float sv[DPL];
 #pragma unroll
     for (int e = 0; e < DPL; ++e) sv[e] = 0.f;
@@ -630,11 +715,11 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const SkArgs a) {
         valid = qev && gvalid[er + e];
         if constexpr (COS) nd = gnorm[er + e];
       } else {
-        row = tb + er + e;
-        const int64_t li = row - seg_lo;
-        valid = qev && row < r1;
-        if constexpr (DT == 2) s = s * (COS ? seg[2 * li + 1] : seg[li]) * qs;   // exact 2^e rescales
-        if constexpr (COS || DT == 6) nd = DT == 2 ? seg[2 * li] : seg[li];
+        row = base + er + e;
+        valid = qev && row < n;
+        const float* tf = trow + ts * 64 + er + e;   // factor 0 at tf[0], factor 1 at tf[32]
+        if constexpr (DT == 2) s = s * (COS ? tf[32] : tf[0]) * qs;   // exact 2^e rescales
+        if constexpr (COS || DT == 6) nd = tf[0];
       }
       if constexpr (DT == 6) {
         // upper bound of the exact (DT 3) score, see "Screened search"; the relative bumps cover the
@@ -666,8 +751,21 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const SkArgs a) {
         if (valid && key > tk.last()) tk.insert(key);
       }
     }
-    if (tile == 0) SK_PROBE(2);
-    if (MODE == 0 && tile == 1) SK_PROBE(3);
+    if (tcount == 0) SK_PROBE(2);
+    if (MODE == 0 && tcount == 1) SK_PROBE(3);
+    ++tcount;
+    if constexpr (MODE == 1) break;
+    ts = ts == 2 ? 0 : ts + 1;
+    if (!last_in_chunk) {
+      ++ti;
+      base += 32;
+    } else {
+      if (next_chunk >= C) break;
+      chunk = next_chunk;
+      ti = 0;
+      cpar ^= 1;
+      base = chunk * CT * 32;
+    }
   }
   SK_PROBE(4);
 
@@ -711,9 +809,9 @@ __global__ __launch_bounds__(512, 1) void sk_score_kernel(const SkArgs a) {
   SK_PROBE(5);
 }
 
-template <int DT, int NS, int KT, bool COS, int RS, int QH, int MODE>
+template <int DT, int NS, int KT, bool COS, int RS, int QH, int MODE, int SCHED>
 hipError_t launch_t(int grid, const SkArgs& a, hipStream_t s) {
-  auto kern = sk_score_kernel<DT, NS, KT, COS, RS, QH, MODE>;
+  auto kern = sk_score_kernel<DT, NS, KT, COS, RS, QH, MODE, SCHED>;
   static bool attr_set = false;   // the dynamic-LDS ceiling is a per-function attribute: set it once
   const size_t lds = sk_lds_bytes(DT, COS, RS, 32 * QH);
   if (!attr_set) {
@@ -721,49 +819,52 @@ hipError_t launch_t(int grid, const SkArgs& a, hipStream_t s) {
       return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, a);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads + (SCHED ? 64 : 0)), lds, s, a);
   return hipGetLastError();
 }
 
-template <int DT, int NS, bool COS, int RS, int QH, int MODE>
+template <int DT, int NS, bool COS, int RS, int QH, int MODE, int SCHED>
 hipError_t launch_kt(int kt, int grid, const SkArgs& a, hipStream_t s) {
   switch (kt) {
-    case 4: return launch_t<DT, NS, 4, COS, RS, QH, MODE>(grid, a, s);
-    case 8: return launch_t<DT, NS, 8, COS, RS, QH, MODE>(grid, a, s);
-    case 16: return launch_t<DT, NS, 16, COS, RS, QH, MODE>(grid, a, s);
-    case 32: if constexpr (QH == 1) return launch_t<DT, NS, 32, COS, RS, QH, MODE>(grid, a, s);
-             else return hipErrorInvalidValue;   // 64 slots x KT 32 spills: served as two 32-slot passes
+    case 4: return launch_t<DT, NS, 4, COS, RS, QH, MODE, SCHED>(grid, a, s);
+    case 8: return launch_t<DT, NS, 8, COS, RS, QH, MODE, SCHED>(grid, a, s);
+    case 16: return launch_t<DT, NS, 16, COS, RS, QH, MODE, SCHED>(grid, a, s);
+    // 64 slots x KT 32 spills (served as two 32-slot passes); the 9-wave form's register budget (168) does not
+    // hold KT 32 lists
+    case 32: if constexpr (QH == 1 && SCHED == 0) return launch_t<DT, NS, 32, COS, RS, QH, MODE, 0>(grid, a, s);
+             else return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }
 
-template <int DT, bool COS, int RS, int QH, int MODE>
+template <int DT, bool COS, int RS, int QH, int MODE, int SCHED>
 hipError_t launch_ns(int ns, int kt, int grid, const SkArgs& a, hipStream_t s) {
   switch (ns) {
-    case 1: return launch_kt<DT, 1, COS, RS, QH, MODE>(kt, grid, a, s);
-    case 2: return launch_kt<DT, 2, COS, RS, QH, MODE>(kt, grid, a, s);
-    case 3: if constexpr (DT != 1) return launch_kt<DT, 3, COS, RS, QH, MODE>(kt, grid, a, s);
+    case 1: return launch_kt<DT, 1, COS, RS, QH, MODE, SCHED>(kt, grid, a, s);
+    case 2: return launch_kt<DT, 2, COS, RS, QH, MODE, SCHED>(kt, grid, a, s);
+    case 3: if constexpr (DT != 1) return launch_kt<DT, 3, COS, RS, QH, MODE, SCHED>(kt, grid, a, s);
             else return hipErrorInvalidValue;
-    case 4: if constexpr (DT != 1) return launch_kt<DT, 4, COS, RS, QH, MODE>(kt, grid, a, s);
+    case 4: if constexpr (DT != 1) return launch_kt<DT, 4, COS, RS, QH, MODE, SCHED>(kt, grid, a, s);
             else return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }
 
-template <int DT, int RS, int QH, int MODE = 0>
+template <int DT, int RS, int QH, int MODE = 0, int SCHED = 0>
 hipError_t launch_metric(int metric, int ns, int kt, int grid, const SkArgs& a, hipStream_t s) {
-  return metric ? launch_ns<DT, true, RS, QH, MODE>(ns, kt, grid, a, s)
-                : launch_ns<DT, false, RS, QH, MODE>(ns, kt, grid, a, s);
+  return metric ? launch_ns<DT, true, RS, QH, MODE, SCHED>(ns, kt, grid, a, s)
+                : launch_ns<DT, false, RS, QH, MODE, SCHED>(ns, kt, grid, a, s);
 }
 
 }  // namespace sk
 
 size_t sk_lds_bytes(int sdt, bool cos, int ring, int qslots) {
-  const int sw = (cos || sdt == 6 ? 1 : 0) + (sdt == 2 ? 1 : 0);
-  // + MODE 1 scratch: W [8][32] + akeys [32] keys, grow / gnorm / gvalid [32], xk [32] keys
+  (void)sdt;
+  (void)cos;
+  // + per-row factors [3][2][32], next-chunk words [4], query scalars [3][qslots], MODE 1 scratch: W [8][32] +
+  // akeys [32] keys, grow / gnorm / gvalid [32], xk [32] keys
   const size_t verify = (size_t)(kWaves * 32 + 32 + 32) * 8 + 3 * 32 * 4;
-  return sk::ring_bytes(ring) + sk::red_bytes(ring, qslots / 32) + (size_t)sk::kSegRows * (sw > 0 ? sw : 1) * 4 +
-         3 * qslots * 4 + verify;
+  return sk::ring_bytes(ring) + sk::red_bytes(ring, qslots / 32) + 3 * 64 * 4 + 4 * 4 + 3 * qslots * 4 + verify;
 }
 
 bool sk_supports_64(int sdt) { return sdt == KDT_BF16 || sdt == KDT_F32_SPLIT; }
@@ -784,8 +885,9 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
     if (sdt != KDT_F32_X3 || qslots != 32 || ring != 2 || grid != 32) return hipErrorInvalidValue;
     return sk::launch_metric<3, 2, 1, 1>(metric, ns, kt, grid, a, s);
   }
-  if (sdt == KDT_SCREEN) {
+  if (sdt == KDT_SCREEN) {   // dynamic schedule (9-wave form) when asked for and the lists fit its registers
     if (qslots != 32 || ring != 2) return hipErrorInvalidValue;
+    if (a.dyn && a.ctr && kt <= 16) return sk::launch_metric<6, 2, 1, 0, 1>(metric, ns, kt, grid, a, s);
     return sk::launch_metric<6, 2, 1>(metric, ns, kt, grid, a, s);
   }
   if (qslots == 64) {   // one corpus pass for up to 64 queries: bf16 and fp32-split storage, ring 2
@@ -805,23 +907,16 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
       default: return hipErrorInvalidValue;
     }
   }
-#ifdef RR_SK_RING3   // A/B builds only (tools/kbench.hip): measured no faster, see kSkRing
-  if (ring == 3) {   // (the f32-MFMA form DT 0 is a kbench reference only: ring 2)
-    switch (sdt) {
-      case 1: return sk::launch_metric<1, 3, 1>(metric, ns, kt, grid, a, s);
-      case 2: return sk::launch_metric<2, 3, 1>(metric, ns, kt, grid, a, s);
-      case 3: return sk::launch_metric<3, 3, 1>(metric, ns, kt, grid, a, s);
-      default: return hipErrorInvalidValue;
-    }
-  }
-#endif
+
   return hipErrorInvalidValue;
 }
 
 hipError_t launch_sk(int sdt, int metric, int kt, int grid, const void* c, const float* nr, const float* rs,
                      const float* q, int64_t n, int d, int b, uint32_t base, uint64_t* cand, hipStream_t s, int ring,
-                     int qslots) {
+                     int qslots, uint32_t* ctr) {
   SkArgs a{};
+  a.ctr = ctr;
+  a.dyn = ctr != nullptr;
   a.corpus = (const char*)c;
   a.norms = nr;
   a.rscale = rs;

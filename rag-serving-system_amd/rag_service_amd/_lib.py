@@ -74,6 +74,7 @@ SIGNATURES = {
     "rr_search_async": (_c_int, [_vp, _fp, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_i32)]),
     "rr_wait": (_c_int, [_vp, _c_i32, _fp, _i64p]),
     "rr_screen_stats": (_c_int, [_vp, _i64p, _i64p]),
+    "rr_set_schedule": (_c_int, [_vp, _c_int]),
     "rr_last_shape": (_c_int, [_vp, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32)]),
     "rr_dist_info": (_c_int, [_vp, _ip, _ip]),
 }
@@ -299,6 +300,10 @@ class Index:
         'exact' (split-K, fp32 scored exactly in one pass), 'fused' (register-streaming kernel) or
         'screen-fallback' (test hook: the screened search's exact fallback pass always runs)."""
         _check(self._lib.rr_set_kernel(self._h, self.KERNELS[kernel]))
+
+    def set_schedule(self, dynamic: bool) -> None:
+        """Split-K work schedule: dynamic chunk counter (default) or static round-robin chunks."""
+        _check(self._lib.rr_set_schedule(self._h, 1 if dynamic else 0))
 
     def screen_stats(self) -> Tuple[int, int]:
         """(screened search blocks, blocks that needed the exact fallback pass)."""

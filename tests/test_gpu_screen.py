@@ -161,3 +161,39 @@ def test_screened_rccl_one_rank(Index):
         assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), k
     ref.close()
     rc.close()
+
+
+@pytest.mark.parametrize("metric", ["cosine", "dot"])
+def test_dynamic_schedule_equals_static(Index, metric):
+    """The screen's dynamic chunk schedule (9th wave dequeuing chunks from a device counter that each launch
+    resets) against the static round-robin one: identical results over back-to-back launches of different
+    sizes on one handle (a counter left wrong by one launch would skip or repeat chunks in the next)."""
+    rng = np.random.default_rng(31)
+    corpus = rng.standard_normal((70001, 1024)).astype(np.float32)
+    corpus /= np.linalg.norm(corpus, axis=1, keepdims=True)
+    ix = Index(dtype="fp32", metric=metric)
+    ix.load(corpus)
+    st = Index(dtype="fp32", metric=metric)
+    st.load(corpus)
+    st.set_schedule(False)
+    for b, k in [(32, 5), (7, 1), (32, 7), (45, 3), (1, 5)] * 3:
+        q = rng.standard_normal((b, 1024)).astype(np.float32)
+        got = ix.search(q, k)
+        want = st.search(q, k)
+        assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), (b, k)
+    ix.set_queries(q)
+    for _ in range(50):
+        ix.search_staged(5)
+    s, i = ix.fetch()
+    want = st.search(q, 5)
+    assert np.array_equal(i, want[1]) and np.array_equal(s, want[0])
+    small = Index(dtype="fp32", metric=metric)       # fewer chunks than workgroups, and a single chunk
+    for n in (1000, 40, 257 * 64):
+        small.load(corpus[:n])
+        st.load(corpus[:n])
+        got = small.search(q, 5)
+        want = st.search(q, 5)
+        assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), n
+    ix.close()
+    st.close()
+    small.close()

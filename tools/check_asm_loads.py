@@ -1,6 +1,6 @@
 """Audit a kernel's .s for the inline-asm load hazard of cdna_hip_programming.md §5.7 item 1: no
-compiler instruction may write a VGPR that is the destination of a still-outstanding vector-memory
-load. Linear scan of the listing: a FIFO of outstanding vector-memory ops is pushed by every
+compiler instruction may read or write a VGPR that is the destination of a still-outstanding vector-memory
+load or returning atomic. Linear scan of the listing: a FIFO of outstanding vector-memory ops is pushed by every
 global/buffer load/store and popped by every `s_waitcnt vmcnt(n)` (loads return in order).
 usage: python tools/check_asm_loads.py file.s kernel_symbol"""
 import re
@@ -34,7 +34,8 @@ for i in range(start, end):
     m = re.match(r"(global|buffer)_(load|store|atomic)\w*\s+" + REG, t)
     if m:
         regs = set()
-        if m.group(2) == "load" and "lds" not in t:
+        # destinations: loads (not LDS-DMA), and returning atomics (sc0) — the value lands asynchronously
+        if (m.group(2) == "load" and "lds" not in t) or (m.group(2) == "atomic" and re.search(r"\bsc0\b", t)):
             regs = set(range(int(m.group(3)), int(m.group(4) or m.group(3)) + 1))
         fifo.append(regs if inasm else set())  # hipcc waits for its own loads
         n_asm += inasm

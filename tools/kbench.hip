@@ -4,8 +4,6 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I rag-serving-system_amd/csrc \
 //         tools/kbench.hip -o tools/kbench && tools/kbench [n_docs] [rounds]
-#define RR_SK_RING3 1
-#define RR_SK_SCREEN_PROBE 1
 #include "../rag-serving-system_amd/csrc/rr_kernels.hip"
 #include "../rag-serving-system_amd/csrc/rr_sk.hip"
 
@@ -299,8 +297,7 @@ int main(int argc, char** argv) {
 #define VK(DT, BUF, COS, RS) Variant{"sk DT=" #DT " COS=" #COS " ring=" #RS, BUF, \
     [&](const void* c, uint64_t* o) { return launch_sk(DT, COS, 8, grid, c, DT == 2 ? norms2 : norms, rscale, q, n, d, b, 0, o, s, RS); }, {}}
   std::vector<Variant> vs = {V32(2, 1, 1, true, 0, 8), VS(2, 1, 1, true, 0, 8), V16(2, 1, 1, true, 0, 8),
-                             VK(3, 0, 1, 2), VK(3, 0, 1, 3), VK(2, 2, 1, 2), VK(2, 2, 1, 3), VK(1, 1, 1, 2), VK(1, 1, 1, 3),
-                             VK(3, 0, 0, 2), VK(3, 0, 0, 3)};
+                             VK(3, 0, 1, 2), VK(6, 0, 1, 2), VK(2, 2, 1, 2), VK(1, 1, 1, 2), VK(3, 0, 0, 2)};
   std::vector<Variant> streams = {
       Variant{"stream frag U=8 fp32", 0, [&](const void* c, uint64_t*) {
         hipLaunchKernelGGL(stream_frag<8>, dim3(grid), dim3(512), 0, s, (const u32x4*)c, n, d, sink);
@@ -368,8 +365,8 @@ int main(int argc, char** argv) {
     const int count = argc > 4 ? atoi(argv[4]) : 40;
     const int idle_ms = argc > 5 ? atoi(argv[5]) : 3000;
     CK(hipFuncSetAttribute((const void*)stream_sk<3, 1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 3 * 4096));
-    std::vector<Variant> tv = {VK(3, 0, 1, 2), VK(4, 0, 1, 2), VK(5, 0, 1, 2), VK(2, 2, 1, 2), streams[9],
-                               VK(4, 0, 1, 2), VK(3, 0, 1, 2)};
+    std::vector<Variant> tv = {VK(3, 0, 1, 2), VK(6, 0, 1, 2), VK(2, 2, 1, 2), streams[9], VK(6, 0, 1, 2),
+                               VK(3, 0, 1, 2)};
     std::vector<hipEvent_t> ev(2 * count);
     for (auto& e : ev) CK(hipEventCreate(&e));
     for (auto& v : tv) {
