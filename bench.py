@@ -33,12 +33,20 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "rag-serving-system_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-SCORE_KERNEL_DOC = ("similarity + top-k kernel: sk_score_kernel (split-K, LDS-DMA) where the shape allows, "
-                    "else fused_score_kernel")
+SCORE_KERNEL_DOC = ("the corpus-streaming kernel: sk_score_kernel MODE 0 (split-K, LDS-DMA; for fp32 storage the "
+                    "screened search's f16 screen, DT 6, whose exact verify of the candidates runs overlapped on "
+                    "the exchange stream), else fused_score_kernel")
 
 
 def is_score_kernel(name: str) -> bool:
-    return "sk_score_kernel" in name or "fused_score_kernel" in name
+    """The corpus-streaming launches: sk_score_kernel<DT, NS, KT, COS, RS, QH, MODE, SCHED> with MODE 0 (MODE 1
+    is the screened search's 32-workgroup verify), or fused_score_kernel."""
+    if "fused_score_kernel" in name:
+        return True
+    if "sk_score_kernel<" not in name:
+        return False
+    targs = name.split("sk_score_kernel<", 1)[1].split(">", 1)[0].split(",")
+    return len(targs) >= 7 and targs[6].strip() == "0"
 
 
 def host_cpu_model() -> str:
@@ -100,7 +108,8 @@ def algorithmic_bytes(rows: int, d: int, batch: int, dtype: str, metric: str) ->
     """HBM bytes one fused launch must move: the corpus rows once (4 B/element fp32 and fp32-split, 2 B bf16),
     the per-row factors it reads (norm for cosine, row scale for fp32-split), the fp32 queries once."""
     elem = 2 if dtype == "bf16" else 4
-    per_row = (4 if metric == "cosine" else 0) + (4 if dtype == "fp32-split" else 0)
+    # per-row factors: the norm (cosine; and the fp32 screen's error bound for either metric), the split scale
+    per_row = (4 if metric == "cosine" or dtype == "fp32" else 0) + (4 if dtype == "fp32-split" else 0)
     return rows * (d * elem + per_row) + batch * d * 4
 
 
@@ -422,7 +431,7 @@ def pmc_counters(args, kernel_s):
             busy = statistics.median(per["SQ_VALU_MFMA_BUSY_CYCLES"])
             cyc = statistics.median(per["GRBM_GUI_ACTIVE"]) / 8
             flops = 2.0 * args.batch * args.docs * args.dim
-            peak = {"fp32": 2500.0, "bf16": 2500.0, "fp32-split": 2500.0}[args.dtype]   # products on bf16/f16 MFMAs
+            peak = {"fp32": 2500.0, "bf16": 2500.0, "fp32-split": 2500.0}[args.dtype]   # products on f16/bf16 MFMAs
             mfma = {"busy_frac": round(busy / (4 * cus * cyc), 4), "busy_cycles": busy, "kernel_cycles": cyc,
                     "clock_GHz": round(cyc / kernel_s / 1e9, 3) if kernel_s else None,
                     "alg_tflops": round(flops / kernel_s / 1e12, 2) if kernel_s else None,

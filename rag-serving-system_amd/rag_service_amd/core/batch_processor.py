@@ -54,37 +54,40 @@ class BatchProcessor(threading.Thread):
         self.running = True
         try:
             self.embedding_model["model"].to(self.device)
-            logger.info(f"Models assigned to device: {self.device}")
+            logger.info("embedding model placed on %s", self.device)
         except Exception as e:
-            logger.error(f"Error moving models to device {self.device}: {e}")
-        logger.info("BatchProcessor initialized.")
+            logger.error("could not place the embedding model on %s: %s", self.device, e)
+        logger.info("batch processor ready")
 
     def stop(self):
-        logger.info("Stopping BatchProcessor...")
+        logger.info("batch processor stopping")
         self.running = False
 
     # batch_processor.py:47-71
     def run(self):
-        logger.info("BatchProcessor started.")
+        logger.info("batch processor running")
         while self.running:
             try:
                 batch = self.request_queue.get_batch()
                 if not batch:
                     time.sleep(self.polling_interval)
                     continue
-                logger.info(f"Processing batch of size {len(batch)}...")
+                logger.info("batch of %d requests", len(batch))
                 start_time = time.time()
                 self._process_batch(batch)
-                logger.info(f"Batch processed in {time.time() - start_time:.4f} seconds.")
+                logger.info("batch done in %.4f s", time.time() - start_time)
             except Exception as e:
-                logger.error(f"Critical error in BatchProcessor run loop: {e}", exc_info=True)
-        logger.info("BatchProcessor stopped.")
+                logger.error("run loop: unexpected failure, continuing: %s", e, exc_info=True)
+        logger.info("batch processor stopped")
 
     def retrieve(self, queries: List[str], ks: List[int]) -> List[List[str]]:
         """Embedding half + retrieval (the path BASELINE config 4 measures end to end)."""
         import torch
         emb = embed_queries(self.embedding_model, queries, self.device)
-        if self.device_handoff and emb.is_cuda and hasattr(self.retriever, "batch_retrieve_device"):
+        # the C-ABI reads a device pointer on the retriever's FIRST device; any other placement takes the host path
+        first = getattr(self.retriever, "devices", [0])[0]
+        if (self.device_handoff and emb.is_cuda and emb.device.index == first
+                and hasattr(self.retriever, "batch_retrieve_device")):
             emb = emb.float().contiguous()
             torch.cuda.current_stream(emb.device).synchronize()   # the C-ABI reads it on its own stream
             out = self.retriever.batch_retrieve_device(emb.data_ptr(), emb.shape[0], emb.shape[1], ks)
@@ -107,9 +110,9 @@ class BatchProcessor(threading.Thread):
                 try:
                     self.request_queue.store_result(request_id, {"result": str(outputs[i])})
                 except Exception as e:
-                    logger.error(f"Error processing result for request {request_id}: {e}")
+                    logger.error("request %s: storing its result failed: %s", request_id, e)
                     self.request_queue.store_result(request_id, {"error": str(e)})
         except Exception as e:
-            logger.error(f"Error processing batch (requests: {request_ids}): {e}")
+            logger.error("batch of %d requests failed: %s", len(request_ids), e)
             for request_id in request_ids:
                 self.request_queue.store_result(request_id, {"error": str(e), "status": "failed"})

@@ -40,17 +40,18 @@ class _HipRetrieverBase:
     def __init__(self, doc_embeddings: np.ndarray, documents: List[str], dtype: str = "fp32",
                  devices: Optional[Sequence[int]] = None):
         if doc_embeddings.dtype != np.float32:
-            logger.warning(f"Input doc_embeddings dtype is {doc_embeddings.dtype}, converting to float32.")
+            logger.warning("corpus arrives as %s; storing float32 values", doc_embeddings.dtype)
             doc_embeddings = doc_embeddings.astype(np.float32)
         try:
             self.index = Index(devices=devices, dtype=dtype, metric=self._metric)
             self.index.load(doc_embeddings)
-            logger.info(f"Moved document embeddings ({doc_embeddings.shape}) to HBM "
-                        f"({dtype}, {self._metric}, devices={list(devices) if devices else [0]}).")
+            logger.info("corpus %s resident in HBM: storage %s, metric %s, devices %s", doc_embeddings.shape, dtype,
+                        self._metric, list(devices) if devices else [0])
         except Exception as e:
-            logger.error(f"Failed to move document embeddings to the GPU: {e}", exc_info=True)
+            logger.error("corpus upload to the GPU failed: %s", e, exc_info=True)
             raise
         self.documents = documents
+        self.devices = list(devices) if devices else [0]
         self.N_A = int(doc_embeddings.shape[0])
         self.D = int(doc_embeddings.shape[1])
         self.dtype = dtype
@@ -84,25 +85,25 @@ class HipRetriever(_HipRetrieverBase):
                  devices: Optional[Sequence[int]] = None, metric: str = "cosine"):
         self._metric = metric
         super().__init__(doc_embeddings, documents, dtype=dtype, devices=devices)
-        logger.info(f"Initialized HipRetriever with {self.N_A} documents (Dim={self.D}).")
+        logger.info("HipRetriever ready: %d rows x %d", self.N_A, self.D)
 
     # retriever.py:615-683
     def retrieve(self, query_emb: np.ndarray, k: int = 2) -> List[str]:
         start_time = time.time()
         if not isinstance(query_emb, np.ndarray):
-            logger.error(f"HipRetriever.retrieve expects query_emb as NumPy array, got {type(query_emb)}")
+            logger.error("retrieve: query must be a numpy.ndarray, not %s", type(query_emb).__name__)
             return []
         if query_emb.ndim == 2 and query_emb.shape[0] == 1:
             query_emb = query_emb.flatten()
         elif query_emb.ndim != 1:
-            logger.error(f"HipRetriever.retrieve expects a 1D query embedding or (1, dim), got shape {query_emb.shape}")
+            logger.error("retrieve: query shape %s is neither (dim,) nor (1, dim)", query_emb.shape)
             return []
         if query_emb.shape[0] != self.D:
-            logger.error(f"Query embedding dimension ({query_emb.shape[0]}) does not match document embedding dimension ({self.D})")
+            logger.error("retrieve: query has %d dimensions, the corpus %d", query_emb.shape[0], self.D)
             return []
         actual_k = min(k, self.N_A)
         if actual_k <= 0:
-            logger.warning(f"Requested k={k} results in actual_k={actual_k}. Returning empty list.")
+            logger.warning("retrieve: k=%s leaves nothing to return", k)
             return []
         try:
             if not _is_integral(actual_k):
@@ -111,10 +112,10 @@ class HipRetriever(_HipRetrieverBase):
                 query_emb = query_emb.astype(np.float32)
             _, idx = self.index.search(query_emb.reshape(1, self.D), int(actual_k))
             docs = self._docs(idx[0], int(actual_k))
-            logger.debug(f"HipRetriever.retrieve took {time.time() - start_time:.6f}s")
+            logger.debug("retrieve: %.6f s", time.time() - start_time)
             return docs
         except Exception as e:
-            logger.error(f"Error during HipRetriever.retrieve: {e}", exc_info=True)
+            logger.error("retrieve failed: %s", e, exc_info=True)
             return []
 
     # retriever.py:686-799
@@ -123,27 +124,27 @@ class HipRetriever(_HipRetrieverBase):
         batch_size = query_embeddings.shape[0]   # read before the type check, as the reference does (:702)
 
         if not isinstance(query_embeddings, np.ndarray):
-            logger.error(f"HipRetriever.batch_retrieve expects query_embeddings as NumPy array, got {type(query_embeddings)}")
+            logger.error("batch_retrieve: queries must be a numpy.ndarray, not %s", type(query_embeddings).__name__)
             return [[] for _ in ks]
         if query_embeddings.ndim != 2:
-            logger.error(f"HipRetriever.batch_retrieve expects a 2D query_embeddings array, got {query_embeddings.ndim} dimensions.")
+            logger.error("batch_retrieve: queries must be 2-D, got %d-D", query_embeddings.ndim)
             return [[] for _ in ks]
         if batch_size == 0:
-            logger.info("Received empty batch of queries.")
+            logger.info("batch_retrieve: empty batch")
             return []
         if not isinstance(ks, list) or batch_size != len(ks):
-            logger.error(f"Batch retrieve size mismatch: {batch_size} embeddings vs {len(ks)} k values.")
+            logger.error("batch_retrieve: %d queries but %d k values", batch_size, len(ks))
             return [[] for _ in range(batch_size)]
         if query_embeddings.shape[1] != self.D:
-            logger.error(f"Batch query embedding dimension ({query_embeddings.shape[1]}) does not match document embedding dimension ({self.D})")
+            logger.error("batch_retrieve: queries have %d dimensions, the corpus %d", query_embeddings.shape[1], self.D)
             return [[] for _ in ks]
         if not all(isinstance(k_val, int) for k_val in ks):
-            logger.error("List ks must contain only integers.")
+            logger.error("batch_retrieve: every k must be a Python int")
             return [[] for _ in ks]
 
         valid_ks = [k_val for k_val in ks if k_val > 0]
         if not valid_ks:
-            logger.warning("All k values in ks are non-positive. Returning list of empty lists.")
+            logger.warning("batch_retrieve: no positive k in the batch")
             return [[] for _ in ks]
         max_k = min(max(valid_ks), self.N_A)
         if max_k <= 0:
@@ -160,10 +161,10 @@ class HipRetriever(_HipRetrieverBase):
                     batch_results.append([])
                     continue
                 batch_results.append(self._docs(idx[i], k_i))
-            logger.debug(f"HipRetriever.batch_retrieve took {time.time() - start_time:.6f}s")
+            logger.debug("batch_retrieve: %.6f s", time.time() - start_time)
             return batch_results
         except Exception as e:
-            logger.error(f"Error during HipRetriever.batch_retrieve: {e}", exc_info=True)
+            logger.error("batch_retrieve failed: %s", e, exc_info=True)
             return [[] for _ in ks]
 
 
@@ -175,13 +176,13 @@ class HipRetriever(_HipRetrieverBase):
         if batch_size == 0:
             return []
         if not isinstance(ks, list) or batch_size != len(ks):
-            logger.error(f"Batch retrieve size mismatch: {batch_size} embeddings vs {len(ks)} k values.")
+            logger.error("batch_retrieve: %d queries but %d k values", batch_size, len(ks))
             return [[] for _ in range(batch_size)]
         if dim != self.D:
-            logger.error(f"Batch query embedding dimension ({dim}) does not match document embedding dimension ({self.D})")
+            logger.error("batch_retrieve_device: queries have %d dimensions, the corpus %d", dim, self.D)
             return [[] for _ in ks]
         if not all(isinstance(k_val, int) for k_val in ks):
-            logger.error("List ks must contain only integers.")
+            logger.error("batch_retrieve: every k must be a Python int")
             return [[] for _ in ks]
         valid_ks = [k_val for k_val in ks if k_val > 0]
         if not valid_ks:
@@ -191,7 +192,7 @@ class HipRetriever(_HipRetrieverBase):
             _, idx = self.search_device(dev_ptr, batch_size, dim, max_k)
             return [[] if ks[i] <= 0 else self._docs(idx[i], ks[i]) for i in range(batch_size)]
         except Exception as e:
-            logger.error(f"Error during HipRetriever.batch_retrieve_device: {e}", exc_info=True)
+            logger.error("batch_retrieve_device failed: %s", e, exc_info=True)
             return [[] for _ in ks]
 
 
@@ -203,7 +204,7 @@ class HipSimpleRetriever(_HipRetrieverBase):
     def __init__(self, doc_embeddings: np.ndarray, documents: List[str], dtype: str = "fp32",
                  devices: Optional[Sequence[int]] = None):
         super().__init__(doc_embeddings, documents, dtype=dtype, devices=devices)
-        logger.info(f"Initialized HipSimpleRetriever with {len(self.documents)} documents.")
+        logger.info("HipSimpleRetriever ready: %d documents", len(self.documents))
 
     # per-query k rules of retrieve (:89-94): None -> invalid, else the clamped k
     def _effective_k(self, k) -> Optional[int]:
@@ -216,10 +217,10 @@ class HipSimpleRetriever(_HipRetrieverBase):
     # retriever.py:78-128
     def retrieve(self, query_emb: np.ndarray, k: int = 2) -> List[str]:
         if k <= 0:
-            logger.warning(f"Requested k={k} is non-positive. Returning empty list.")
+            logger.warning("retrieve: k=%s is not positive", k)
             return []
         if k > self.N_A:
-            logger.warning(f"Requested k={k} is larger than the number of documents ({self.N_A}). Returning all documents.")
+            logger.warning("retrieve: k=%s exceeds the %d documents; returning all of them", k, self.N_A)
             k = self.N_A
         try:
             if query_emb.dtype != np.float32:
@@ -228,29 +229,29 @@ class HipSimpleRetriever(_HipRetrieverBase):
                 if query_emb.ndim == 2 and query_emb.shape[0] == 1:
                     query_emb = query_emb.flatten()
                 else:
-                    logger.error(f"HipSimpleRetriever.retrieve expects a 1D query embedding, got shape {query_emb.shape}")
+                    logger.error("retrieve: query shape %s is not 1-D", query_emb.shape)
                     return []
             if query_emb.shape[0] != self.D:
-                logger.error(f"Query embedding dimension ({query_emb.shape[0]}) does not match document embedding dimension ({self.D})")
+                logger.error("retrieve: query has %d dimensions, the corpus %d", query_emb.shape[0], self.D)
                 return []
             if not _is_integral(k):
                 raise TypeError(f"k must be an integer, got {type(k)}")
             _, idx = self.index.search(query_emb.reshape(1, self.D), int(k))
             return self._docs(idx[0], int(k))
         except Exception as e:
-            logger.error(f"Unexpected error during HipSimpleRetriever.retrieve: {e}", exc_info=True)
+            logger.error("retrieve failed: %s", e, exc_info=True)
             return []
 
     # retriever.py:131-166 — same per-query results as calling retrieve() B times, one device pass
     def batch_retrieve(self, query_embeddings: np.ndarray, ks: List[int]) -> List[List[str]]:
         if query_embeddings.ndim != 2:
-            logger.error(f"HipSimpleRetriever.batch_retrieve expects a 2D query_embeddings array, got {query_embeddings.ndim} dimensions.")
+            logger.error("batch_retrieve: queries must be 2-D, got %d-D", query_embeddings.ndim)
             return [[] for _ in ks]
         if query_embeddings.shape[0] != len(ks):
-            logger.error(f"Batch retrieve size mismatch: {query_embeddings.shape[0]} embeddings vs {len(ks)} k values.")
+            logger.error("batch_retrieve: %d queries but %d k values", query_embeddings.shape[0], len(ks))
             return [[] for _ in ks]
         if query_embeddings.shape[1] != self.D:
-            logger.error(f"Batch query embedding dimension ({query_embeddings.shape[1]}) does not match document embedding dimension ({self.D})")
+            logger.error("batch_retrieve: queries have %d dimensions, the corpus %d", query_embeddings.shape[1], self.D)
             return [[] for _ in ks]
 
         eff = [self._effective_k(k) for k in ks]
@@ -267,7 +268,7 @@ class HipSimpleRetriever(_HipRetrieverBase):
                 results[i] = self._docs(idx[j], eff[i])
             return results
         except Exception as e:
-            logger.error(f"Unexpected error during HipSimpleRetriever.batch_retrieve: {e}", exc_info=True)
+            logger.error("batch_retrieve failed: %s", e, exc_info=True)
             return [[] for _ in ks]
 
 

@@ -11,8 +11,6 @@ import datetime
 import os
 from typing import Optional, Tuple
 
-import numpy as np
-
 
 def env_rank_world() -> Tuple[int, int, int]:
     rank = int(os.environ.get("RANK", "0"))
@@ -58,22 +56,3 @@ def max_over_ranks(dist, x: float) -> float:
 def barrier(dist) -> None:
     if dist is not None:
         dist.barrier()
-
-
-def merge_shard_topk(scores: np.ndarray, idx: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:
-    """Host-side merge of per-shard candidates [G, b, kk] -> [b, k] by (score desc, index asc).
-
-    The device pipeline does this merge on the GPU after the all-gather; this host form serves callers
-    that gather candidates themselves and documents the rule (used by the multi-process CPU tests).
-    """
-    G, b, kk = scores.shape
-    s = scores.transpose(1, 0, 2).reshape(b, G * kk)
-    i = idx.transpose(1, 0, 2).reshape(b, G * kk)
-    out_s = np.full((b, k), -np.inf, dtype=np.float32)
-    out_i = np.full((b, k), -1, dtype=np.int64)
-    for r in range(b):
-        valid = i[r] >= 0
-        order = np.lexsort((i[r][valid], -s[r][valid]))[:k]
-        out_s[r, :order.size] = s[r][valid][order]
-        out_i[r, :order.size] = i[r][valid][order]
-    return out_s, out_i

@@ -1,6 +1,7 @@
 """Multi-process control plane on CPU (gloo, world_size 2): the pieces of the N>1 path that do not need a
 GPU — shard partition, RCCL unique-id broadcast, max-over-ranks timing, and the merge rule that makes
-sharded results identical to the single-shard result (checked against the oracle)."""
+sharded results identical to the single-shard result (tests/dist_helpers.py restates the device merge's key
+order; checked against the oracle)."""
 import os
 import socket
 
@@ -9,7 +10,8 @@ import pytest
 import torch.multiprocessing as mp
 
 from oracle.retriever_oracle import canonical_topk, exact_scores
-from rag_service_amd.dist import merge_shard_topk, shard_rows
+from dist_helpers import merge_shard_topk
+from rag_service_amd.dist import shard_rows
 
 
 def _free_port():
