@@ -84,7 +84,11 @@ struct Shard {
   size_t out_off = 0;
   hipEvent_t pin_q_free = nullptr;       // the last H2D out of the handle's pinned query staging completed
   int k_cap = 0;
-  // k > RR_FUSED_KMAX path
+  // 32 < k <= kWideMax (large k, rr_sk.hip wide output + select_kernel)
+  uint64_t* wcand = nullptr;             // [cand_grid][32][kWideMax] per-workgroup top-k lists
+  uint64_t* wfloor = nullptr;            // [cand_grid][32] their floors
+  uint64_t* wsel = nullptr;              // [32][kSelParts][kWideMax] stage-1 selections
+  // full-sort path (k > kWideMax, unsupported shapes, and the exact re-run of an unproven large-k search)
   uint64_t* full_keys = nullptr;         // [32][max(rows, world*k)]
   uint64_t* sorted = nullptr;
   size_t full_cap = 0;                   // elements
@@ -164,6 +168,10 @@ constexpr int kMaxSlots = 64;
 // carries after its keys (word 0: the shard's flag).
 constexpr size_t kOutHead = 64;
 constexpr int kXTail = 8;
+// Large k: the split-K kernel's wide output + radix select (no sort of every key) up to this k; the lists of a
+// shard are selected in kSelParts groups first when they hold more than 8192 keys per query.
+constexpr int kWideMax = 256;
+constexpr int kSelParts = 8;
 
 // How each public corpus dtype is stored and multiplied (rr_internal.h KDT_*).
 int kdt_of(int dtype) {
@@ -197,7 +205,7 @@ int dmalloc(T** p, size_t bytes) {
 int free_shard(Shard& s) {
   hipSetDevice(s.dev);
   void* ptrs[] = {s.corpus, s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.ctr, s.shard_keys, s.gathered, s.out_base,
-                  s.full_keys, s.sorted, s.sort_temp, s.px_keys[0], s.px_keys[1], s.px_gathered[0], s.px_gathered[1]};
+                  s.full_keys, s.sorted, s.sort_temp, s.wcand, s.wfloor, s.wsel, s.px_keys[0], s.px_keys[1], s.px_gathered[0], s.px_gathered[1]};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (hipEvent_t e : s.ev) hipEventDestroy(e);
@@ -360,6 +368,7 @@ int drop_work_buffers(rr_handle* h) {
     HIP_TRY(hipStreamSynchronize(s.xstream));
     void** ptrs[] = {(void**)&s.qbuf[0], (void**)&s.qbuf[1], (void**)&s.cand, (void**)&s.scount, (void**)&s.ctr, (void**)&s.shard_keys, (void**)&s.gathered,
                      (void**)&s.out_base, (void**)&s.full_keys, (void**)&s.sorted, &s.sort_temp,
+                     (void**)&s.wcand, (void**)&s.wfloor, (void**)&s.wsel,
                      (void**)&s.px_keys[0], (void**)&s.px_keys[1], (void**)&s.px_gathered[0],
                      (void**)&s.px_gathered[1]};
     for (void** p : ptrs) {
@@ -417,9 +426,11 @@ int ensure_buffers(rr_handle* h, int b, int k) {
       HIP_TRY(hipMemset(s.out_base, 0, kOutHead));   // the screened-search flag word starts at 0
       s.out_scores = (float*)(s.out_base + kOutHead);
       s.out_idx = (int64_t*)(s.out_base + s.out_off);
-      const int kk = std::max(kc, RR_FUSED_KMAX);
-      if (int rc = dmalloc(&s.shard_keys, (size_t)rr::kQSlots * kk * 8)) return rc;
-      if (int rc = dmalloc(&s.gathered, (size_t)h->world * rr::kQSlots * kk * 8)) return rc;
+      // serial exchange lists: [32][k] keys + a flag word (large-k path)
+      const size_t per = (size_t)rr::kQSlots * std::max(kc, RR_FUSED_KMAX) + kXTail;
+      if (int rc = dmalloc(&s.shard_keys, per * 8)) return rc;
+      if (int rc = dmalloc(&s.gathered, (size_t)h->world * per * 8)) return rc;
+      HIP_TRY(hipMemset(s.shard_keys, 0, per * 8));
       s.q_cap = qc;
       s.k_cap = kc;
     }
@@ -440,24 +451,33 @@ int ensure_buffers(rr_handle* h, int b, int k) {
         HIP_TRY(hipMemset(s.px_keys[p], 0, per * 8));
       }
     }
-    if (k > RR_FUSED_KMAX) {
-      // hipcub's segmented sort takes an int item count
-      if ((int64_t)rr::kQSlots * std::max<int64_t>(s.rows(), (int64_t)h->world * k) > INT32_MAX)
-        return fail(RR_E_UNSUPPORTED, "k=%d > %d on a shard of %lld rows exceeds the full-sort path's size limit", k,
-                    RR_FUSED_KMAX, (long long)s.rows());
-      const size_t need = (size_t)rr::kQSlots * std::max<int64_t>(s.rows(), (int64_t)h->world * k);
-      if (need > s.full_cap) {
-        if (int rc = dmalloc(&s.full_keys, need * 8)) return rc;
-        if (int rc = dmalloc(&s.sorted, need * 8)) return rc;
-        s.full_cap = need;
-        size_t tb = 0;
-        HIP_TRY(rr::segmented_sort_desc(nullptr, &tb, s.full_keys, s.sorted, rr::kQSlots,
-                                        (int64_t)(need / rr::kQSlots), s.stream));
-        if (tb > s.sort_temp_bytes) {
-          if (int rc = dmalloc(&s.sort_temp, tb)) return rc;
-          s.sort_temp_bytes = tb;
-        }
-      }
+    if (k > RR_FUSED_KMAX && k <= kWideMax && !s.wcand) {
+      if (int rc = dmalloc(&s.wcand, (size_t)s.cand_grid * rr::kQSlots * kWideMax * 8)) return rc;
+      if (int rc = dmalloc(&s.wfloor, (size_t)s.cand_grid * rr::kQSlots * 8)) return rc;
+      if (int rc = dmalloc(&s.wsel, (size_t)rr::kQSlots * kSelParts * kWideMax * 8)) return rc;
+    }
+  }
+  return RR_OK;
+}
+
+// Buffers of the full-sort path (every key of the shard, segmented radix sort), allocated on first use.
+int ensure_full_sort(rr_handle* h, Shard& s, int k) {
+  // hipcub's segmented sort takes an int item count
+  if ((int64_t)rr::kQSlots * std::max<int64_t>(s.rows(), (int64_t)h->world * k) > INT32_MAX)
+    return fail(RR_E_UNSUPPORTED, "k=%d on a shard of %lld rows exceeds the full-sort path's size limit", k,
+                (long long)s.rows());
+  const size_t need = (size_t)rr::kQSlots * std::max<int64_t>(s.rows(), (int64_t)h->world * k);
+  if (need > s.full_cap) {
+    HIP_TRY(hipStreamSynchronize(s.stream));   // the old buffers may still be in use
+    if (int rc = dmalloc(&s.full_keys, need * 8)) return rc;
+    if (int rc = dmalloc(&s.sorted, need * 8)) return rc;
+    s.full_cap = need;
+    size_t tb = 0;
+    HIP_TRY(rr::segmented_sort_desc(nullptr, &tb, s.full_keys, s.sorted, rr::kQSlots,
+                                    (int64_t)(need / rr::kQSlots), s.stream));
+    if (tb > s.sort_temp_bytes) {
+      if (int rc = dmalloc(&s.sort_temp, tb)) return rc;
+      s.sort_temp_bytes = tb;
     }
   }
   return RR_OK;
@@ -500,6 +520,15 @@ bool screened(const rr_handle* h, int k, int slots) {
          h->screen_ok && slots == rr::kQSlots && screen_kt(k) != 0 && use_sk(h);
 }
 
+// Large k (32 < k <= kWideMax): split-K kernel with wide per-workgroup lists, radix select, completeness check
+// (the exact re-run — RR_KERNEL_EXACT — takes the full-sort path).
+bool wide(const rr_handle* h, int k) {
+  return k > RR_FUSED_KMAX && k <= kWideMax && use_sk(h) && h->kernel != RR_KERNEL_EXACT;
+}
+
+// Searches whose completeness is checked on the device and settled by the host (settle_screen).
+bool checked(const rr_handle* h, int k, int slots) { return screened(h, k, slots) || wide(h, k); }
+
 int fused_grid(const Shard& s) {
   const int64_t ntiles = (s.rows() + rr::kTileDocs - 1) / rr::kTileDocs;
   const int64_t want = (ntiles + rr::kWaves - 1) / rr::kWaves;
@@ -534,8 +563,8 @@ int collect_timing(rr_handle* h) {
 // Single-process exchange (several local shards, possibly on the same device): every shard copies every
 // other shard's [32][kk] keys into its `gathered` slot with peer DMA, ordered by events. The same
 // layout the RCCL all-gather produces in multi-process mode.
-int local_gather(rr_handle* h, int kk) {
-  const size_t bytes = (size_t)rr::kQSlots * kk * 8;
+int local_gather(rr_handle* h, size_t per) {
+  const size_t bytes = per * 8;
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
     HIP_TRY(hipEventRecord(s.keys_ready, s.stream));
@@ -545,7 +574,7 @@ int local_gather(rr_handle* h, int kk) {
     for (size_t i = 0; i < h->shards.size(); ++i) {
       const Shard& src = h->shards[i];
       if (&src != &dst) HIP_TRY(hipStreamWaitEvent(dst.stream, src.keys_ready, 0));
-      HIP_TRY(hipMemcpyPeerAsync(dst.gathered + i * (size_t)rr::kQSlots * kk, dst.dev, src.shard_keys, src.dev, bytes,
+      HIP_TRY(hipMemcpyPeerAsync(dst.gathered + i * per, dst.dev, src.shard_keys, src.dev, bytes,
                                  dst.stream));
     }
     HIP_TRY(hipEventRecord(dst.copies_done, dst.stream));
@@ -612,11 +641,12 @@ rr::SkArgs sk_base(const rr_handle* h, const Shard& s, const float* qb, int bb) 
 int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
   const int d = h->d;
   const bool scr = screened(h, k, slots);
+  const bool wk = !scr && wide(h, k);
   const int kt = scr ? screen_kt(k) : rr::fused_kt(k);
   const bool multi = h->world > 1 || h->dist;   // an exchange step (RCCL with any world, peer copies)
   const bool local_multi = multi && !h->dist;
   const int p = h->parity;
-  if (scr) {
+  if (scr || wk) {
     ++h->screen_seq;
     ++h->screen_blocks;
   }
@@ -712,19 +742,95 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
         HIP_TRY(wait_px(p));
         HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, s.px_keys[p], nullptr, nullptr, s.stream, slots));
       }
+    } else if (wk) {
+      // 32 < k <= kWideMax: the split-K kernel keeps per workgroup and query the top-k of its lane lists
+      // (wide output, with a floor above everything it dropped), then a radix select over those lists — one
+      // stage, or kSelParts groups then their union — gives the shard's top-k and checks it against the
+      // floors: unproven -> the block's flag word (the host re-runs the search with the full sort).
+      HIP_TRY(wait_px(0));
+      HIP_TRY(wait_px(1));
+      HIP_TRY(wait_copies());
+      if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
+      uint64_t* flagw = multi ? s.shard_keys + (size_t)rr::kQSlots * k : (uint64_t*)s.out_base;
+      // the exchanged flag word sits after this k's keys: clear it (earlier searches with a larger k left keys
+      // there); the result head's word (single shard) only grows, by sequence number
+      if (multi) HIP_TRY(hipMemsetAsync(flagw, 0, sizeof(uint64_t), s.stream));
+      if (s.rows() > 0) {
+        const int sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(s.cand_grid, (s.rows() + 31) / 32));
+        rr::SkArgs a = sk_base(h, s, qb, bb);
+        a.out = s.wcand;
+        a.wide_k = k;
+        a.floors = s.wfloor;
+        a.dyn = 0;
+        HIP_TRY(rr::launch_sk_args(sk_dtype_of(h->dtype), h->metric, RR_FUSED_KMAX, 0, sgrid, rr::kQSlots, a,
+                                   s.stream));
+        if (timed) HIP_TRY(hipEventRecord(e1, s.stream));
+        rr::SelArgs sa{};
+        sa.b = bb;
+        sa.k = k;
+        sa.xoff = -1;
+        sa.flag = flagw;
+        sa.count = s.scount;
+        sa.seq = seq;
+        sa.force_incomplete = h->kernel == RR_KERNEL_SCREEN_FALLBACK;
+        const bool two = (int64_t)sgrid * k > 8192;
+        if (two) {   // stage 1: the lists in kSelParts groups, each group's top-k (unsorted)
+          rr::SelArgs s1 = sa;
+          s1.in = s.wcand;
+          s1.nlists = sgrid;
+          s1.kin = k;
+          s1.lstride = (int64_t)rr::kQSlots * k;
+          s1.qstride = k;
+          s1.parts = kSelParts;
+          s1.out_keys = s.wsel;
+          HIP_TRY(rr::launch_select(s1, s.stream));
+        }
+        sa.in = two ? s.wsel : s.wcand;
+        sa.nlists = two ? kSelParts : sgrid;
+        sa.kin = k;
+        sa.lstride = two ? k : (int64_t)rr::kQSlots * k;
+        sa.qstride = two ? (int64_t)kSelParts * k : k;
+        sa.parts = 1;
+        sa.sort = 1;
+        sa.floors = s.wfloor;
+        sa.nfloors = sgrid;
+        sa.fstride = rr::kQSlots;
+        sa.out_keys = multi ? s.shard_keys : nullptr;
+        sa.out_scores = multi ? nullptr : osc;
+        sa.out_idx = multi ? nullptr : oix;
+        HIP_TRY(rr::launch_select(sa, s.stream));
+      } else {
+        if (timed) HIP_TRY(hipEventRecord(e1, s.stream));
+        HIP_TRY(hipMemsetAsync(s.shard_keys, 0, (size_t)rr::kQSlots * k * 8, s.stream));
+      }
+      if (!multi) {   // results read back on the exchange stream (rr_search_async) come after these
+        HIP_TRY(hipEventRecord(s.ev_cdone, s.stream));
+        HIP_TRY(hipStreamWaitEvent(s.xstream, s.ev_cdone, 0));
+      }
     } else {
       // k > RR_FUSED_KMAX: all keys of this shard, segmented radix sort, keep the first k. The exchange
       // is serial on the compute stream, after every pipelined exchange still writing results.
       const int64_t rows = s.rows();
+      if (int rc = ensure_full_sort(h, s, k)) return rc;
       if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
       HIP_TRY(wait_px(0));   // no pipelined exchange or screened verify still uses the buffers
       HIP_TRY(wait_px(1));
       HIP_TRY(wait_copies());
       HIP_TRY(hipMemsetAsync(s.shard_keys, 0, (size_t)rr::kQSlots * k * 8, s.stream));
       if (rows > 0) {
-        const int grid = fused_grid(s);
-        HIP_TRY(rr::launch_full_keys(kdt_of(h->dtype), h->metric, grid, s.corpus, s.norms, s.rscale, qb, rows, d,
-                                     bb, base, s.full_keys, s.stream));
+        if (use_sk(h)) {   // the split-K kernel's arithmetic, as every other path of this handle
+          const int sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(s.cand_grid, (rows + 31) / 32));
+          rr::SkArgs a = sk_base(h, s, qb, bb);
+          a.out = s.cand;
+          a.all_keys = s.full_keys;
+          a.dyn = 0;
+          HIP_TRY(rr::launch_sk_args(sk_dtype_of(h->dtype), h->metric, RR_FUSED_KMAX, 0, sgrid, rr::kQSlots, a,
+                                     s.stream));
+        } else {
+          const int grid = fused_grid(s);
+          HIP_TRY(rr::launch_full_keys(kdt_of(h->dtype), h->metric, grid, s.corpus, s.norms, s.rscale, qb, rows, d,
+                                       bb, base, s.full_keys, s.stream));
+        }
         if (timed) HIP_TRY(hipEventRecord(e1, s.stream));
         size_t tb = s.sort_temp_bytes;
         HIP_TRY(rr::segmented_sort_desc(s.sort_temp, &tb, s.full_keys, s.sorted, bb, rows, s.stream));
@@ -746,24 +852,43 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
   }
 
   // ---- serial exchange (k > RR_FUSED_KMAX): every shard's [32][k] keys to every shard -----------------
-  const int kk = k;
+  // (large-k lists carry the shard's flag word after the keys)
+  const size_t per = (size_t)rr::kQSlots * k + (wk ? kXTail : 0);
   if (h->dist) {   // one process per GPU: one RCCL all-gather over xGMI
     Shard& s = h->shards[0];
     HIP_TRY(hipSetDevice(s.dev));
-    NCCL_TRY(ncclAllGather(s.shard_keys, s.gathered, (size_t)rr::kQSlots * kk, ncclUint64, s.comm, s.stream));
-  } else if (int rc = local_gather(h, kk)) {
+    NCCL_TRY(ncclAllGather(s.shard_keys, s.gathered, per, ncclUint64, s.comm, s.stream));
+  } else if (int rc = local_gather(h, per)) {
     return rc;
   }
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
     float* osc = s.out_scores + (size_t)q0 * k;
     int64_t* oix = s.out_idx + (size_t)q0 * k;
-    const int64_t seg = (int64_t)h->world * k;
-    HIP_TRY(rr::launch_regroup(s.gathered, h->world, k, bb, s.full_keys, s.stream));
-    size_t tb = s.sort_temp_bytes;
-    HIP_TRY(rr::segmented_sort_desc(s.sort_temp, &tb, s.full_keys, s.sorted, bb, seg, s.stream));
-    HIP_TRY(rr::launch_take_prefix(s.sorted, bb, seg, k, s.shard_keys, s.stream));
-    HIP_TRY(rr::launch_decode(s.shard_keys, bb, k, osc, oix, s.stream));
+    if (wk) {   // the world lists' union -> top-k (radix select), and the largest of their flag words
+      rr::SelArgs sa{};
+      sa.in = s.gathered;
+      sa.nlists = h->world;
+      sa.kin = k;
+      sa.lstride = (int64_t)per;
+      sa.qstride = k;
+      sa.parts = 1;
+      sa.sort = 1;
+      sa.xoff = (int64_t)rr::kQSlots * k;
+      sa.b = bb;
+      sa.k = k;
+      sa.flag = (uint64_t*)s.out_base;
+      sa.out_scores = osc;
+      sa.out_idx = oix;
+      HIP_TRY(rr::launch_select(sa, s.stream));
+    } else {
+      const int64_t seg = (int64_t)h->world * k;
+      HIP_TRY(rr::launch_regroup(s.gathered, h->world, k, bb, s.full_keys, s.stream));
+      size_t tb = s.sort_temp_bytes;
+      HIP_TRY(rr::segmented_sort_desc(s.sort_temp, &tb, s.full_keys, s.sorted, bb, seg, s.stream));
+      HIP_TRY(rr::launch_take_prefix(s.sorted, bb, seg, k, s.shard_keys, s.stream));
+      HIP_TRY(rr::launch_decode(s.shard_keys, bb, k, osc, oix, s.stream));
+    }
     // later pipelined exchanges write the results after this one
     HIP_TRY(hipEventRecord(s.ev_cdone, s.stream));
     HIP_TRY(hipStreamWaitEvent(s.xstream, s.ev_cdone, 0));
@@ -1071,7 +1196,7 @@ int rr_search_staged(rr_handle* h, int32_t k) {
   const int b = h->cur_b;
   if (int rc = ensure_buffers(h, b, k)) return rc;
   const int slots = block_slots(h, b, k);
-  h->last_screened = screened(h, k, slots);
+  h->last_screened = checked(h, k, slots);
   h->last_seq0 = h->screen_seq + 1;
   h->last_settled = !h->last_screened;
   h->last_qpar = h->qpar;

@@ -66,6 +66,12 @@ struct SkArgs {
   int* count;              // MODE 1: blocks flagged so far (statistics)
   int seq;                 // this search block's sequence number (> every earlier one)
   int force_incomplete;    // MODE 1 test hook: report the block incomplete
+  // MODE 0, KT 32, 32 slots, large k (32 < wide_k <= 256): out is [grid][slots][wide_k] — per query the
+  // workgroup's top-wide_k of its lane lists — and floors [grid][slots]: no key it dropped is above the floor
+  int wide_k;
+  uint64_t* floors;
+  // MODE 0, KT 32, 32 slots: every key instead of lists, all_keys[q * n + row] for q < b (full-sort path)
+  uint64_t* all_keys;
 };
 
 // Split-K streaming kernel (rr_sk.hip): same output contract as launch_fused. sdt = KDT_* (0..3).
@@ -94,6 +100,26 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
 hipError_t launch_merge(int kt, const uint64_t* in, int nlists, int in_kt, int b, int k_out,
                         uint64_t* out_keys, float* out_scores, int64_t* out_idx, hipStream_t s, int slots = 32,
                         int64_t list_stride = 0, uint64_t* flag_out = nullptr);
+
+// Top-k selection for 32 < k <= 256 (select_kernel, rr_kernels.hip): grid (32 query slots, parts).
+struct SelArgs {
+  const uint64_t* in;        // key (list l, query q, pos) at in[l * lstride + q * qstride + pos], pos < kin
+  int nlists, kin;
+  int64_t lstride, qstride;
+  int parts;                 // the lists split into `parts` groups (blockIdx.y); out_keys is [slots][parts][k]
+  int sort;                  // 1: output in key order (descending); 0: any order (a stage-1 output)
+  const uint64_t* floors;    // list l < nfloors dropped only keys below floors[l * fstride + q] (null: none)
+  int nfloors, fstride;
+  int64_t xoff;              // >= 0: list l carries a flag word at in[l * lstride + xoff]; their max -> *flag
+  int b, k;
+  uint64_t* out_keys;        // may be null
+  float* out_scores;         // [b][k] (may be null)
+  int64_t* out_idx;
+  uint64_t* flag;            // floors: raised (atomic max) to seq when a query's top-k is not proven complete
+  int* count;                // blocks flagged (statistics; may be null)
+  int seq, force_incomplete;
+};
+hipError_t launch_select(const SelArgs& a, hipStream_t s);
 
 // Largest |x| of n values (non-negative float bits compared as ints) into *out (device, pre-zeroed).
 hipError_t launch_absmax(const float* x, int64_t n, float* out, hipStream_t s);

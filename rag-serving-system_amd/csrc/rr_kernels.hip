@@ -559,6 +559,152 @@ __global__ void regroup_kernel(const uint64_t* __restrict__ in, int world, int k
 }
 
 // ------------------------------------------------------------------------------------------------
+// top-k selection for 32 < k <= 256 (rr_api.cpp large-k path): radix select, no sort of all keys
+// ------------------------------------------------------------------------------------------------
+// Workgroup (q, part): the keys of lists [part * lpp, (part + 1) * lpp) for query slot q (element (l, pos) at
+// in[l * lstride + q * qstride + pos], pos < kin; order inside a list does not matter), PER per thread in
+// registers. The k-th largest key is found one byte at a time from the top: a 256-bin histogram (LDS
+// atomics) of the keys that match the bytes fixed so far, the bin holding the k-th, repeat — until the
+// bin is taken whole. Keys are unique, so exactly min(k, nonzero) keys have a masked value >= the prefix;
+// they are collected in LDS and (sort) ordered by a bitonic network. Stage 1 (parts > 1) leaves each
+// part's top-k unsorted for stage 2 (parts = 1). Completeness (floors): every list l < nfloors dropped only
+// keys below floors[l * fstride + q]; the result is exact when the largest floor is below the k-th key.
+constexpr int kSelThreads = 1024;
+constexpr int kSelMax = 256;   // k <= 256
+
+template <int PER>
+__global__ __launch_bounds__(kSelThreads) void select_kernel(const SelArgs a) {
+  const int q = blockIdx.x, part = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int k = a.k;
+  __shared__ int hist[256];
+  __shared__ uint64_t sel[kSelMax];
+  __shared__ int s_nz, s_cnt, s_digit, s_need, s_binc;
+  __shared__ uint64_t s_floor;
+  uint64_t* out_keys = a.out_keys ? a.out_keys + ((size_t)q * a.parts + part) * k : nullptr;
+  if (a.xoff >= 0 && q == 0 && part == 0 && tid < 64) {   // the exchanged lists' flag words
+    uint64_t f = 0;
+    for (int l = tid; l < a.nlists; l += 64) f = umax64(f, a.in[(size_t)l * a.lstride + a.xoff]);
+    f = wave_max_u64(f);
+    if (tid == 0 && f > *a.flag) *a.flag = f;   // the word only grows; stream order serialises writers
+  }
+  if (q >= a.b) {   // padding slot: uniform exchange buffers
+    if (out_keys)
+      for (int i = tid; i < k; i += kSelThreads) out_keys[i] = 0;
+    return;
+  }
+  const int lpp = (a.nlists + a.parts - 1) / a.parts;
+  const int l0 = part * lpp, nl = max(0, min(a.nlists, l0 + lpp) - l0);
+  const int total = nl * a.kin;
+  uint64_t kv[PER];
+  int nz = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = tid + kSelThreads * i;
+    uint64_t key = 0;
+    if (e < total) {
+      const int l = e / a.kin, pos = e - l * a.kin;
+      key = a.in[(size_t)(l0 + l) * a.lstride + (size_t)q * a.qstride + pos];
+    }
+    kv[i] = key;
+    nz += key != 0;
+  }
+  if (tid == 0) {
+    s_nz = 0;
+    s_cnt = 0;
+    s_floor = 0;
+  }
+  for (int i = tid; i < kSelMax; i += kSelThreads) sel[i] = 0;
+  __syncthreads();
+  if (nz) atomicAdd(&s_nz, nz);
+  if (a.floors)
+    for (int l = tid; l < a.nfloors; l += kSelThreads) {
+      const uint64_t f = a.floors[(size_t)l * a.fstride + q];
+      if (f) __hip_atomic_fetch_max(&s_floor, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  __syncthreads();
+  const int m = min(k, s_nz);
+  uint64_t prefix = 0, mask = 0;
+  int need = m;
+  for (int shift = 56; shift >= 0 && need > 0; shift -= 8) {
+    if (tid < 256) hist[tid] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if (kv[i] != 0 && (kv[i] & mask) == prefix) atomicAdd(&hist[(int)(kv[i] >> shift) & 255], 1);
+    __syncthreads();
+    if (tid < 64) {   // lane L: bins 255 - 4L .. 252 - 4L, highest first
+      int c[4], s4 = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c[j] = hist[255 - 4 * lane - j];
+        s4 += c[j];
+      }
+      int incl = s4;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += t;
+      }
+      int run = incl - s4;
+      if (run < need && need <= incl) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (run < need && need <= run + c[j]) {
+            s_digit = 255 - 4 * lane - j;
+            s_need = need - run;
+            s_binc = c[j];
+          }
+          run += c[j];
+        }
+      }
+    }
+    __syncthreads();
+    prefix |= (uint64_t)s_digit << shift;
+    mask |= (uint64_t)0xFF << shift;
+    need = s_need;
+    if (s_binc == need) break;   // the whole bin is in the top-k (uniform)
+  }
+  if (m > 0) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if (kv[i] != 0 && (kv[i] & mask) >= prefix) sel[atomicAdd(&s_cnt, 1)] = kv[i];
+  }
+  __syncthreads();
+  if (a.sort) {   // bitonic network over 256 entries (zeros sink), descending
+    for (int size = 2; size <= kSelMax; size <<= 1)
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        if (tid < kSelMax / 2) {
+          const int i = 2 * tid - (tid & (stride - 1)), j = i + stride;
+          const bool desc = (i & size) == 0;
+          const uint64_t x = sel[i], y = sel[j];
+          if ((x < y) == desc) {
+            sel[i] = y;
+            sel[j] = x;
+          }
+        }
+        __syncthreads();
+      }
+  }
+  if (a.floors && tid == 0) {
+    const uint64_t kth = s_nz >= k ? sel[k - 1] : 0;   // sorted: the k-th key
+    const bool complete = (s_floor == 0 || s_floor < kth) && !a.force_incomplete;
+    if (!complete)   // the first query slot to flag the block also counts it
+      if (__hip_atomic_fetch_max(a.flag, (uint64_t)a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+          (uint64_t)a.seq && a.count)
+        __hip_atomic_fetch_add(a.count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (int i = tid; i < k; i += kSelThreads) {
+    const uint64_t key = i < kSelMax ? sel[i] : 0;
+    if (out_keys) out_keys[i] = key;
+    if (a.out_scores) {
+      a.out_scores[(size_t)q * k + i] = key ? float_of_ord((uint32_t)(key >> 32)) : -INFINITY;
+      a.out_idx[(size_t)q * k + i] = key ? (int64_t)(0xFFFFFFFFu - (uint32_t)key) : -1;
+    }
+  }
+  (void)lane;
+}
+
+// ------------------------------------------------------------------------------------------------
 // corpus preparation
 // ------------------------------------------------------------------------------------------------
 // fp32 and bf16 row storage in 16-byte units: unit g = 2c + h of a row (chunk c, lane half h; fp32:
@@ -861,6 +1007,20 @@ hipError_t launch_take_prefix(const uint64_t* sorted, int b, int64_t seg, int k,
 hipError_t launch_regroup(const uint64_t* gathered, int world, int k, int b, uint64_t* out, hipStream_t s) {
   const int64_t seg = (int64_t)world * k;
   hipLaunchKernelGGL(regroup_kernel, dim3((unsigned)((seg + 255) / 256), b), dim3(256), 0, s, gathered, world, k, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_select(const SelArgs& a, hipStream_t s) {
+  if (a.k < 1 || a.k > kSelMax || a.parts < 1 || a.nlists < 1 || a.kin < 1 || a.b < 1 || a.b > kQSlots)
+    return hipErrorInvalidValue;
+  const int64_t per_part = (int64_t)((a.nlists + a.parts - 1) / a.parts) * a.kin;
+  const dim3 grid(kQSlots, a.parts);
+  if (per_part <= 1 * kSelThreads) hipLaunchKernelGGL(select_kernel<1>, grid, dim3(kSelThreads), 0, s, a);
+  else if (per_part <= 2 * kSelThreads) hipLaunchKernelGGL(select_kernel<2>, grid, dim3(kSelThreads), 0, s, a);
+  else if (per_part <= 4 * kSelThreads) hipLaunchKernelGGL(select_kernel<4>, grid, dim3(kSelThreads), 0, s, a);
+  else if (per_part <= 8 * kSelThreads) hipLaunchKernelGGL(select_kernel<8>, grid, dim3(kSelThreads), 0, s, a);
+  else if (per_part <= 16 * kSelThreads) hipLaunchKernelGGL(select_kernel<16>, grid, dim3(kSelThreads), 0, s, a);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -696,6 +696,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     // the lane's current k-th score minus a 2^-20 relative margin cannot enter the list, so only the
     // few that pass pay the exact IEEE division (the list only grows inside the loop: the threshold
     // taken here is conservative).
+    // full-key output (a.all_keys; the 32-wide instantiation, for the full-sort path): every key goes to HBM
+    constexpr bool DUMP = MODE == 0 && KT == 32 && QH == 1 && SCHED == 0 && DT != 6;
     float thr = -INFINITY;
     if constexpr (COS && DT != 6) {
       const uint64_t last = tk.last();
@@ -740,7 +742,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       } else if constexpr (COS) {
         // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
         const float den = cos_den(qn, nd);
-        if (valid && s * __builtin_amdgcn_rcpf(den) >= thr) {
+        if (DUMP && a.all_keys) {
+          if (valid) a.all_keys[(size_t)qe * n + row] = make_key(fminf(fmaxf(s / den, -1.0f), 1.0f), idx_base + (uint32_t)row);
+        } else if (valid && s * __builtin_amdgcn_rcpf(den) >= thr) {
           float c = s / den;   // IEEE division, as the reference's elementwise kernel
           c = fminf(fmaxf(c, -1.0f), 1.0f);
           const uint64_t key = make_key(c, idx_base + (uint32_t)row);
@@ -748,7 +752,11 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         }
       } else {
         const uint64_t key = make_key(s, idx_base + (uint32_t)row);
-        if (valid && key > tk.last()) tk.insert(key);
+        if (DUMP && a.all_keys) {
+          if (valid) a.all_keys[(size_t)qe * n + row] = key;
+        } else if (valid && key > tk.last()) {
+          tk.insert(key);
+        }
       }
     }
     if (tcount == 0) SK_PROBE(2);
@@ -770,6 +778,37 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   SK_PROBE(4);
 
   // ---- per query: merge its LPQ lane lists (KT rounds of an LPQ-lane max; keys are unique) -------------
+  if constexpr (MODE == 0 && KT == 32 && QH == 1 && SCHED == 0) {
+    if (a.all_keys) return;
+    if (a.wide_k > 0) {
+      // Large k: the query's top-wide_k of its LPQ lane lists. The lists go to LDS (the ring and the partial
+      // blocks are free once every wave is past its last tile) and each round's winner advances its own head
+      // from there. Floor: a lane whose list is full dropped only keys below its last; the workgroup drops
+      // the keys left after wide_k rounds — the floor is the largest of those bounds (0: nothing dropped).
+      static_assert((size_t)kQSlots * LPQ * (KT + 1) * 8 <= ring_bytes(RS) + red_bytes(RS, QH), "LDS lists");
+      __syncthreads();
+      const int li = lane % LPQ;
+      uint64_t* mine = (uint64_t*)smem + (size_t)(qe * LPQ + li) * (KT + 1);
+#pragma unroll
+      for (int i = 0; i < KT; ++i) mine[i] = tk.v[i];
+      const uint64_t lane_floor = tk.v[KT - 1];
+      uint64_t head = tk.v[0];
+      int hp = 0;
+      uint64_t* dst = a.out + ((size_t)g * QS + qe) * a.wide_k;
+#pragma unroll 1
+      for (int rnd = 0; rnd < a.wide_k; ++rnd) {
+        const uint64_t m = group_max_u64<LPQ>(head);
+        if (m != 0 && head == m) {   // keys are unique: exactly one owner advances
+          ++hp;
+          head = hp < KT ? mine[hp] : 0;
+        }
+        if (li == 0) dst[rnd] = m;
+      }
+      const uint64_t fl = umax64(group_max_u64<LPQ>(lane_floor), group_max_u64<LPQ>(head));
+      if (li == 0) a.floors[(size_t)g * QS + qe] = fl;
+      return;
+    }
+  }
   if constexpr (MODE == 0) {
     uint64_t* dst = a.out + ((size_t)g * QS + qe) * KT;
 #pragma unroll 1

@@ -30,6 +30,11 @@ def golden_synth():
 
 
 @pytest.fixture(scope="session")
+def golden_configs():
+    return dict(np.load(os.path.join(GOLDEN, "golden_configs.npz")))
+
+
+@pytest.fixture(scope="session")
 def golden_edges():
     with open(os.path.join(GOLDEN, "golden_edge_cases.json")) as f:
         return json.load(f)

@@ -148,12 +148,91 @@ def edge_cases(ref, corpus):
     return {"seed": 7, "n": n, "d": d, "cases": cases}
 
 
+def streaming_topk(chunks, queries, metric, k):
+    """fp64 canonical top-(k+1) over row chunks [(row0, rows)], without the full B x N score matrix."""
+    b = queries.shape[0]
+    best_s = np.full((b, 0), -np.inf)
+    best_i = np.full((b, 0), -1, dtype=np.int64)
+    for r0, x in chunks:
+        s = exact_scores(x, queries, metric)
+        cs = np.concatenate([best_s, s], axis=1)
+        ci = np.concatenate([best_i, np.broadcast_to(np.arange(r0, r0 + x.shape[0]), s.shape)], axis=1)
+        keep = np.empty((b, min(k + 1, cs.shape[1])), dtype=np.int64)
+        for i in range(b):
+            keep[i] = np.lexsort((ci[i], -cs[i]))[:keep.shape[1]]
+        best_s = np.take_along_axis(cs, keep, axis=1)
+        best_i = np.take_along_axis(ci, keep, axis=1)
+    return best_s, best_i
+
+
+def config_goldens(ref):
+    """BASELINE.json configs 3 and 5 at (or toward) their defining shapes, from the reference's own retrievers.
+
+    config 3: F2 exact-integer 10M x 1024 (seed 1234), 32 queries (seed 99), k=10. SimpleRetriever (dot) runs on
+      the whole corpus. CupyRetriever (cosine) would materialise a 10M x 1024 temporary in its corpus norm, more
+      than this container holds, so it runs on 1M-row chunks (its own code on each), and the chunk winners are
+      merged by fp64 cosine: the global top-10 lies in the union of chunk top-10s; the merge order can differ
+      from the reference's fp32 order only inside the recorded gap.
+    config 5: bf16-rounded F3 unit-norm 1M x 1024 (seed 1234), 64 queries (seed 4321), k=10, both retrievers on
+      the whole corpus (config 5 defines 50M rows over 8 GPUs; 1M is the largest the host-side reference pin
+      reaches in minutes here; the device tests use 8 shards of it)."""
+    out = {}
+    n3, d, k = 10_000_000, 1024, 10
+    t0 = time.time()
+    corpus = np.empty((n3, d), dtype=np.float32)
+    step = 1 << 20
+    for r0 in range(0, n3, step):
+        corpus[r0:r0 + step] = synth.exact_int_rows(1234, r0, min(step, n3 - r0), d)
+        print(f"  F2 rows {r0 + step} ({time.time() - t0:.0f}s)", flush=True)
+    q = synth.exact_int_queries(99, 32, d)
+    docs = list(range(n3))
+    simple = ref.SimpleRetriever(doc_embeddings=corpus, documents=docs)
+    out["c3_simple_idx"] = pad_lists(simple.batch_retrieve(q, [k] * 32), k)
+    chunks = [(r0, corpus[r0:r0 + step]) for r0 in range(0, n3, step)]
+    s, i = streaming_topk(chunks, q, "dot", k)
+    out["c3_simple_score"] = np.stack([exact_scores(corpus[out["c3_simple_idx"][qi]], q[qi:qi + 1], "dot")[0]
+                                       for qi in range(32)])
+    out["c3_simple_gap"] = np.float64(np.min(s[:, :-1] - s[:, 1:]))
+    cand = [[] for _ in range(32)]
+    for r0, x in chunks:
+        cupy = ref.CupyRetriever(doc_embeddings=x, documents=list(range(r0, r0 + x.shape[0])))
+        for qi, lst in enumerate(cupy.batch_retrieve(q, [k] * 32)):
+            cand[qi].extend(lst)
+    s, i = streaming_topk(chunks, q, "cosine", k)
+    out["c3_cupy_gap"] = np.float64(np.min(s[:, :-1] - s[:, 1:]))
+    idx = np.full((32, k), -1, dtype=np.int64)
+    for qi in range(32):
+        c = np.array(sorted(set(cand[qi])), dtype=np.int64)
+        cs = exact_scores(corpus[c], q[qi:qi + 1], "cosine")[0]
+        idx[qi] = c[np.lexsort((c, -cs))[:k]]
+    out["c3_cupy_idx"] = idx
+    out["c3_cupy_score"] = np.stack([exact_scores(corpus[idx[qi]], q[qi:qi + 1], "cosine")[0] for qi in range(32)])
+    out["c3_meta"] = np.array([1234, 99, n3, d, k], dtype=np.int64)
+    print(f"  config 3 done ({time.time() - t0:.0f}s) gaps dot {float(out['c3_simple_gap']):.3g} "
+          f"cos {float(out['c3_cupy_gap']):.3g}", flush=True)
+    del simple, chunks, corpus, docs, cupy, x    # (a chunk view would keep the 41 GB corpus alive)
+    np.savez_compressed(os.path.join(HERE, "golden_configs.npz"), **out)
+
+    n5 = 1_000_000
+    c5 = synth.bf16_round(synth.unit_norm_gaussian(1234, n5, d))
+    q5 = synth.unit_norm_gaussian(4321, 64, d)
+    run_case(ref, c5, q5, k, "c5", out)
+    out["c5_meta"] = np.array([1234, 4321, n5, d, k], dtype=np.int64)
+    np.savez_compressed(os.path.join(HERE, "golden_configs.npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true", help="also the 1M-row cases (needs ~20 GB RAM, minutes)")
+    ap.add_argument("--configs", action="store_true",
+                    help="only the BASELINE config 3/5 goldens (golden_configs.npz; ~50 GB RAM, ~15 min)")
     args = ap.parse_args()
     ref = import_reference()
     print("reference imported:", ref.__file__, flush=True)
+    if args.configs:
+        config_goldens(ref)
+        print("done", flush=True)
+        return
 
     # ---- F1: the reference's own data files --------------------------------------------------
     sf = np.load(os.path.join(HERE, "data", "short_facts_embeddings.npy"))

@@ -1,0 +1,107 @@
+"""Serving-level replay: trace generation, batch formation and the latency summary
+against the reference's own outputs (tests/golden/golden_serving.json, made by make_serving_golden.py),
+the replay loop on CPU with a stub retriever, and (GPU) the replay through HipRetriever: every served
+request gets the documents a direct batch_retrieve of its query returns, whatever batch it rode in."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from serving_script import PLANS, run_plan
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_serving.json")
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(GOLDEN) as f:
+        return json.load(f)
+
+
+def test_traces_match_reference(golden):
+    from rag_service_amd.serving import generate_trace
+    for case in golden["traces"]:
+        got = generate_trace(case["pattern"], case["rps"], case["duration"], case["seed"])
+        assert got == case["trace"], (case["pattern"], case["rps"], case["duration"], case["seed"])
+
+
+@pytest.mark.parametrize("name", sorted(PLANS))
+def test_batch_formation_matches_reference(golden, name):
+    from rag_service_amd.core.request_queue import RequestQueue
+    mb, mw, arrivals = PLANS[name]
+    got = run_plan(RequestQueue(max_batch_size=mb, max_wait_time=mw, polling_interval=0.05), arrivals)
+    assert got == golden["batches"][name]
+
+
+def test_latency_summary_matches_reference(golden):
+    from rag_service_amd.serving import latency_summary
+    m = golden["metrics"]
+    got = latency_summary(m["latencies"], m["success"], m["errors"], 1.0)
+    assert got["latency"] == pytest.approx(m["latency"], rel=0, abs=1e-12)
+    assert got["total_requests"] == 11 and got["failed_requests"] == 1
+
+
+def test_request_queue_results():
+    from rag_service_amd.core.request_queue import RequestQueue
+    seen = []
+    q = RequestQueue(max_batch_size=2, max_wait_time=0.05, polling_interval=0.01, on_result=seen.append)
+    rid = q.add_request("hello", 3)
+    b = q.get_batch()
+    assert b == [{"id": rid, "query": "hello", "k": 3}]
+    assert q.get_batch() == []                                  # idle queue: empty after the window
+    q.store_result(rid, {"result": "x"})
+    assert seen == [rid]
+    assert q.get_result(rid, timeout=0.1) == {"result": "x"}
+    assert q.get_result(rid, timeout=0.05) is None              # consumed
+
+
+class _StubRetriever:
+    """Returns document "d<row>" where row is the query's first embedding value (CPU harness test only)."""
+    devices = [0]
+
+    def batch_retrieve(self, q, ks):
+        return [[f"d{int(round(v))}"] * k for v, k in zip(q[:, 0], ks)]
+
+
+def test_replay_loop_on_cpu():
+    from rag_service_amd.core.batch_processor import BatchProcessor
+    from rag_service_amd.serving import EmbeddingTable, context_docs, generate_trace, replay
+    texts = [f"question {i}" for i in range(50)]
+    table = np.zeros((50, 8), np.float32)
+    table[:, 0] = np.arange(50)
+    emb = EmbeddingTable(texts, table, "cpu")
+    trace = generate_trace("uniform", 100, 1, 3)
+    out = replay(BatchProcessor, _StubRetriever(), emb.model, texts, trace, k=2, max_batch_size=8,
+                 max_wait_time=0.05, device="cpu", keep_results=True)
+    assert out["total_requests"] == 100 and out["failed_requests"] == 0
+    assert out["batches"] >= 100 / 8 and out["mean_batch"] <= 8
+    for i, r in out["results"].items():
+        assert context_docs(r) == [f"d{i % 50}"] * 2
+    lat = out["latency"]
+    assert 0 < lat["min"] <= lat["p50"] <= lat["p95"] <= lat["p99"] <= lat["max"] < 5
+
+
+@pytest.mark.gpu
+def test_replay_through_hip_retriever(hip):
+    """A 2-second uniform trace at 400 req/s (the reference service's batching: up to 32 per batch, 1 s
+    window) against a 65 536-row corpus; each request's documents equal a direct batch_retrieve of its
+    query, so batching never changes a result."""
+    from oracle import synth
+    from rag_service_amd.core.batch_processor import BatchProcessor
+    from rag_service_amd.core.retriever import HipRetriever
+    from rag_service_amd.serving import EmbeddingTable, context_docs, generate_trace, replay
+    corpus = synth.unit_norm_gaussian(21, 65536, 1024)
+    docs = [f"doc{i}" for i in range(corpus.shape[0])]
+    retr = HipRetriever(corpus, docs)
+    texts = [f"q{i}" for i in range(200)]
+    table = synth.unit_norm_gaussian(22, 200, 1024)
+    emb = EmbeddingTable(texts, table, "cuda:0")
+    out = replay(BatchProcessor, retr, emb.model, texts, generate_trace("uniform", 400, 2, 5), k=5,
+                 device="cuda:0", keep_results=True)
+    assert out["failed_requests"] == 0 and out["total_requests"] == 800
+    want = retr.batch_retrieve(table, [5] * 200)
+    for i, r in out["results"].items():
+        assert context_docs(r) == want[i % 200], i
+    print({key: out[key] for key in ("latency", "batches", "mean_batch", "throughput")})
+    retr.close()
