@@ -104,6 +104,18 @@ __device__ __forceinline__ void glds16(const void* src, unsigned lds) {
       : "memory");
 }
 
+// The same with a scalar base address and a per-lane 32-bit offset (global saddr form): the per-slab address
+// arithmetic is then scalar; the lane offset is loop-invariant.
+__device__ __forceinline__ void glds16s(const void* sbase, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile(
+      "s_waitcnt lgkmcnt(0)\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds)
+      : "memory");
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
@@ -310,12 +322,24 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   const char* ring = smem + (size_t)w * RS * kSlabBytes;
   const char* lane_src = corpus + (size_t)w * KS + ((cl ^ rl) << 4);
 
+  // per-lane part of a slab address: row rl of each 8-row group, swizzled 16-byte column (< 8 rows: 32-bit)
+  const unsigned lane_off = (unsigned)(rl * row_bytes + ((cl ^ rl) << 4));
+  const char* wave_src = corpus + (size_t)w * KS;
   auto issue = [&](int64_t base, int j, int slot) {   // slab j (this wave's K-slice) of the tile at row base
+    if (base + 32 <= n) {   // whole tile (workgroup-uniform): scalar addresses
+      const int64_t sb = __builtin_amdgcn_readfirstlane((int)(base >> 32)) * 0x100000000ll +
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)base);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int64_t row = base + 8 * i + rl;
-      row = row < n ? row : n - 1;                    // partial last tile: re-read a valid row
-      glds16(lane_src + row * row_bytes + j * kSlabRowBytes, ring_lds + slot * kSlabBytes + i * 1024);
+      for (int i = 0; i < 4; ++i)
+        glds16s(wave_src + (sb + 8 * i) * row_bytes + j * kSlabRowBytes, lane_off,
+                ring_lds + slot * kSlabBytes + i * 1024);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int64_t row = base + 8 * i + rl;
+        row = row < n ? row : n - 1;                    // partial last tile: re-read a valid row
+        glds16(lane_src + row * row_bytes + j * kSlabRowBytes, ring_lds + slot * kSlabBytes + i * 1024);
+      }
     }
   };
   // wave 0: the per-row factors of the tile at row base into factor slot ts (lanes 0-31: the norm, or the
@@ -354,11 +378,23 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     }
   }
 
+  // Slabs in flight per wave: LA = 2 when a tile has at least two slabs — slab i + 2 is issued into slab i's
+  // slot as soon as slab i's fragments are in registers (before its MFMAs), so two slabs stay in flight through
+  // the MFMAs and the epilogue — else 1 (slab i + 1 issued before waiting for slab i).
+#ifndef RR_SK_LOOKAHEAD
+#define RR_SK_LOOKAHEAD 2
+#endif
+  constexpr int LA = NS >= 2 && QH == 1 ? RR_SK_LOOKAHEAD : 1;   // (64 slots: measured faster with 1)
+  int pend = 0;   // LA 2: vector-memory ops this wave issued after the slab it waits for next
   int64_t chunk = g, base = chunk * CT * 32;
   if constexpr (MODE == 0) {
-    if (chunk < C) {   // prologue: the first tile's factors and slab 0
+    if (chunk < C) {   // prologue: the first tile's factors and slab 0 (and 1)
       if (FX && w == 0) issue_factors(base, 0);
       issue(base, 0, 0);
+      if constexpr (LA == 2) {
+        issue(base, 1, 1);
+        pend = 4;
+      }
     }
   }
   // ---- query side: this wave's K-slice of every query as MFMA B operands, |q| and split exponents.
@@ -440,7 +476,37 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       }
     }
   };
-  if constexpr (DT != 2) build_frags();
+  // Pin the fragments: an empty asm that "rewrites" each one makes them opaque values, so they stay in VGPRs
+  // for the whole launch. Without it hipcc kept the fp32 query values instead and re-derived the fragments
+  // (mask, bf16 / f16 splits) inside the tile loop for every slab — the 64-slot bf16 kernel's main VALU cost.
+  auto pin_frags = [&]() {
+#pragma unroll
+    for (int qh = 0; qh < QH; ++qh)
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        if constexpr (DT == 0) {
+#pragma unroll
+          for (int m = 0; m < 16; ++m) asm volatile("" : "+v"(qfs[qh].v[j][m]));
+        } else if constexpr (DT == 1) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) asm volatile("" : "+v"(qfs[qh].hi[j][t]), "+v"(qfs[qh].lo[j][t]));
+        } else if constexpr (DT == 2) {
+#pragma unroll
+          for (int t = 0; t < 2; ++t) asm volatile("" : "+v"(qfs[qh].hi[j][t]), "+v"(qfs[qh].lo[j][t]));
+        } else if constexpr (DT == 3) {
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+            asm volatile("" : "+v"(qfs[qh].c0[j][t]), "+v"(qfs[qh].c1[j][t]), "+v"(qfs[qh].c2[j][t]));
+        } else {
+#pragma unroll
+          for (int t = 0; t < 2; ++t) asm volatile("" : "+v"(qfs[qh].c0[j][t]), "+v"(qfs[qh].c1[j][t]));
+        }
+      }
+  };
+  if constexpr (DT != 2) {
+    build_frags();
+    pin_frags();
+  }
   // ---- per-query scalars: |q| (cosine, fp32 as cp.linalg.norm, retriever.py:602), split exponents (DT 2),
   // sum |q| (DT 6 bound), max |q| (MODE 1: the screen's f16 range). All loads of a group of 4 queries are
   // issued before any is used (one L2/HBM latency per group, not one per query); the sums are the same
@@ -521,7 +587,10 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     __syncthreads();
   }
 
-  if constexpr (DT == 2) build_frags();
+  if constexpr (DT == 2) {
+    build_frags();
+    pin_frags();
+  }
 
   // ---- MODE 1: this query's candidates (the queries' fragments and scalars above are already built, so
   // their loads overlapped the list loads), then their rows straight into registers ---------------------------
@@ -574,9 +643,43 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     for (int qh = 0; qh < QH; ++qh)
 #pragma unroll
       for (int i = 0; i < 16; ++i) accs[qh][i] = 0.f;
+    // LA 2: after slab j's fragments are read, its slot takes slab j + 2 — of this tile, or slab 0 / 1 of the
+    // next tile (found at slab NS - 2; wave 0 issues that tile's factors before its slab 0)
+    auto issue_ahead = [&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      int n_is = 0;
+      if constexpr (j + 2 < NS) {
+        issue(base, j + 2, slot);
+        n_is = 4;
+      } else if constexpr (j + 2 == NS) {
+        if (!last_in_chunk) {
+          next_base = base + 32;
+        } else {   // (SCHED: nxt[] was published before this chunk's first tile barrier; a chunk with a
+                   // successor has >= 2 tiles, so that barrier is behind us)
+          next_chunk = !SCHED ? chunk + G : chunk == C - 1 ? C : (int64_t)nxt[cpar];
+          next_base = next_chunk < C ? next_chunk * CT * 32 : -1;
+        }
+        if (next_base >= 0) {
+          if (FX && w == 0) {
+            issue_factors(next_base, ts == 2 ? 0 : ts + 1);
+            n_is += 1;
+          }
+          issue(next_base, 0, slot);
+          n_is += 4;
+        }
+      } else {
+        if (next_base >= 0) {
+          issue(next_base, 1, slot);
+          n_is = 4;
+        }
+      }
+      pend = n_is;
+    };
     static_for<0, NS>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      if constexpr (MODE == 0) {
+      if constexpr (MODE == 0 && LA == 2) {
+        wait_vm_n(pend);   // slab j landed (loads complete in order; the pend ops issued after it may not have)
+      } else if constexpr (MODE == 0) {
         // keep one slab in flight: issue the next slab (of this tile, or slab 0 of the next tile with wave 0
         // issuing that tile's factors first) into the slot consumed last, then wait for this one. Wave 0's
         // counted wait includes its single-instruction extras issued after this slab (factors, counter).
@@ -608,6 +711,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         f32x4 av[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) av[i] = *(const f32x4*)(sl + slab_off(r, 4 * h + i));
+        if constexpr (MODE == 0 && LA == 2) issue_ahead(jc);
 #pragma unroll
         for (int m = 0; m < 16; ++m)
           for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m >> 2][m & 3], qfs[qh].v[j][m], accs[qh], 0, 0, 0);
@@ -615,6 +719,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         bf16x8 av[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) av[t] = *(const bf16x8*)(sl + slab_off(r, 2 * t + h));
+        if constexpr (MODE == 0 && LA == 2) issue_ahead(jc);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[t], qfs[qh].hi[j][t], accs[qh], 0, 0, 0);
@@ -627,6 +732,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           ah[t] = *(const f16x8*)(sl + slab_off(r, 4 * t + 2 * h));
           al[t] = *(const f16x8*)(sl + slab_off(r, 4 * t + 2 * h + 1));
         }
+        if constexpr (MODE == 0 && LA == 2) issue_ahead(jc);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t], qfs[qh].hi[j][t], accs[qh], 0, 0, 0);
@@ -638,6 +744,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           av[i] = MODE == 1 ? vrow[MODE == 1 ? j : 0][i] : *(const f32x4*)(sl + slab_off(r, 4 * (i >> 1) + 2 * h + (i & 1)));
+        if constexpr (MODE == 0 && LA == 2) issue_ahead(jc);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           const float x[8] = {av[2 * t].x, av[2 * t].y, av[2 * t].z, av[2 * t].w,
@@ -698,9 +805,15 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     // taken here is conservative).
     // full-key output (a.all_keys; the 32-wide instantiation, for the full-sort path): every key goes to HBM
     constexpr bool DUMP = MODE == 0 && KT == 32 && QH == 1 && SCHED == 0 && DT != 6;
+    // The bar a key must clear: the largest last entry of the query's LPQ lane lists (once full). A key at or
+    // below it cannot be in this workgroup's top-KT for the query (that lane alone holds KT keys above it), so
+    // no lane keeps it — the merged lists are the same as without the bar, but lanes insert ~LPQ x less often
+    // (the branch-free insert is the epilogue's largest VALU cost, and it runs for the whole wave whenever
+    // any of its lanes inserts). For the large-k floors: a key dropped here is below a full lane's last entry.
+    const uint64_t bar = group_max_u64<LPQ>(tk.last());
     float thr = -INFINITY;
     if constexpr (COS && DT != 6) {
-      const uint64_t last = tk.last();
+      const uint64_t last = bar;
       if (last != 0) {
         const float t = float_of_ord((uint32_t)(last >> 32));
         thr = t - fabsf(t) * 0x1p-20f - 0x1p-100f;
@@ -738,7 +851,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           u = v;
         }
         const uint64_t key = make_key(u, idx_base + (uint32_t)row);
-        if (valid && key > tk.last()) tk.insert(key);
+        if (valid && key > bar) tk.insert(key);
       } else if constexpr (COS) {
         // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
         const float den = cos_den(qn, nd);
@@ -748,13 +861,13 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           float c = s / den;   // IEEE division, as the reference's elementwise kernel
           c = fminf(fmaxf(c, -1.0f), 1.0f);
           const uint64_t key = make_key(c, idx_base + (uint32_t)row);
-          if (key > tk.last()) tk.insert(key);
+          if (key > bar) tk.insert(key);
         }
       } else {
         const uint64_t key = make_key(s, idx_base + (uint32_t)row);
         if (DUMP && a.all_keys) {
           if (valid) a.all_keys[(size_t)qe * n + row] = key;
-        } else if (valid && key > tk.last()) {
+        } else if (valid && key > bar) {
           tk.insert(key);
         }
       }

@@ -16,7 +16,8 @@ import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # rag-serving-system_amd/
 REPO_ROOT = os.path.dirname(PKG_ROOT)
-LIB_PATH = os.path.join(PKG_ROOT, "librag_retrieval.so")
+# RR_LIBRARY: another build of the same library (A/B measurements of kernel variants in one box call)
+LIB_PATH = os.environ.get("RR_LIBRARY") or os.path.join(PKG_ROOT, "librag_retrieval.so")
 HEADER_PATH = os.path.join(REPO_ROOT, "include", "rag_retrieval.h")
 
 # mirrors include/rag_retrieval.h
