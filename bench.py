@@ -34,8 +34,9 @@ sys.path.insert(0, os.path.join(REPO, "rag-serving-system_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 SCORE_KERNEL_DOC = ("the corpus-streaming kernel: sk_score_kernel MODE 0 (split-K, LDS-DMA; for fp32 storage the "
-                    "screened search's f16 screen, DT 6, whose exact verify of the candidates runs overlapped on "
-                    "the exchange stream), else fused_score_kernel")
+                    "screened search's screen — DT 7 over the f16 screening copy of the rows when the handle keeps "
+                    "one, else DT 6 over the fp32 rows — whose exact fp32 verify of the candidates runs overlapped "
+                    "on the exchange stream), else fused_score_kernel")
 
 
 def is_score_kernel(name: str) -> bool:
@@ -104,10 +105,11 @@ def cpu_baseline(n_docs: int, d: int, batch: int, k: int, budget_s: float) -> di
                                       "argpartition/argsort (a stronger CPU point)"}}
 
 
-def algorithmic_bytes(rows: int, d: int, batch: int, dtype: str, metric: str) -> int:
-    """HBM bytes one fused launch must move: the corpus rows once (4 B/element fp32 and fp32-split, 2 B bf16),
-    the per-row factors it reads (norm for cosine, row scale for fp32-split), the fp32 queries once."""
-    elem = 2 if dtype == "bf16" else 4
+def algorithmic_bytes(rows: int, d: int, batch: int, dtype: str, metric: str, screen16: bool = False) -> int:
+    """HBM bytes one corpus-streaming launch must move: the rows once (4 B/element fp32 and fp32-split, 2 B bf16,
+    2 B when the fp32 screen streams the f16 screening copy), the per-row factors it reads (norm for cosine,
+    row scale for fp32-split), the fp32 queries once."""
+    elem = 2 if dtype == "bf16" or screen16 else 4
     # per-row factors: the norm (cosine; and the fp32 screen's error bound for either metric), the split scale
     per_row = (4 if metric == "cosine" or dtype == "fp32" else 0) + (4 if dtype == "fp32-split" else 0)
     return rows * (d * elem + per_row) + batch * d * 4
@@ -265,10 +267,13 @@ def main() -> None:
     # ---- steady state: the same staged loop again, long after the GPU left idle ---------------------
     st_el, st_ms, st_n = timed_steps(ix, args.k, args.steady_steps, 0, dist, cuda_sync, 10)
     st_el = max_over_ranks(dist, st_el)
+    scr_blocks, scr_fallbacks = ix.screen_stats()
 
     # ---- roofline of the fused kernel (rank 0's shard) ---------------------------------------------
     n_local = se - sb
-    alg_bytes = algorithmic_bytes(n_local, args.dim, args.batch, args.dtype, args.metric)
+    # the fp32 screened search (k <= 29) streams the f16 screening copy when the handle keeps one
+    screen16 = args.dtype == "fp32" and args.k <= 29 and ix.screen_copy()
+    alg_bytes = algorithmic_bytes(n_local, args.dim, args.batch, args.dtype, args.metric, screen16)
     avg_kernel_s = (kern_ms / max(launches, 1)) / 1e3
     achieved = alg_bytes / avg_kernel_s / 1e9 if launches else None
     step_s = elapsed / args.steps
@@ -366,7 +371,9 @@ def main() -> None:
                          "kernel_timing": f"HIP events on the kernel's stream around every {every}-th "
                                           f"similarity-kernel launch of the timed region ({launches} launches)",
                          "kernel_le_step": consistent,
-                         "alg_bytes_per_launch": alg_bytes},
+                         "alg_bytes_per_launch": alg_bytes,
+                         "screen_copy": bool(screen16),
+                         "screened_blocks": scr_blocks, "screen_fallbacks": scr_fallbacks},
             "cpu_baseline": cpu,
             "other_dtypes": variants or None,
             "ingest": ingest,

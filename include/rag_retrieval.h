@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 2
+#define RR_ABI_VERSION 3
 
 /* error codes */
 #define RR_OK             0
@@ -194,6 +194,14 @@ int rr_set_kernel(rr_handle* h, int kernel);
  * tiles, then the next free one from a device counter, so workgroups on faster CUs take more; 0 = static
  * (chunks dealt round-robin). Results are identical; for A/B measurements. */
 int rr_set_schedule(rr_handle* h, int dynamic);
+
+/* The screened search's f16 copy (fp32 storage): the screen pass reads an f16 copy of the rows — exactly the
+ * values it would round the fp32 rows to in registers — so it streams half the bytes; the verify and every
+ * result still come from the fp32 rows (bit-identical results either way). The copy costs 2 bytes per element
+ * of HBM and is made at load time when it fits (default). use = 1: keep one (from the next load), 0: free it
+ * and screen from the fp32 rows, -1: leave as is. *present (may be null): the copy is in use on every local
+ * shard. */
+int rr_screen_copy(rr_handle* h, int32_t use, int32_t* present);
 
 /* Screened-search counters since the corpus was (re)loaded: search blocks screened (summed over local
  * shards) and how many of them needed the exact fallback pass. Synchronises the handle's streams. */

@@ -56,6 +56,7 @@ struct Shard {
   hipStream_t stream = nullptr;
   int64_t row_begin = 0, row_end = 0;   // global rows held
   void* corpus = nullptr;                // [rows][d] fp32 or bf16
+  uint16_t* scr16 = nullptr;             // fp32 storage: f16 copy of the rows for the screened search (or null)
   float* norms = nullptr;                // [round_up(rows, 32) + 32] |row| (pad = 1)
   float* rscale = nullptr;               // [same] split-f16 row scale 2^-e (pad = 1)
   float* qbuf[2] = {nullptr, nullptr};   // staged queries, double-buffered ([q_cap][d] fp32 each): a new
@@ -114,6 +115,7 @@ struct AsyncSlot {
   int32_t b = 0, k = 0, ticket = -1;
   bool pending = false;
   bool screened = false;   // the search ran screened blocks, the first with sequence number seq0
+  bool narrow = false;     // ... with 16-entry lists where 2k + 2 wanted 32
   int seq0 = 0;
 };
 constexpr int kAsyncSlots = 4;
@@ -155,6 +157,11 @@ struct rr_handle {
   int last_qpar = 0;            // ... and the query buffer it read
   int qpar = 0;                 // the staged queries live in every shard's qbuf[qpar]
   int dyn_sched = 1;            // split-K kernels: dynamic chunk schedule (rr_set_schedule)
+  int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy)
+  int64_t narrow_blocks = 0;    // screened blocks run with 16-entry lists where 2k + 2 wanted 32 (screen_kt)
+  int64_t narrow_reruns = 0;    // ... and re-runs of such searches
+  bool screen_wide = false;     // narrow lists re-ran too often on this corpus: use the wide ones
+  bool last_narrow = false;     // the last search ran narrow lists
 };
 
 namespace {
@@ -204,7 +211,7 @@ int dmalloc(T** p, size_t bytes) {
 
 int free_shard(Shard& s) {
   hipSetDevice(s.dev);
-  void* ptrs[] = {s.corpus, s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.ctr, s.shard_keys, s.gathered, s.out_base,
+  void* ptrs[] = {s.corpus, s.scr16, s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.ctr, s.shard_keys, s.gathered, s.out_base,
                   s.full_keys, s.sorted, s.sort_temp, s.wcand, s.wfloor, s.wsel, s.px_keys[0], s.px_keys[1], s.px_gathered[0], s.px_gathered[1]};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -228,6 +235,19 @@ int alloc_corpus(rr_handle* h, Shard& s) {
   HIP_TRY(hipSetDevice(s.dev));
   const int64_t rows = s.rows();
   if (int rc = dmalloc(&s.corpus, (size_t)std::max<int64_t>(rows, 1) * h->d * elem_bytes(h->dtype))) return rc;
+  // the screened search's f16 copy (half the fp32 bytes): only when HBM has room for it — without it the screen
+  // reads the fp32 rows and rounds them to f16 in registers (the same values)
+  if (s.scr16) HIP_TRY(hipFree(s.scr16));
+  s.scr16 = nullptr;
+  size_t free_b = 0, total_b = 0;
+  const size_t need16 = (size_t)rows * h->d * 2;
+  if (h->dtype == RR_DTYPE_F32 && h->screen_copy && rows > 0 && hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+      free_b > need16 + (4ull << 30)) {   // leave room for the norms and the search buffers
+    if (hipMalloc((void**)&s.scr16, need16) != hipSuccess) {
+      s.scr16 = nullptr;
+      (void)hipGetLastError();
+    }
+  }
   const int64_t npad = (rows + rr::kTileDocs - 1) / rr::kTileDocs * rr::kTileDocs + rr::kTileDocs;
   if (int rc = dmalloc(&s.norms, (size_t)npad * sizeof(float))) return rc;
   if (int rc = dmalloc(&s.rscale, (size_t)npad * sizeof(float))) return rc;
@@ -285,6 +305,8 @@ hipError_t store_rows(rr_handle* h, Shard& s, const float* tmp, int64_t dst_row,
       return rr::launch_split_f32(tmp, nr, d, (float*)s.corpus + dst_row * d, s.norms + dst_row,
                                   s.rscale + dst_row, s.stream);
     default:
+      if (s.scr16)
+        if (hipError_t e = rr::launch_f32_to_f16(tmp, s.scr16 + dst_row * d, nr, d, s.stream)) return e;
       return rr::launch_permute_f32(tmp, (float*)s.corpus + dst_row * d, nr, d, 0, s.stream);
   }
 }
@@ -387,6 +409,8 @@ int drop_work_buffers(rr_handle* h) {
   h->parity = 0;
   h->screen_blocks = 0;   // the flagged-block counters (scount) were freed above
   h->screen_reruns = 0;
+  h->narrow_blocks = h->narrow_reruns = 0;
+  h->screen_wide = false;
   h->last_screened = false;
   h->last_settled = true;
   h->qpar = 0;
@@ -499,14 +523,25 @@ bool use_sk(const rr_handle* h) {
 }
 
 // Screened search (rr_sk.hip "Screened search"): list width for k (>= k + 3 spare, 2k + 2 when it fits),
-// 0 when k is too large for it.
-int screen_kt(int k) {
-  const int want = std::max(2 * k + 2, k + 3);
+// 0 when k is too large for it. Where 2k + 2 would need 32-entry lists but k + 3 fits 16 (k = 8..13: BASELINE
+// config 3's k = 10), 16-entry lists are used — the screen's cheaper form (smaller inserts, the dynamic schedule)
+// — until they prove too narrow for the data: more than 1 in 32 narrow blocks re-run exactly (over at least 64)
+// switches the handle to the wide lists (re-armed at the next load).
+int screen_kt(const rr_handle* h, int k) {
+  int want = std::max(2 * k + 2, k + 3);
+  if (want > 16 && k + 3 <= 16 && !h->screen_wide) want = 16;
   if (want <= RR_FUSED_KMAX) return rr::fused_kt(want);
   return k + 3 <= RR_FUSED_KMAX ? RR_FUSED_KMAX : 0;
 }
+bool narrow_lists(const rr_handle* h, int k) { return std::max(2 * k + 2, k + 3) > 16 && screen_kt(h, k) == 16; }
+void note_rerun(rr_handle* h, bool narrow) {
+  if (!narrow) return;
+  ++h->narrow_reruns;
+  if (h->narrow_blocks >= 64 && h->narrow_reruns * 32 > h->narrow_blocks) h->screen_wide = true;
+}
 
-// Error bound of the screen (rr_sk.hip): eps = kScreenEpsA |x||q| + kScreenEpsB (sqrt(d) |x| + sum|q|).
+// Error bound of the screen (rr_sk.hip, DT 6 and DT 7 alike: the same f16 values of x, <= 16 MFMAs per wave partial):
+// eps = kScreenEpsA |x||q| + kScreenEpsB (sqrt(d) |x| + sum|q|).
 //   f16(x): <= 2^-11 |x| + 2^-25 per element; q - c0 - c1: <= 2^-22 |q| + 2^-24.99;
 //   fp32 accumulation, any order, of the screen (<= 16 MFMAs x 17 roundings + 8 per score) and of the exact
 //   DT 3 score (48 x 17 + 8, plus its dropped split terms <= 4 x 2^-24 |xq|): <= 1.7e-5 and 4.9e-5 of
@@ -517,7 +552,7 @@ constexpr float kScreenEpsB = 4.0e-8f;
 
 bool screened(const rr_handle* h, int k, int slots) {
   return (h->kernel == RR_KERNEL_AUTO || h->kernel == RR_KERNEL_SCREEN_FALLBACK) && h->dtype == RR_DTYPE_F32 &&
-         h->screen_ok && slots == rr::kQSlots && screen_kt(k) != 0 && use_sk(h);
+         h->screen_ok && slots == rr::kQSlots && screen_kt(h, k) != 0 && use_sk(h);
 }
 
 // Large k (32 < k <= kWideMax): split-K kernel with wide per-workgroup lists, radix select, completeness check
@@ -642,13 +677,14 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
   const int d = h->d;
   const bool scr = screened(h, k, slots);
   const bool wk = !scr && wide(h, k);
-  const int kt = scr ? screen_kt(k) : rr::fused_kt(k);
+  const int kt = scr ? screen_kt(h, k) : rr::fused_kt(k);
   const bool multi = h->world > 1 || h->dist;   // an exchange step (RCCL with any world, peer copies)
   const bool local_multi = multi && !h->dist;
   const int p = h->parity;
   if (scr || wk) {
     ++h->screen_seq;
     ++h->screen_blocks;
+    if (scr && narrow_lists(h, k)) ++h->narrow_blocks;
   }
   const int seq = h->screen_seq;
   for (size_t si = 0; si < h->shards.size(); ++si) {
@@ -693,7 +729,11 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
         a.eps_a = kScreenEpsA;
         a.eps_b = kScreenEpsB;
         a.sqrt_d = sqrtf((float)d) * (1.0f + 0x1p-20f);
-        HIP_TRY(rr::launch_sk_args(rr::KDT_SCREEN, h->metric, kt, 0, sgrid, rr::kQSlots, a, s.stream));
+        // the f16 copy holds exactly the values the fp32-reading screen rounds to: half the bytes
+        const bool s16 = s.scr16 && h->screen_copy && rr::sk_slabs(rr::KDT_SCREEN16, d);
+        if (s16) a.corpus = (const char*)s.scr16;
+        HIP_TRY(rr::launch_sk_args(s16 ? rr::KDT_SCREEN16 : rr::KDT_SCREEN, h->metric, kt, 0, sgrid, rr::kQSlots, a,
+                                   s.stream));
       }
       if (timed) HIP_TRY(hipEventRecord(e1, s.stream));
       HIP_TRY(hipEventRecord(s.ev_scr[p], s.stream));
@@ -1197,6 +1237,7 @@ int rr_search_staged(rr_handle* h, int32_t k) {
   if (int rc = ensure_buffers(h, b, k)) return rc;
   const int slots = block_slots(h, b, k);
   h->last_screened = checked(h, k, slots);
+  h->last_narrow = screened(h, k, slots) && narrow_lists(h, k);
   h->last_seq0 = h->screen_seq + 1;
   h->last_settled = !h->last_screened;
   h->last_qpar = h->qpar;
@@ -1237,6 +1278,7 @@ int settle_screen(rr_handle* h, uint64_t flag, bool* rerun) {
   if (flag < (uint64_t)h->last_seq0) return RR_OK;
   // the search's own queries (begin_stage keeps its buffer intact until it is settled); a batch staged
   // since stays staged
+  const bool was_narrow = h->last_narrow;
   const int saved_kernel = h->kernel, saved_qpar = h->qpar, saved_b = h->cur_b;
   h->kernel = RR_KERNEL_EXACT;
   h->qpar = h->last_qpar;
@@ -1247,6 +1289,7 @@ int settle_screen(rr_handle* h, uint64_t flag, bool* rerun) {
   h->cur_b = saved_b;
   if (rc) return rc;
   ++h->screen_reruns;
+  note_rerun(h, was_narrow);
   *rerun = true;
   return sync_streams(h);
 }
@@ -1359,6 +1402,7 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
   a.k = k;
   a.ticket = t;
   a.screened = h->last_screened;
+  a.narrow = h->last_narrow;
   a.seq0 = h->last_seq0;
   a.pending = true;
   h->next_ticket = t + 1 < 0x40000000 ? t + 1 : 0;
@@ -1396,6 +1440,7 @@ int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx) {
     h->kernel = saved;
     if (rc) return rc;
     ++h->screen_reruns;
+    note_rerun(h, a.narrow);
     return rr_fetch_results(h, out_scores, out_idx);
   }
   memcpy(out_scores, a.pin + res_off + kOutHead, cnt * 4);
@@ -1430,6 +1475,27 @@ int rr_set_schedule(rr_handle* h, int dynamic) {
   if (!h) return fail(RR_E_INVALID, "null handle");
   if (int rc = sync_streams(h)) return rc;   // no launch in flight uses the counter
   h->dyn_sched = dynamic ? 1 : 0;
+  return RR_OK;
+}
+
+int rr_screen_copy(rr_handle* h, int32_t use, int32_t* present) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  if (use >= 0) {
+    h->screen_copy = use ? 1 : 0;
+    if (!use)
+      for (Shard& s : h->shards)
+        if (s.scr16) {
+          HIP_TRY(hipSetDevice(s.dev));
+          HIP_TRY(hipStreamSynchronize(s.stream));
+          HIP_TRY(hipFree(s.scr16));
+          s.scr16 = nullptr;
+        }
+  }
+  if (present) {
+    bool all = !h->shards.empty();
+    for (const Shard& s : h->shards) all = all && (s.scr16 != nullptr || s.rows() == 0);
+    *present = all && h->screen_copy && h->loaded ? 1 : 0;
+  }
   return RR_OK;
 }
 

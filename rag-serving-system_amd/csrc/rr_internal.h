@@ -28,6 +28,9 @@ constexpr int KDT_F32_X3 = 3;
 //   KDT_SCREEN   : fp32 rows read as f16 against the query's f16 hi + lo: an upper bound of the KDT_F32_X3
 //                  score for the screened search (split-K kernel only; rr_sk.hip "Screened search")
 constexpr int KDT_SCREEN = 6;
+//   KDT_SCREEN16 : the same screen over an f16 copy of the fp32 rows (the values KDT_SCREEN rounds to in
+//                  registers, stored: half the bytes per screened search; rr_sk.hip DT 7)
+constexpr int KDT_SCREEN16 = 7;
 
 // Smallest fused-kernel list width KT >= k (4, 8, 16, 32); 0 if k > RR_FUSED_KMAX.
 int fused_kt(int k);
@@ -147,6 +150,8 @@ hipError_t launch_decode(const uint64_t* keys, int b, int k, float* scores, int6
 // fp32 (MFMA) and bf16 rows use the pair_unit layout (rr_kernels.hip); conversions take whole rows.
 hipError_t launch_permute_f32(const float* in, float* out, int64_t nrows, int d, int inverse, hipStream_t s);
 hipError_t launch_f32_to_bf16(const float* in, uint16_t* out, int64_t nrows, int d, hipStream_t s);
+// fp32 rows -> f16 (round to nearest even) in the same 8-element pair_unit layout as bf16 storage (the screen copy)
+hipError_t launch_f32_to_f16(const float* in, uint16_t* out, int64_t nrows, int d, hipStream_t s);
 hipError_t launch_row_norms(int dtype, const void* corpus, int64_t n, int d, float* norms, hipStream_t s);
 hipError_t launch_synth(int kind, uint64_t seed, int64_t row_begin, int64_t n_rows, int d, float* out,
                         hipStream_t s);

@@ -727,7 +727,8 @@ __global__ void permute_f32_kernel(const u32x4* __restrict__ in, u32x4* __restri
   else out[row * upr + pair_unit(g)] = in[i];
 }
 
-__global__ void f32_to_bf16_kernel(const float* __restrict__ in, u32x4* __restrict__ out, int64_t nrows, int d) {
+template <bool F16>
+__global__ void f32_to_16_kernel(const float* __restrict__ in, u32x4* __restrict__ out, int64_t nrows, int d) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // one 8-element group
   const int gpr = d >> 3;
   if (i >= nrows * gpr) return;
@@ -735,10 +736,17 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ in, u32x4* __restri
   const int g = (int)(i - row * gpr);
   const f32x4 x0 = ((const f32x4*)in)[2 * i], x1 = ((const f32x4*)in)[2 * i + 1];
   const float xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-  bf16x8 v;
+  if constexpr (F16) {
+    f16x8 v;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = (__bf16)xs[j];
-  out[row * gpr + pair_unit(g)] = __builtin_bit_cast(u32x4, v);
+    for (int j = 0; j < 8; ++j) v[j] = (_Float16)xs[j];
+    out[row * gpr + pair_unit(g)] = __builtin_bit_cast(u32x4, v);
+  } else {
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (__bf16)xs[j];
+    out[row * gpr + pair_unit(g)] = __builtin_bit_cast(u32x4, v);
+  }
 }
 
 __global__ void bf16_to_f32_kernel(const u32x4* __restrict__ in, float* __restrict__ out, int64_t nrows, int d) {
@@ -1039,8 +1047,15 @@ hipError_t launch_permute_f32(const float* in, float* out, int64_t nrows, int d,
 
 hipError_t launch_f32_to_bf16(const float* in, uint16_t* out, int64_t nrows, int d, hipStream_t s) {
   const int64_t groups = nrows * (d >> 3);
-  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, in, (u32x4*)out,
-                     nrows, d);
+  hipLaunchKernelGGL(f32_to_16_kernel<false>, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, in,
+                     (u32x4*)out, nrows, d);
+  return hipGetLastError();
+}
+
+hipError_t launch_f32_to_f16(const float* in, uint16_t* out, int64_t nrows, int d, hipStream_t s) {
+  const int64_t groups = nrows * (d >> 3);
+  hipLaunchKernelGGL(f32_to_16_kernel<true>, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, in,
+                     (u32x4*)out, nrows, d);
   return hipGetLastError();
 }
 

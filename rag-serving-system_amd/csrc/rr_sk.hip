@@ -200,6 +200,8 @@ template <int NS>
 struct QFrag<3, NS> { bf16x8 c0[NS][2], c1[NS][2], c2[NS][2]; };
 template <int NS>
 struct QFrag<6, NS> { f16x8 c0[NS][2], c1[NS][2]; };          // screen: q = c0 + c1 (+ <= 2^-22 |q|)
+template <int NS>
+struct QFrag<7, NS> { f16x8 c0[NS][4], c1[NS][4]; };          // screen over the f16 copy: 4 K-steps per slab
 
 
 // LDS byte offset (within a slot) of 16-byte column position cp of tile row r (swizzled image)
@@ -274,13 +276,14 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
-  constexpr int EB = DT == 1 ? 2 : 4;                           // storage bytes per element
+  constexpr bool SCR = DT == 6 || DT == 7;                      // the screen (upper bounds, "Screened search")
+  constexpr int EB = DT == 1 || DT == 7 ? 2 : 4;                // storage bytes per element
   const int row_bytes = d * EB;
   constexpr int KS = NS * kSlabRowBytes;                        // bytes of a row per wave
   const int p0 = w * (KS / 16);                                 // first 16-byte storage unit of the slice
 
   float* red = (float*)(smem + ring_bytes(RS));
-  constexpr int SW = (COS || DT == 6 ? 1 : 0) + (DT == 2 ? 1 : 0);   // per-row factors (norm, split scale)
+  constexpr int SW = (COS || SCR ? 1 : 0) + (DT == 2 ? 1 : 0);   // per-row factors (norm, split scale)
   constexpr int FX = SW > 0 ? 1 : 0;                            // LDS-DMA instructions per tile for them
   float* trow = (float*)(smem + ring_bytes(RS) + red_bytes(RS, QH));   // [3 tiles][2 factors][32 rows]
   int* nxt = (int*)(trow + 3 * 64);                             // [2] next chunk (dynamic schedule), + pad
@@ -437,6 +440,19 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
               qf.lo[j][t][e] = (__bf16)(x - (float)bh);
             }
           }
+        } else if constexpr (DT == 7) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {   // the bf16 layout (position 2t + h, 8 elements), f16 pieces c0 + c1
+            const int L = inv_pair(p0 + 8 * j + 2 * t + h);
+            const f32x4 va = qvec(8 * L), vb = qvec(8 * L + 4);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float x = e < 4 ? va[e] : vb[e - 4];
+              const _Float16 c0 = (_Float16)x;
+              qf.c0[j][t][e] = c0;
+              qf.c1[j][t][e] = (_Float16)(x - (float)c0);
+            }
+          }
         } else if constexpr (DT == 2) {
           const int ex = qv ? qexp[rq] : 0;
 #pragma unroll
@@ -497,6 +513,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #pragma unroll
           for (int t = 0; t < 2; ++t)
             asm volatile("" : "+v"(qfs[qh].c0[j][t]), "+v"(qfs[qh].c1[j][t]), "+v"(qfs[qh].c2[j][t]));
+        } else if constexpr (DT == 7) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) asm volatile("" : "+v"(qfs[qh].c0[j][t]), "+v"(qfs[qh].c1[j][t]));
         } else {
 #pragma unroll
           for (int t = 0; t < 2; ++t) asm volatile("" : "+v"(qfs[qh].c0[j][t]), "+v"(qfs[qh].c1[j][t]));
@@ -540,7 +559,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       }
     }
     __syncthreads();
-  } else if (COS || DT == 2 || DT == 6) {
+  } else if (COS || DT == 2 || SCR) {
     const int nc = d >> 2;                      // float4 per row (d <= 1024 on this kernel: <= 4 per lane)
 #pragma unroll
     for (int g4 = 0; g4 < QH; ++g4) {
@@ -565,21 +584,21 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
             const f32x4 x = v[qi][c];
             ss = fmaf(x.x, x.x, ss); ss = fmaf(x.y, x.y, ss); ss = fmaf(x.z, x.z, ss); ss = fmaf(x.w, x.w, ss);
             m = fmaxf(m, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
-            if constexpr (DT == 6) sa += (fabsf(x.x) + fabsf(x.y)) + (fabsf(x.z) + fabsf(x.w));
+            if constexpr (SCR) sa += (fabsf(x.x) + fabsf(x.y)) + (fabsf(x.z) + fabsf(x.w));
           }
         }
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
           ss += __shfl_xor(ss, off, 64);
           m = fmaxf(m, __shfl_xor(m, off, 64));
-          if constexpr (DT == 6) sa += __shfl_xor(sa, off, 64);
+          if constexpr (SCR) sa += __shfl_xor(sa, off, 64);
         }
         int E = 0;
         if (m > 0.f) frexpf(m, &E);
         const int ex = m > 0.f ? 15 - E : 0;
         if (lane == 0) {
           qinfo[q] = sqrtf(ss);
-          qinfo[QS + q] = DT == 2 ? ldexpf(1.0f, -ex) : DT == 6 ? sa * (1.0f + 0x1p-20f) : m;
+          qinfo[QS + q] = DT == 2 ? ldexpf(1.0f, -ex) : SCR ? sa * (1.0f + 0x1p-20f) : m;
           qexp[q] = ex;
         }
       }
@@ -623,9 +642,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   constexpr int LPQ = 16 / QH, DPL = 2 * QH;
   const int qe = 4 * QH * w + lane / LPQ, er = DPL * (lane % LPQ);
   const bool qev = MODE == 1 ? qe == vq : qe < b;
-  const float qn = COS || DT == 6 ? qinfo[qe] : 0.f;
+  const float qn = COS || SCR ? qinfo[qe] : 0.f;
   const float qs = DT == 2 ? qinfo[QS + qe] : 1.f;
-  const float qsa = DT == 6 ? qinfo[QS + qe] : 0.f;
+  const float qsa = SCR ? qinfo[QS + qe] : 0.f;
 
   TopK<KT> tk;
   tk.init();
@@ -725,6 +744,16 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[t], qfs[qh].hi[j][t], accs[qh], 0, 0, 0);
           for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[t], qfs[qh].lo[j][t], accs[qh], 0, 0, 0);
         }
+      } else if constexpr (DT == 7) {   // screen over the f16 copy: x exactly as DT 6 rounds it, half the bytes
+        f16x8 av[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) av[t] = *(const f16x8*)(sl + slab_off(r, 2 * t + h));
+        if constexpr (MODE == 0 && LA == 2) issue_ahead(jc);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[t], qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
+          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[t], qfs[qh].c1[j][t], accs[qh], 0, 0, 0);
+        }
       } else if constexpr (DT == 2) {
         f16x8 ah[2], al[2];
 #pragma unroll
@@ -804,7 +833,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     // few that pass pay the exact IEEE division (the list only grows inside the loop: the threshold
     // taken here is conservative).
     // full-key output (a.all_keys; the 32-wide instantiation, for the full-sort path): every key goes to HBM
-    constexpr bool DUMP = MODE == 0 && KT == 32 && QH == 1 && SCHED == 0 && DT != 6;
+    constexpr bool DUMP = MODE == 0 && KT == 32 && QH == 1 && SCHED == 0 && !SCR;
     // The bar a key must clear: the largest last entry of the query's LPQ lane lists (once full). A key at or
     // below it cannot be in this workgroup's top-KT for the query (that lane alone holds KT keys above it), so
     // no lane keeps it — the merged lists are the same as without the bar, but lanes insert ~LPQ x less often
@@ -812,7 +841,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     // any of its lanes inserts). For the large-k floors: a key dropped here is below a full lane's last entry.
     const uint64_t bar = group_max_u64<LPQ>(tk.last());
     float thr = -INFINITY;
-    if constexpr (COS && DT != 6) {
+    if constexpr (COS && !SCR) {
       const uint64_t last = bar;
       if (last != 0) {
         const float t = float_of_ord((uint32_t)(last >> 32));
@@ -834,9 +863,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         valid = qev && row < n;
         const float* tf = trow + ts * 64 + er + e;   // factor 0 at tf[0], factor 1 at tf[32]
         if constexpr (DT == 2) s = s * (COS ? tf[32] : tf[0]) * qs;   // exact 2^e rescales
-        if constexpr (COS || DT == 6) nd = tf[0];
+        if constexpr (COS || SCR) nd = tf[0];
       }
-      if constexpr (DT == 6) {
+      if constexpr (SCR) {
         // upper bound of the exact (DT 3) score, see "Screened search"; the relative bumps cover the
         // roundings of the bound's own arithmetic and of the reciprocal (<= 1 ulp)
         const float eps = fmaf(a.eps_a * nd, qn, a.eps_b * fmaf(a.sqrt_d, nd, qsa));
@@ -994,9 +1023,9 @@ hipError_t launch_ns(int ns, int kt, int grid, const SkArgs& a, hipStream_t s) {
   switch (ns) {
     case 1: return launch_kt<DT, 1, COS, RS, QH, MODE, SCHED>(kt, grid, a, s);
     case 2: return launch_kt<DT, 2, COS, RS, QH, MODE, SCHED>(kt, grid, a, s);
-    case 3: if constexpr (DT != 1) return launch_kt<DT, 3, COS, RS, QH, MODE, SCHED>(kt, grid, a, s);
+    case 3: if constexpr (DT != 1 && DT != 7) return launch_kt<DT, 3, COS, RS, QH, MODE, SCHED>(kt, grid, a, s);
             else return hipErrorInvalidValue;
-    case 4: if constexpr (DT != 1) return launch_kt<DT, 4, COS, RS, QH, MODE, SCHED>(kt, grid, a, s);
+    case 4: if constexpr (DT != 1 && DT != 7) return launch_kt<DT, 4, COS, RS, QH, MODE, SCHED>(kt, grid, a, s);
             else return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
@@ -1021,11 +1050,11 @@ size_t sk_lds_bytes(int sdt, bool cos, int ring, int qslots) {
 
 bool sk_supports_64(int sdt) { return sdt == KDT_BF16 || sdt == KDT_F32_SPLIT; }
 int sk_slabs(int sdt, int d) {
-  const int eb = sdt == 1 ? 2 : 4;
+  const int eb = sdt == KDT_BF16 || sdt == KDT_SCREEN16 ? 2 : 4;
   const int ks = d * eb / kWaves;   // row bytes per wave
   if (d <= 0 || ks % sk::kSlabRowBytes != 0) return 0;
   const int ns = ks / sk::kSlabRowBytes;
-  return (ns >= 1 && ns <= (sdt == 1 ? 2 : 4)) ? ns : 0;
+  return (ns >= 1 && ns <= (eb == 2 ? 2 : 4)) ? ns : 0;
 }
 
 hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int qslots, const SkArgs& a,
@@ -1041,6 +1070,12 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
     if (qslots != 32 || ring != 2) return hipErrorInvalidValue;
     if (a.dyn && a.ctr && kt <= 16) return sk::launch_metric<6, 2, 1, 0, 1>(metric, ns, kt, grid, a, s);
     return sk::launch_metric<6, 2, 1>(metric, ns, kt, grid, a, s);
+  }
+  if (sdt == KDT_SCREEN16) {   // the screen over the f16 copy (a.corpus = that copy)
+    const int ns16 = sk_slabs(KDT_SCREEN16, a.d);
+    if (qslots != 32 || ring != 2 || !ns16) return hipErrorInvalidValue;
+    if (a.dyn && a.ctr && kt <= 16) return sk::launch_metric<7, 2, 1, 0, 1>(metric, ns16, kt, grid, a, s);
+    return sk::launch_metric<7, 2, 1>(metric, ns16, kt, grid, a, s);
   }
   if (qslots == 64) {   // one corpus pass for up to 64 queries: bf16 and fp32-split storage, ring 2
     if (ring != 2) return hipErrorInvalidValue;

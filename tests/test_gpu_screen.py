@@ -197,3 +197,32 @@ def test_dynamic_schedule_equals_static(Index, metric):
     ix.close()
     st.close()
     small.close()
+
+
+@pytest.mark.parametrize("metric", ["cosine", "dot"])
+def test_screen_copy_equals_fp32_screen_and_exact(Index, metric):
+    """The screen over the f16 copy (DT 7, half the bytes) and the screen over the fp32 rows (DT 6) both
+    end in the exact fp32 verify: results bit-identical to each other and to the one-pass exact kernel,
+    across reloads and with the copy freed."""
+    rng = np.random.default_rng(77)
+    corpus = rng.standard_normal((20011, 1024)).astype(np.float32) * rng.uniform(0.5, 2, (20011, 1)).astype(np.float32)
+    q = rng.standard_normal((45, 1024)).astype(np.float32)
+    ix = Index(dtype="fp32", metric=metric)
+    ix.load(corpus)
+    assert ix.screen_copy()                                   # made at load (default)
+    ex = Index(dtype="fp32", metric=metric)
+    ex.load(corpus)
+    ex.set_kernel("exact")
+    for k in (1, 5, 10, 29):
+        want = ex.search(q, k)
+        got16 = ix.search(q, k)
+        ix.screen_copy(False)
+        assert not ix.screen_copy()
+        got32 = ix.search(q, k)
+        for got in (got16, got32):
+            assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), k
+        ix.screen_copy(True)
+        ix.load(corpus)                                       # the copy comes back with the next load
+        assert ix.screen_copy()
+    ix.close()
+    ex.close()
