@@ -67,6 +67,7 @@ struct Shard {
   uint64_t* cand = nullptr;              // 2 x [grid][64][32] per-workgroup candidates (the screened search
   int cand_grid = 0;                     // alternates the halves by parity; the other paths use half 0)
   int* scount = nullptr;                 // screened search: blocks this shard flagged for the exact pass
+  int* pin_scount = nullptr;             // pinned host copy of scount, refreshed after each verify (no sync)
   uint32_t* ctr = nullptr;               // split-K chunk counter (dynamic schedule), 0 between launches
   uint64_t* shard_keys = nullptr;        // [32][k_cap] this shard's top-k (all-gather send buffer)
   uint64_t* gathered = nullptr;          // [world][32][k_cap] (all-gather receive buffer)
@@ -217,6 +218,7 @@ int free_shard(Shard& s) {
     if (p) hipFree(p);
   for (hipEvent_t e : s.ev) hipEventDestroy(e);
   s.ev.clear();
+  if (s.pin_scount) hipHostFree(s.pin_scount);
   if (s.keys_ready) hipEventDestroy(s.keys_ready);
   if (s.pin_q_free) hipEventDestroy(s.pin_q_free);
   if (s.copies_done) hipEventDestroy(s.copies_done);
@@ -463,6 +465,8 @@ int ensure_buffers(rr_handle* h, int b, int k) {
       if (int rc = dmalloc(&s.cand, 2 * cand_half(s) * 8)) return rc;
       if (int rc = dmalloc(&s.scount, sizeof(int))) return rc;
       HIP_TRY(hipMemset(s.scount, 0, sizeof(int)));
+      if (!s.pin_scount) HIP_TRY(hipHostMalloc((void**)&s.pin_scount, sizeof(int), hipHostMallocDefault));
+      *(volatile int*)s.pin_scount = 0;
       if (int rc = dmalloc(&s.ctr, sizeof(uint32_t))) return rc;
       HIP_TRY(hipMemset(s.ctr, 0, sizeof(uint32_t)));
     }
@@ -538,6 +542,17 @@ void note_rerun(rr_handle* h, bool narrow) {
   if (!narrow) return;
   ++h->narrow_reruns;
   if (h->narrow_blocks >= 64 && h->narrow_reruns * 32 > h->narrow_blocks) h->screen_wide = true;
+}
+// The same rule on the device's flagged-block counts (staged searches whose results nobody fetches are never
+// re-run, but flag just the same): blocks flagged since the load, as the pinned copies last showed them.
+// (One process per GPU: ranks must agree on the list width — it sizes the all-gather — so there only the re-run
+// rule applies: every rank sees the same exchanged flag and re-runs the same searches.)
+void check_narrow(rr_handle* h) {
+  if (h->screen_wide || h->narrow_blocks < 64 || h->dist) return;
+  int64_t flagged = 0;
+  for (const Shard& s : h->shards)
+    if (s.pin_scount) flagged += *(volatile const int*)s.pin_scount;
+  if (flagged * 32 > h->narrow_blocks) h->screen_wide = true;
 }
 
 // Error bound of the screen (rr_sk.hip, DT 6 and DT 7 alike: the same f16 values of x, <= 16 MFMAs per wave partial):
@@ -715,11 +730,14 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
     if (timed)
       if (int rc = next_event_pair(s, &e0, &e1)) return rc;
     if (scr) {
-      // screened search. Compute stream: the screen (upper bounds) into cand[p], once the verify of the block
-      // two back has read that half. Exchange stream: the verify (exact DT 3 scores of the KT candidates;
-      // results, or this shard's exact keys for the exchange; raises the block's flag word when the bound
-      // cannot prove completeness: settle_screen re-runs then), overlapping the next block's screen.
-      HIP_TRY(wait_px(p));
+      // screened search, on the compute stream: the screen (upper bounds) into cand[p], then the verify (exact
+      // DT 3 scores of the KT candidates; results, or this shard's exact keys for the exchange; raises the
+      // block's flag word when the bound cannot prove completeness: settle_screen re-runs then). The verify
+      // follows in-stream: a cross-stream hand-off costs ~20-25 us of dispatch latency on MI355X
+      // (profiles/r02/steps/), more than the ~17 us verify that running it on the exchange stream overlapped.
+      // With an exchange, px_keys[p] is rewritten only after its previous exchange (two blocks back) is done.
+      hipStream_t vs = s.stream;
+      if (multi) HIP_TRY(wait_px(p));
       uint64_t* candp = s.cand + (size_t)p * cand_half(s);
       const int sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(s.cand_grid, (s.rows() + 31) / 32));
       if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
@@ -736,8 +754,6 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
                                    s.stream));
       }
       if (timed) HIP_TRY(hipEventRecord(e1, s.stream));
-      HIP_TRY(hipEventRecord(s.ev_scr[p], s.stream));
-      HIP_TRY(hipStreamWaitEvent(s.xstream, s.ev_scr[p], 0));
       if (s.rows() > 0) {
         rr::SkArgs v = sk_base(h, s, qb, bb);
         v.vin = candp;
@@ -751,12 +767,17 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
         v.count = s.scount;
         v.seq = seq;
         v.force_incomplete = h->kernel == RR_KERNEL_SCREEN_FALLBACK;
-        HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 1, rr::kQSlots, rr::kQSlots, v, s.xstream));
+        HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 1, rr::kQSlots, rr::kQSlots, v, vs));
       } else {   // a shard without rows contributes empty lists
-        HIP_TRY(hipMemsetAsync(s.px_keys[p], 0, (size_t)slots * kt * 8, s.xstream));
+        HIP_TRY(hipMemsetAsync(s.px_keys[p], 0, (size_t)slots * kt * 8, vs));
       }
-      HIP_TRY(hipEventRecord(s.ev_qread[h->qpar], s.xstream));
-      if (!multi) HIP_TRY(hipEventRecord(s.ev_xdone[p], s.xstream));
+      HIP_TRY(hipEventRecord(s.ev_qread[h->qpar], vs));
+      // the flagged-block count reaches the host without a sync (read a block or two late by check_narrow), every
+      // 8th block, on the exchange stream so that the copy gates nothing on the compute stream
+      if (s.rows() > 0 && (h->screen_blocks & 7) == 0) {
+        HIP_TRY(hipStreamWaitEvent(s.xstream, s.ev_qread[h->qpar], 0));
+        HIP_TRY(hipMemcpyAsync(s.pin_scount, s.scount, sizeof(int), hipMemcpyDeviceToHost, s.xstream));
+      }
     } else if (kt) {
       int grid = fused_grid(s);
       HIP_TRY(wait_px(0));   // no screened verify still reads cand or writes the results
@@ -886,7 +907,7 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
     return RR_OK;
   }
   if (kt) {
-    if (int rc = enqueue_exchange_px(h, p, q0, bb, k, kt, slots, scr)) return rc;
+    if (int rc = enqueue_exchange_px(h, p, q0, bb, k, kt, slots, false)) return rc;
     h->parity ^= 1;
     return RR_OK;
   }
@@ -1236,6 +1257,7 @@ int rr_search_staged(rr_handle* h, int32_t k) {
   const int b = h->cur_b;
   if (int rc = ensure_buffers(h, b, k)) return rc;
   const int slots = block_slots(h, b, k);
+  check_narrow(h);
   h->last_screened = checked(h, k, slots);
   h->last_narrow = screened(h, k, slots) && narrow_lists(h, k);
   h->last_seq0 = h->screen_seq + 1;
@@ -1393,7 +1415,7 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
   // (the serial k > 32 exchange also orders it after itself), else the compute stream
   Shard& s0 = h->shards[0];
   HIP_TRY(hipSetDevice(s0.dev));
-  hipStream_t rs = (h->world > 1 || h->dist || h->last_screened) ? s0.xstream : s0.stream;
+  hipStream_t rs = (h->world > 1 || h->dist) ? s0.xstream : s0.stream;
   HIP_TRY(hipMemcpyAsync(a.pin + res_off, s0.out_base, kOutHead, hipMemcpyDeviceToHost, rs));
   HIP_TRY(hipMemcpyAsync(a.pin + res_off + kOutHead, s0.out_scores, cnt * 4, hipMemcpyDeviceToHost, rs));
   HIP_TRY(hipMemcpyAsync(a.pin + idx_off, s0.out_idx, cnt * 8, hipMemcpyDeviceToHost, rs));

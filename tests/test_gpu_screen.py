@@ -226,3 +226,30 @@ def test_screen_copy_equals_fp32_screen_and_exact(Index, metric):
         assert ix.screen_copy()
     ix.close()
     ex.close()
+
+
+def test_narrow_lists_switch_to_wide(Index):
+    """k = 10 screens with 16-entry lists (k + 3 spare). Twenty near-copies of each query make the 16th upper
+    bound exceed the exact 10th score: every block is re-run exactly — until, after 64 narrow blocks, the
+    handle switches to 32-entry lists, which prove these blocks complete. Results are exact throughout."""
+    rng = np.random.default_rng(5)
+    corpus = synth.unit_norm_gaussian(91, 65536, 1024)
+    q = synth.unit_norm_gaussian(92, 32, 1024)
+    for i in range(32):
+        near = q[i] + 1e-6 * rng.standard_normal((20, 1024)).astype(np.float32)
+        corpus[1000 + 40 * i:1020 + 40 * i] = near / np.linalg.norm(near, axis=1, keepdims=True)
+    ix = Index(dtype="fp32", metric="cosine")
+    ix.load(corpus)
+    ex = Index(dtype="fp32", metric="cosine")
+    ex.load(corpus)
+    ex.set_kernel("exact")
+    want = ex.search(q, 10)
+    for step in range(80):
+        got = ix.search(q, 10)
+        assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), step
+        if step == 69:
+            flagged70 = ix.screen_stats()[1]
+    blocks, flagged = ix.screen_stats()
+    assert blocks == 80 and 64 <= flagged <= 70 and flagged == flagged70     # none after the switch
+    ix.close()
+    ex.close()
