@@ -61,8 +61,7 @@ struct Shard {
   float* rscale = nullptr;               // [same] split-f16 row scale 2^-e (pad = 1)
   float* qbuf[2] = {nullptr, nullptr};   // staged queries, double-buffered ([q_cap][d] fp32 each): a new
                                          // batch is copied into one while verifies may still read the other
-  hipEvent_t ev_qread[2] = {nullptr, nullptr};   // xstream: the last verify reading qbuf[i] has finished
-  hipEvent_t ev_scr[2] = {nullptr, nullptr};     // compute stream: the screen of parity p has written cand[p]
+  hipEvent_t ev_scr[2] = {nullptr, nullptr};     // compute stream: a block's verify done ([0]: the flag-count copy)
   int q_cap = 0;
   uint64_t* cand = nullptr;              // 2 x [grid][64][32] per-workgroup candidates (the screened search
   int cand_grid = 0;                     // alternates the halves by parity; the other paths use half 0)
@@ -222,8 +221,8 @@ int free_shard(Shard& s) {
   if (s.keys_ready) hipEventDestroy(s.keys_ready);
   if (s.pin_q_free) hipEventDestroy(s.pin_q_free);
   if (s.copies_done) hipEventDestroy(s.copies_done);
-  for (hipEvent_t e : {s.ev_keys[0], s.ev_keys[1], s.ev_xdone[0], s.ev_xdone[1], s.ev_cdone, s.ev_qread[0],
-                       s.ev_qread[1], s.ev_scr[0], s.ev_scr[1]})
+  for (hipEvent_t e : {s.ev_keys[0], s.ev_keys[1], s.ev_xdone[0], s.ev_xdone[1], s.ev_cdone, s.ev_scr[0],
+                       s.ev_scr[1]})
     if (e) hipEventDestroy(e);
   if (s.xstream) hipStreamDestroy(s.xstream);
   if (s.comm) ncclCommDestroy(s.comm);
@@ -771,11 +770,12 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
       } else {   // a shard without rows contributes empty lists
         HIP_TRY(hipMemsetAsync(s.px_keys[p], 0, (size_t)slots * kt * 8, vs));
       }
-      HIP_TRY(hipEventRecord(s.ev_qread[h->qpar], vs));
       // the flagged-block count reaches the host without a sync (read a block or two late by check_narrow), every
-      // 8th block, on the exchange stream so that the copy gates nothing on the compute stream
+      // 8th block, on the exchange stream so that the copy gates nothing on the compute stream. (No event is
+      // recorded on the other blocks: each record between two kernels widened the dispatch gap.)
       if (s.rows() > 0 && (h->screen_blocks & 7) == 0) {
-        HIP_TRY(hipStreamWaitEvent(s.xstream, s.ev_qread[h->qpar], 0));
+        HIP_TRY(hipEventRecord(s.ev_scr[0], vs));
+        HIP_TRY(hipStreamWaitEvent(s.xstream, s.ev_scr[0], 0));
         HIP_TRY(hipMemcpyAsync(s.pin_scount, s.scount, sizeof(int), hipMemcpyDeviceToHost, s.xstream));
       }
     } else if (kt) {
@@ -957,17 +957,14 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
   return RR_OK;
 }
 
-// A new batch goes into the query buffer the last search did not read (that search's verifies may still be
-// running on the exchange streams). The last screened search can be re-run only while its buffer is intact,
-// so it is settled first when its buffer is the one about to be rewritten (two batches staged, no search).
+// A new batch goes into the query buffer the last search did not read: every reader of a query buffer runs on
+// the compute stream, where the new batch's copy is ordered after them. The last checked search can be re-run
+// only while its buffer is intact, so it is settled first when its buffer is the one about to be rewritten
+// (two batches staged, no search).
 int begin_stage(rr_handle* h, int* nq) {
   const int t = h->qpar ^ 1;
   if (h->last_screened && !h->last_settled && h->last_qpar == t)
     if (int rc = rr_synchronize(h)) return rc;
-  for (Shard& s : h->shards) {
-    HIP_TRY(hipSetDevice(s.dev));
-    HIP_TRY(hipStreamWaitEvent(s.stream, s.ev_qread[t], 0));
-  }
   *nq = t;
   return RR_OK;
 }
@@ -1023,8 +1020,8 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.keys_ready, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.copies_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.xstream, hipStreamNonBlocking);
-    for (hipEvent_t* ev : {&s.ev_keys[0], &s.ev_keys[1], &s.ev_xdone[0], &s.ev_xdone[1], &s.ev_cdone, &s.ev_qread[0],
-                           &s.ev_qread[1], &s.ev_scr[0], &s.ev_scr[1]})
+    for (hipEvent_t* ev : {&s.ev_keys[0], &s.ev_keys[1], &s.ev_xdone[0], &s.ev_xdone[1], &s.ev_cdone, &s.ev_scr[0],
+                           &s.ev_scr[1]})
       if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e != hipSuccess) {
       rr_destroy(h);

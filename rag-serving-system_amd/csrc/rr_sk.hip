@@ -403,6 +403,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // ---- query side: this wave's K-slice of every query as MFMA B operands, |q| and split exponents.
   // Runs while the prologue slabs above are in flight (their latency overlaps the query loads).
   QFrag<DT, NS> qfs[QH];
+  // the screen's per-query scalars from the fragments' own loads (SCR): this lane's sum of x^2 and of |x| over the
+  // query values it converts (its part of the wave's K-slice)
+  float scr_ss = 0.f, scr_sa = 0.f;
   auto build_frags = [&]() {
     // lane: query r (+ 32 per half), K half h
 #pragma unroll
@@ -451,6 +454,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
               const _Float16 c0 = (_Float16)x;
               qf.c0[j][t][e] = c0;
               qf.c1[j][t][e] = (_Float16)(x - (float)c0);
+              scr_ss = fmaf(x, x, scr_ss);
+              scr_sa += fabsf(x);
             }
           }
         } else if constexpr (DT == 2) {
@@ -485,6 +490,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
                 const _Float16 c0 = (_Float16)x[e];
                 qf.c0[j][t][e] = c0;
                 qf.c1[j][t][e] = (_Float16)(x[e] - (float)c0);
+                scr_ss = fmaf(x[e], x[e], scr_ss);
+                scr_sa += fabsf(x[e]);
               }
             }
           }
@@ -559,7 +566,20 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       }
     }
     __syncthreads();
-  } else if (COS || DT == 2 || SCR) {
+  } else if constexpr (SCR) {
+    // The screen's |q| and sum|q| from the values the fragments were built from (each wave holds its K-slice of
+    // every query; lanes r and r + 32 the two halves): per-wave partials in the verify scratch (unused in MODE 0),
+    // summed per query in wave order below. No second read of the query rows: every workgroup re-reading all 32
+    // rows from L2 was the larger part of the launch's start-up (8-10 us). The order of these sums differs from
+    // the exact path's |q|, so the bound takes a 2^-18 relative bump for it (rr_sk.hip epilogue).
+    const float ss = scr_ss + __shfl_xor(scr_ss, 32, 64), sa = scr_sa + __shfl_xor(scr_sa, 32, 64);
+    float* part = (float*)vW;
+    if (lane < 32) {
+      part[w * 32 + lane] = ss;
+      part[kWaves * 32 + w * 32 + lane] = sa;
+    }
+    __syncthreads();
+  } else if (COS || DT == 2) {
     const int nc = d >> 2;                      // float4 per row (d <= 1024 on this kernel: <= 4 per lane)
 #pragma unroll
     for (int g4 = 0; g4 < QH; ++g4) {
@@ -642,9 +662,20 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   constexpr int LPQ = 16 / QH, DPL = 2 * QH;
   const int qe = 4 * QH * w + lane / LPQ, er = DPL * (lane % LPQ);
   const bool qev = MODE == 1 ? qe == vq : qe < b;
-  const float qn = COS || SCR ? qinfo[qe] : 0.f;
+  float qn = COS && !SCR ? qinfo[qe] : 0.f;
   const float qs = DT == 2 ? qinfo[QS + qe] : 1.f;
-  const float qsa = SCR ? qinfo[QS + qe] : 0.f;
+  float qsa = 0.f;
+  if constexpr (SCR) {
+    const float* part = (const float*)vW;
+    float s2 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < kWaves; ++ww) {
+      s2 += part[ww * 32 + qe];
+      s1 += part[kWaves * 32 + ww * 32 + qe];
+    }
+    qn = sqrtf(s2);
+    qsa = s1 * (1.0f + 0x1p-18f);
+  }
 
   TopK<KT> tk;
   tk.init();
@@ -874,7 +905,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         float u;
         if constexpr (COS) {
           u = v * __builtin_amdgcn_rcpf(cos_den(qn, nd));
-          u += fabsf(u) * 0x1p-20f + 0x1p-126f;
+          u += fabsf(u) * 0x1p-18f + 0x1p-126f;   // (+ |q| in another summation order than the exact path's)
           u = fminf(fmaxf(u, -1.0f), 1.0f);   // the exact score is clipped to [-1, 1] (retriever.py:609)
         } else {
           u = v;

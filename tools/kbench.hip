@@ -231,6 +231,9 @@ int main(int argc, char** argv) {
   CK(launch_synth(1, 1234, 0, n, d, c32, s));
   CK(launch_synth(1, 99, 0, b, d, q, s));
   CK(launch_f32_to_bf16(c32, c16, n, d, s));
+  uint16_t* cf16;   // the f16 screening copy (DT 7)
+  CK(hipMalloc(&cf16, (size_t)n * d * 2));
+  CK(launch_f32_to_f16(c32, cf16, n, d, s));
   CK(launch_row_norms(0, c32, n, d, norms, s));
   float *csplit, *norms2, *rscale;
   CK(hipMalloc(&csplit, (size_t)n * d * 4));
@@ -258,8 +261,8 @@ int main(int argc, char** argv) {
 #ifdef RR_SK_PROBE
   if (argc > 3 && strcmp(argv[3], "probe") == 0) {   // per-workgroup phase timestamps of the split-K kernel
     struct P { const char* name; int dt; int cos; const void* c; const float* nr; };
-    const P ps[] = {{"sk fp32 (DT 3) cos", 3, 1, c32, norms}, {"sk bf16 (DT 1) cos", 1, 1, c16, norms},
-                    {"sk fp32 (DT 3) dot", 3, 0, c32, norms}};
+    const P ps[] = {{"sk f16 screen copy (DT 7) cos", 7, 1, cf16, norms}, {"sk fp32 (DT 3) cos", 3, 1, c32, norms},
+                    {"sk bf16 (DT 1) cos", 1, 1, c16, norms}, {"sk fp32 (DT 3) dot", 3, 0, c32, norms}};
     std::vector<unsigned long long> h((size_t)grid * 8);
     for (const P& p : ps) {
       for (int rep = 0; rep < 4; ++rep) {
