@@ -207,7 +207,7 @@ struct QFrag<7, NS> { f16x8 c0[NS][4], c1[NS][4]; };          // screen over the
 // LDS byte offset (within a slot) of 16-byte column position cp of tile row r (swizzled image)
 __device__ __forceinline__ int slab_off(int r, int cp) { return (r >> 3) * 1024 + (r & 7) * 128 + ((cp ^ (r & 7)) << 4); }
 
-// Verify stage (MODE 1): the screen's [nlists][QS][KT] upper-bound lists -> this query's global top-KT by u
+// Verify stage (MODE 1): the screen's [QS][nlists][KT] upper-bound lists -> this query's global top-KT by u
 // in akeys[] (LDS), KT rounds of a wave-wide max per wave, then one wave merges the 8 wave lists.
 template <int KT>
 __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict__ in, int nlists, int qslots, int q,
@@ -215,14 +215,14 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   TopK<KT> tk;
   if (tid < nlists) {
-    const uint64_t* src = in + ((size_t)tid * qslots + q) * KT;
+    const uint64_t* src = in + ((size_t)q * nlists + tid) * KT;   // query-major screen lists
 #pragma unroll
     for (int i = 0; i < KT; ++i) tk.v[i] = src[i];
   } else {
     tk.init();
   }
   for (int l = tid + kThreads; l < nlists; l += kThreads) {   // lists beyond 512 folded in (sorted input)
-    const uint64_t* src = in + ((size_t)l * qslots + q) * KT;
+    const uint64_t* src = in + ((size_t)q * nlists + l) * KT;
     for (int i = 0; i < KT; ++i) {
       const uint64_t key = src[i];
       if (key <= tk.last()) break;
@@ -983,7 +983,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     }
   }
   if constexpr (MODE == 0) {
-    uint64_t* dst = a.out + ((size_t)g * QS + qe) * KT;
+    // the screen's lists go query-major, [QS][grid][KT]: each verify workgroup then reads its query's lists as
+    // one contiguous block (the other paths' merge_kernel reads [grid][QS][KT])
+    uint64_t* dst = a.out + (SCR ? ((size_t)qe * G + g) : ((size_t)g * QS + qe)) * KT;
 #pragma unroll 1
     for (int rnd = 0; rnd < KT; ++rnd) {
       const uint64_t m = group_max_u64<LPQ>(tk.v[0]);
