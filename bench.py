@@ -278,6 +278,9 @@ def main() -> None:
     achieved = alg_bytes / avg_kernel_s / 1e9 if launches else None
     step_s = elapsed / args.steps
     consistent = bool(launches) and avg_kernel_s <= step_s * 1.001
+    # screened blocks on two compute streams (small shards): consecutive screens overlap at their ends, so a launch's
+    # event-timed span includes time shared with its neighbour; the per-step rate is then the sustained figure
+    streams = ix.compute_streams() if args.dtype == "fp32" else 1
     if args.pmc_child:            # only the fused-kernel launches matter to the parent's PMC parse
         ix.close()
         return
@@ -371,6 +374,11 @@ def main() -> None:
                          "kernel_timing": f"HIP events on the kernel's stream around every {every}-th "
                                           f"similarity-kernel launch of the timed region ({launches} launches)",
                          "kernel_le_step": consistent,
+                         "compute_streams": streams,
+                         "step_frac": round(alg_bytes / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                         "step_frac_note": "algorithmic bytes of one launch / ms_per_step: the sustained fraction of "
+                                           "peak over the timed steps (with two compute streams the launches overlap "
+                                           "and a launch's own span overstates its time)",
                          "alg_bytes_per_launch": alg_bytes,
                          "screen_copy": bool(screen16),
                          "screened_blocks": scr_blocks, "screen_fallbacks": scr_fallbacks},

@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -62,12 +63,24 @@ struct Shard {
   float* qbuf[2] = {nullptr, nullptr};   // staged queries, double-buffered ([q_cap][d] fp32 each): a new
                                          // batch is copied into one while verifies may still read the other
   hipEvent_t ev_scr[2] = {nullptr, nullptr};     // compute stream: a block's verify done ([0]: the flag-count copy)
+  // Two compute streams (rr_set_compute_streams): screened blocks of parity 1 run on cstream2, so block i + 1's
+  // screen starts while block i's screen drains its last chunks and its verify runs. Everything else stays on
+  // `stream`; the two meet through events: ev_fork (stream -> cstream2: queries staged, other searches' work),
+  // ev_join (cstream2 -> stream), ev_vdone[p] (the last verify on parity p's stream: verifies that write the same
+  // results follow each other).
+  hipStream_t cstream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_vdone[2] = {nullptr, nullptr};
+  bool fork_pending = false;   // ev_fork was recorded since cstream2 last waited on it
+  bool c2_busy = false;        // cstream2 holds work `stream` has not joined
+  int last_vpar = -1;          // parity of the last screened verify (results written in place)
   int q_cap = 0;
   uint64_t* cand = nullptr;              // 2 x [grid][64][32] per-workgroup candidates (the screened search
   int cand_grid = 0;                     // alternates the halves by parity; the other paths use half 0)
   int* scount = nullptr;                 // screened search: blocks this shard flagged for the exact pass
   int* pin_scount = nullptr;             // pinned host copy of scount, refreshed after each verify (no sync)
-  uint32_t* ctr = nullptr;               // split-K chunk counter (dynamic schedule), 0 between launches
+  uint32_t* ctr = nullptr;               // split-K chunk counters (dynamic schedule), 0 between launches: one per
+                                         // compute stream, kCtrStride words apart
   uint64_t* shard_keys = nullptr;        // [32][k_cap] this shard's top-k (all-gather send buffer)
   uint64_t* gathered = nullptr;          // [world][32][k_cap] (all-gather receive buffer)
   // pipelined exchange (k <= RR_FUSED_KMAX, world > 1): the exchange of search i (all-gather + final
@@ -157,6 +170,7 @@ struct rr_handle {
   int last_qpar = 0;            // ... and the query buffer it read
   int qpar = 0;                 // the staged queries live in every shard's qbuf[qpar]
   int dyn_sched = 1;            // split-K kernels: dynamic chunk schedule (rr_set_schedule)
+  int streams = 0;              // compute streams for screened blocks (rr_set_compute_streams; 0 = by shard size)
   int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy)
   int64_t narrow_blocks = 0;    // screened blocks run with 16-entry lists where 2k + 2 wanted 32 (screen_kt)
   int64_t narrow_reruns = 0;    // ... and re-runs of such searches
@@ -179,6 +193,8 @@ constexpr int kXTail = 8;
 // shard are selected in kSelParts groups first when they hold more than 8192 keys per query.
 constexpr int kWideMax = 256;
 constexpr int kSelParts = 8;
+// chunk counters of the two compute streams: one 128-byte line each
+constexpr int kCtrStride = 32;
 
 // How each public corpus dtype is stored and multiplied (rr_internal.h KDT_*).
 int kdt_of(int dtype) {
@@ -224,7 +240,10 @@ int free_shard(Shard& s) {
   for (hipEvent_t e : {s.ev_keys[0], s.ev_keys[1], s.ev_xdone[0], s.ev_xdone[1], s.ev_cdone, s.ev_scr[0],
                        s.ev_scr[1]})
     if (e) hipEventDestroy(e);
+  for (hipEvent_t e : {s.ev_fork, s.ev_join, s.ev_vdone[0], s.ev_vdone[1]})
+    if (e) hipEventDestroy(e);
   if (s.xstream) hipStreamDestroy(s.xstream);
+  if (s.cstream2) hipStreamDestroy(s.cstream2);
   if (s.comm) ncclCommDestroy(s.comm);
   if (s.stream) hipStreamDestroy(s.stream);
   s = Shard();
@@ -389,6 +408,9 @@ int drop_work_buffers(rr_handle* h) {
     HIP_TRY(hipSetDevice(s.dev));
     HIP_TRY(hipStreamSynchronize(s.stream));
     HIP_TRY(hipStreamSynchronize(s.xstream));
+    HIP_TRY(hipStreamSynchronize(s.cstream2));
+    s.c2_busy = s.fork_pending = false;
+    s.last_vpar = -1;
     void** ptrs[] = {(void**)&s.qbuf[0], (void**)&s.qbuf[1], (void**)&s.cand, (void**)&s.scount, (void**)&s.ctr, (void**)&s.shard_keys, (void**)&s.gathered,
                      (void**)&s.out_base, (void**)&s.full_keys, (void**)&s.sorted, &s.sort_temp,
                      (void**)&s.wcand, (void**)&s.wfloor, (void**)&s.wsel,
@@ -466,8 +488,8 @@ int ensure_buffers(rr_handle* h, int b, int k) {
       HIP_TRY(hipMemset(s.scount, 0, sizeof(int)));
       if (!s.pin_scount) HIP_TRY(hipHostMalloc((void**)&s.pin_scount, sizeof(int), hipHostMallocDefault));
       *(volatile int*)s.pin_scount = 0;
-      if (int rc = dmalloc(&s.ctr, sizeof(uint32_t))) return rc;
-      HIP_TRY(hipMemset(s.ctr, 0, sizeof(uint32_t)));
+      if (int rc = dmalloc(&s.ctr, 2 * kCtrStride * sizeof(uint32_t))) return rc;
+      HIP_TRY(hipMemset(s.ctr, 0, 2 * kCtrStride * sizeof(uint32_t)));
     }
     if ((h->world > 1 || h->dist) && !s.px_keys[0]) {
       for (int p = 0; p < 2; ++p) {
@@ -496,6 +518,8 @@ int ensure_full_sort(rr_handle* h, Shard& s, int k) {
   const size_t need = (size_t)rr::kQSlots * std::max<int64_t>(s.rows(), (int64_t)h->world * k);
   if (need > s.full_cap) {
     HIP_TRY(hipStreamSynchronize(s.stream));   // the old buffers may still be in use
+    HIP_TRY(hipStreamSynchronize(s.cstream2));
+    s.c2_busy = false;
     if (int rc = dmalloc(&s.full_keys, need * 8)) return rc;
     if (int rc = dmalloc(&s.sorted, need * 8)) return rc;
     s.full_cap = need;
@@ -563,6 +587,12 @@ void check_narrow(rr_handle* h) {
 //   an 8 % margin on each.
 constexpr float kScreenEpsA = 6.0e-4f;
 constexpr float kScreenEpsB = 4.0e-8f;
+// DT 7 (the f16 copy) multiplies the query as ONE f16 piece (half the matrix-core work of the two-piece split, which
+// measured 3-5 % faster per search: less power drawn, less clock throttling): q - f16(q) <= 2^-11 |q_k| + 2^-25 per
+// element adds <= 2^-11 |x||q| + 2^-25 sqrt(d) |x| (the cross term with the rounding of x is < 2^-22 |x||q|, inside
+// the margins; 8 instead of 16 MFMAs per wave partial only shrink the accumulation term).
+constexpr float kScreen16EpsA = 1.1e-3f;
+constexpr float kScreen16EpsB = 7.5e-8f;
 
 bool screened(const rr_handle* h, int k, int slots) {
   return (h->kernel == RR_KERNEL_AUTO || h->kernel == RR_KERNEL_SCREEN_FALLBACK) && h->dtype == RR_DTYPE_F32 &&
@@ -609,6 +639,40 @@ int collect_timing(rr_handle* h) {
   return RR_OK;
 }
 
+// Screened blocks alternate between two compute streams on shards of at most this many rows (rr_set_compute_streams
+// 0): there a block's fixed costs — start-up, the last chunks, the verify — are a large part of the step and the
+// next block's screen fills them; on larger shards two screens in flight at once streamed slower than one after
+// the other (profiles/r02/ab/ab_streams.txt).
+constexpr int64_t kTwoStreamRows = 600000;
+bool two_streams(const rr_handle* h, const Shard& s) {
+  return h->streams == 2 || (h->streams == 0 && s.rows() <= kTwoStreamRows);
+}
+// The compute stream of a screened block of parity p.
+hipStream_t cstream(const rr_handle* h, const Shard& s, int p) {
+  return p == 1 && two_streams(h, s) ? s.cstream2 : s.stream;
+}
+// `stream` follows everything enqueued on cstream2 so far (current device = s.dev).
+int join_main(Shard& s) {
+  if (!s.c2_busy) return RR_OK;
+  HIP_TRY(hipEventRecord(s.ev_join, s.cstream2));
+  HIP_TRY(hipStreamWaitEvent(s.stream, s.ev_join, 0));
+  s.c2_busy = false;
+  return RR_OK;
+}
+// Work just enqueued on `stream` (staged queries, another kind of search) that the next cstream2 block follows.
+int fork_point(Shard& s) {
+  HIP_TRY(hipEventRecord(s.ev_fork, s.stream));
+  s.fork_pending = true;
+  return RR_OK;
+}
+int fork_all(rr_handle* h) {
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    if (int rc = fork_point(s)) return rc;
+  }
+  return RR_OK;
+}
+
 // Single-process exchange (several local shards, possibly on the same device): every shard copies every
 // other shard's [32][kk] keys into its `gathered` slot with peer DMA, ordered by events. The same
 // layout the RCCL all-gather produces in multi-process mode.
@@ -636,11 +700,11 @@ int local_gather(rr_handle* h, size_t per) {
 // process per GPU, peer copies within one process) into px_gathered[p] and merges it into the results,
 // while the compute stream goes on with the next block. px_keys[p] is rewritten two blocks later and only
 // after ev_xdone[p] of every shard that read it (enqueue_block).
-int enqueue_exchange_px(rr_handle* h, int p, int q0, int bb, int k, int kt, int slots, bool keys_on_x) {
+int enqueue_exchange_px(rr_handle* h, int p, int q0, int bb, int k, int kt, int slots, bool scr) {
   const size_t slot = (size_t)slots * kt + kXTail;   // keys + the shard's flag word
-  for (Shard& s : h->shards) {   // px_keys[p] is written: by the compute stream, or by the verify on xstream
+  for (Shard& s : h->shards) {   // px_keys[p] is written on the block's compute stream (a screened block: its parity's)
     HIP_TRY(hipSetDevice(s.dev));
-    HIP_TRY(hipEventRecord(s.ev_keys[p], keys_on_x ? s.xstream : s.stream));
+    HIP_TRY(hipEventRecord(s.ev_keys[p], scr ? cstream(h, s, p) : s.stream));
   }
   for (Shard& dst : h->shards) {
     HIP_TRY(hipSetDevice(dst.dev));
@@ -687,7 +751,7 @@ rr::SkArgs sk_base(const rr_handle* h, const Shard& s, const float* qb, int bb) 
 }
 
 // Enqueue the device pipeline for query block [q0, q0 + bb) (bb <= slots) on every local shard.
-int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
+int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
   const int d = h->d;
   const bool scr = screened(h, k, slots);
   const bool wk = !scr && wide(h, k);
@@ -714,10 +778,10 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
     };
     // pipelined exchange: px_keys[p] is rewritten only after every exchange that read it has finished
     // (its own all-gather; within one process also the other shards' peer copies of it)
-    auto wait_px = [&](int par) -> hipError_t {
+    auto wait_px = [&](int par, hipStream_t ws) -> hipError_t {
       for (const Shard& o : h->shards)
         if (&o == &s || local_multi)
-          if (hipError_t e = hipStreamWaitEvent(s.stream, o.ev_xdone[par], 0)) return e;
+          if (hipError_t e = hipStreamWaitEvent(ws, o.ev_xdone[par], 0)) return e;
       return hipSuccess;
     };
     const float* qb = s.qbuf[h->qpar] + (size_t)q0 * d;
@@ -735,24 +799,35 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
       // follows in-stream: a cross-stream hand-off costs ~20-25 us of dispatch latency on MI355X
       // (profiles/r02/steps/), more than the ~17 us verify that running it on the exchange stream overlapped.
       // With an exchange, px_keys[p] is rewritten only after its previous exchange (two blocks back) is done.
-      hipStream_t vs = s.stream;
-      if (multi) HIP_TRY(wait_px(p));
+      // (two compute streams: parity 1 on cstream2, after the work of `stream` it must follow)
+      const hipStream_t cs = cstream(h, s, p), vs = cs;
+      if (cs != s.stream) {
+        if (s.fork_pending) HIP_TRY(hipStreamWaitEvent(cs, s.ev_fork, 0));
+        s.fork_pending = false;
+        s.c2_busy = true;
+      }
+      if (multi) HIP_TRY(wait_px(p, cs));
       uint64_t* candp = s.cand + (size_t)p * cand_half(s);
       const int sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(s.cand_grid, (s.rows() + 31) / 32));
-      if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
+      if (timed) HIP_TRY(hipEventRecord(e0, cs));
       if (s.rows() > 0) {
         rr::SkArgs a = sk_base(h, s, qb, bb);
         a.out = candp;
-        a.eps_a = kScreenEpsA;
-        a.eps_b = kScreenEpsB;
+        a.ctr = s.ctr + (cs == s.stream ? 0 : kCtrStride);
         a.sqrt_d = sqrtf((float)d) * (1.0f + 0x1p-20f);
         // the f16 copy holds exactly the values the fp32-reading screen rounds to: half the bytes
         const bool s16 = s.scr16 && h->screen_copy && rr::sk_slabs(rr::KDT_SCREEN16, d);
+        a.eps_a = s16 ? kScreen16EpsA : kScreenEpsA;
+        a.eps_b = s16 ? kScreen16EpsB : kScreenEpsB;
         if (s16) a.corpus = (const char*)s.scr16;
         HIP_TRY(rr::launch_sk_args(s16 ? rr::KDT_SCREEN16 : rr::KDT_SCREEN, h->metric, kt, 0, sgrid, rr::kQSlots, a,
-                                   s.stream));
+                                   cs));
       }
-      if (timed) HIP_TRY(hipEventRecord(e1, s.stream));
+      if (timed) HIP_TRY(hipEventRecord(e1, cs));
+      // results written in place (no exchange): this verify follows the previous one when that ran on the other
+      // stream (the same rows of the result buffer)
+      const bool chain = !multi && two_streams(h, s);
+      if (chain && s.last_vpar >= 0 && s.last_vpar != p) HIP_TRY(hipStreamWaitEvent(vs, s.ev_vdone[s.last_vpar], 0));
       if (s.rows() > 0) {
         rr::SkArgs v = sk_base(h, s, qb, bb);
         v.vin = candp;
@@ -770,6 +845,10 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
       } else {   // a shard without rows contributes empty lists
         HIP_TRY(hipMemsetAsync(s.px_keys[p], 0, (size_t)slots * kt * 8, vs));
       }
+      if (chain) {
+        HIP_TRY(hipEventRecord(s.ev_vdone[p], vs));
+        s.last_vpar = p;
+      }
       // the flagged-block count reaches the host without a sync (read a block or two late by check_narrow), every
       // 8th block, on the exchange stream so that the copy gates nothing on the compute stream. (No event is
       // recorded on the other blocks: each record between two kernels widened the dispatch gap.)
@@ -780,8 +859,8 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
       }
     } else if (kt) {
       int grid = fused_grid(s);
-      HIP_TRY(wait_px(0));   // no screened verify still reads cand or writes the results
-      HIP_TRY(wait_px(1));
+      HIP_TRY(wait_px(0, s.stream));   // no screened verify still reads cand or writes the results
+      HIP_TRY(wait_px(1, s.stream));
       if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
       if (s.rows() > 0) {
         if (use_sk(h)) {
@@ -800,7 +879,7 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
       if (!multi) {
         HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, nullptr, osc, oix, s.stream, slots));
       } else {
-        HIP_TRY(wait_px(p));
+        HIP_TRY(wait_px(p, s.stream));
         HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, s.px_keys[p], nullptr, nullptr, s.stream, slots));
       }
     } else if (wk) {
@@ -808,8 +887,8 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
       // (wide output, with a floor above everything it dropped), then a radix select over those lists — one
       // stage, or kSelParts groups then their union — gives the shard's top-k and checks it against the
       // floors: unproven -> the block's flag word (the host re-runs the search with the full sort).
-      HIP_TRY(wait_px(0));
-      HIP_TRY(wait_px(1));
+      HIP_TRY(wait_px(0, s.stream));
+      HIP_TRY(wait_px(1, s.stream));
       HIP_TRY(wait_copies());
       if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
       uint64_t* flagw = multi ? s.shard_keys + (size_t)rr::kQSlots * k : (uint64_t*)s.out_base;
@@ -874,8 +953,8 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
       const int64_t rows = s.rows();
       if (int rc = ensure_full_sort(h, s, k)) return rc;
       if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
-      HIP_TRY(wait_px(0));   // no pipelined exchange or screened verify still uses the buffers
-      HIP_TRY(wait_px(1));
+      HIP_TRY(wait_px(0, s.stream));   // no pipelined exchange or screened verify still uses the buffers
+      HIP_TRY(wait_px(1, s.stream));
       HIP_TRY(wait_copies());
       HIP_TRY(hipMemsetAsync(s.shard_keys, 0, (size_t)rr::kQSlots * k * 8, s.stream));
       if (rows > 0) {
@@ -907,7 +986,7 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
     return RR_OK;
   }
   if (kt) {
-    if (int rc = enqueue_exchange_px(h, p, q0, bb, k, kt, slots, false)) return rc;
+    if (int rc = enqueue_exchange_px(h, p, q0, bb, k, kt, slots, scr)) return rc;
     h->parity ^= 1;
     return RR_OK;
   }
@@ -957,6 +1036,20 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
   return RR_OK;
 }
 
+// Enqueue one block: a screened block goes on its parity's compute stream; any other block runs on `stream`
+// after everything on cstream2, and later cstream2 blocks follow it.
+int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
+  const bool scr = screened(h, k, slots);
+  if (!scr)
+    for (Shard& s : h->shards) {
+      HIP_TRY(hipSetDevice(s.dev));
+      if (int rc = join_main(s)) return rc;
+      s.last_vpar = -1;
+    }
+  if (int rc = enqueue_block_body(h, q0, bb, k, slots)) return rc;
+  return scr ? RR_OK : fork_all(h);
+}
+
 // A new batch goes into the query buffer the last search did not read: every reader of a query buffer runs on
 // the compute stream, where the new batch's copy is ordered after them. The last checked search can be re-run
 // only while its buffer is intact, so it is settled first when its buffer is the one about to be rewritten
@@ -965,6 +1058,10 @@ int begin_stage(rr_handle* h, int* nq) {
   const int t = h->qpar ^ 1;
   if (h->last_screened && !h->last_settled && h->last_qpar == t)
     if (int rc = rr_synchronize(h)) return rc;
+  for (Shard& s : h->shards) {   // cstream2 blocks may still read that buffer
+    HIP_TRY(hipSetDevice(s.dev));
+    if (int rc = join_main(s)) return rc;
+  }
   *nq = t;
   return RR_OK;
 }
@@ -1020,14 +1117,16 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.keys_ready, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.copies_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.xstream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.cstream2, hipStreamNonBlocking);
     for (hipEvent_t* ev : {&s.ev_keys[0], &s.ev_keys[1], &s.ev_xdone[0], &s.ev_xdone[1], &s.ev_cdone, &s.ev_scr[0],
-                           &s.ev_scr[1]})
+                           &s.ev_scr[1], &s.ev_fork, &s.ev_join, &s.ev_vdone[0], &s.ev_vdone[1]})
       if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e != hipSuccess) {
       rr_destroy(h);
       return fail(RR_E_HIP, "event setup failed: %s", hipGetErrorString(e));
     }
   }
+  if (const char* e = getenv("RR_COMPUTE_STREAMS")) h->streams = std::min(2, std::max(0, atoi(e)));   // (A/B)
   *out = h;
   return RR_OK;
 }
@@ -1221,6 +1320,7 @@ int rr_set_queries(rr_handle* h, const float* host_q, int32_t b, int32_t d) {
     HIP_TRY(hipMemcpyAsync(s.qbuf[nq], h->pin_q, qbytes, hipMemcpyHostToDevice, s.stream));
     HIP_TRY(hipEventRecord(s.pin_q_free, s.stream));
   }
+  if (int rc = fork_all(h)) return rc;
   h->qpar = nq;
   h->cur_b = b;
   return RR_OK;
@@ -1242,6 +1342,7 @@ int rr_set_queries_device(rr_handle* h, const float* dev_q, int32_t b, int32_t d
     else
       HIP_TRY(hipMemcpyPeerAsync(s.qbuf[nq], s.dev, dev_q, src_dev, (size_t)b * d * 4, s.stream));
   }
+  if (int rc = fork_all(h)) return rc;
   h->qpar = nq;
   h->cur_b = b;
   return RR_OK;
@@ -1283,6 +1384,8 @@ int sync_streams(rr_handle* h) {
     HIP_TRY(hipSetDevice(s.dev));
     HIP_TRY(hipStreamSynchronize(s.stream));
     HIP_TRY(hipStreamSynchronize(s.xstream));
+    HIP_TRY(hipStreamSynchronize(s.cstream2));
+    s.c2_busy = false;
   }
   return collect_timing(h);
 }
@@ -1405,6 +1508,7 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
     HIP_TRY(hipSetDevice(s.dev));
     HIP_TRY(hipMemcpyAsync(s.qbuf[nq], a.pin, qbytes, hipMemcpyHostToDevice, s.stream));
   }
+  if (int rc = fork_all(h)) return rc;
   h->qpar = nq;
   h->cur_b = b;
   if (int rc = rr_search_staged(h, k)) return rc;
@@ -1412,7 +1516,10 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
   // (the serial k > 32 exchange also orders it after itself), else the compute stream
   Shard& s0 = h->shards[0];
   HIP_TRY(hipSetDevice(s0.dev));
-  hipStream_t rs = (h->world > 1 || h->dist) ? s0.xstream : s0.stream;
+  const bool xchg = h->world > 1 || h->dist;
+  hipStream_t rs = xchg ? s0.xstream : s0.stream;
+  if (!xchg)
+    if (int rc = join_main(s0)) return rc;   // the last verify may have run on cstream2
   HIP_TRY(hipMemcpyAsync(a.pin + res_off, s0.out_base, kOutHead, hipMemcpyDeviceToHost, rs));
   HIP_TRY(hipMemcpyAsync(a.pin + res_off + kOutHead, s0.out_scores, cnt * 4, hipMemcpyDeviceToHost, rs));
   HIP_TRY(hipMemcpyAsync(a.pin + idx_off, s0.out_idx, cnt * 8, hipMemcpyDeviceToHost, rs));
@@ -1451,6 +1558,7 @@ int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx) {
       HIP_TRY(hipSetDevice(s.dev));
       HIP_TRY(hipMemcpyAsync(s.qbuf[nq], a.pin, qbytes, hipMemcpyHostToDevice, s.stream));
     }
+    if (int rc = fork_all(h)) return rc;
     h->qpar = nq;
     h->cur_b = a.b;
     const int saved = h->kernel;
@@ -1494,6 +1602,18 @@ int rr_set_schedule(rr_handle* h, int dynamic) {
   if (!h) return fail(RR_E_INVALID, "null handle");
   if (int rc = sync_streams(h)) return rc;   // no launch in flight uses the counter
   h->dyn_sched = dynamic ? 1 : 0;
+  return RR_OK;
+}
+
+int rr_set_compute_streams(rr_handle* h, int32_t n, int32_t* in_use) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  if (n < -1 || n > 2) return fail(RR_E_INVALID, "compute streams %d (-1 = as is, 0 = by shard size, 1, 2)", n);
+  if (n >= 0 && n != h->streams) {
+    if (int rc = rr_synchronize(h)) return rc;
+    for (Shard& s : h->shards) s.last_vpar = -1;
+    h->streams = n;
+  }
+  if (in_use) *in_use = h->shards.empty() ? 1 : (two_streams(h, h->shards[0]) ? 2 : 1);
   return RR_OK;
 }
 

@@ -32,6 +32,8 @@
 //     only. Half of DT 0's matrix-core cycles (and no f32-MFMA clock throttling).
 //   6 SCREEN over fp32 rows: x rounded to f16 (one v_cvt_pk_f16_f32 per pair), q = c0 + c1 in f16, two f16
 //     MFMAs per K-step. Not a score: the key is an UPPER BOUND u >= the DT 3 score (see "Screened search").
+//   7 SCREEN over the f16 copy of fp32 rows (the values DT 6 rounds to, stored: half the bytes), q as ONE f16
+//     piece, one f16 MFMA per K-step (the wider bound of rr_api.cpp kScreen16EpsA/B covers q's rounding).
 // The K order inside a wave's slice is a permutation applied identically to both operands.
 //
 // Screened search (fp32 storage, k <= 29; rr_api.cpp enqueue_block):
@@ -201,18 +203,29 @@ struct QFrag<3, NS> { bf16x8 c0[NS][2], c1[NS][2], c2[NS][2]; };
 template <int NS>
 struct QFrag<6, NS> { f16x8 c0[NS][2], c1[NS][2]; };          // screen: q = c0 + c1 (+ <= 2^-22 |q|)
 template <int NS>
-struct QFrag<7, NS> { f16x8 c0[NS][4], c1[NS][4]; };          // screen over the f16 copy: 4 K-steps per slab
+struct QFrag<7, NS> { f16x8 c0[NS][4]; };   // screen over the f16 copy: 4 K-steps per slab, q as one f16 piece
 
 
 // LDS byte offset (within a slot) of 16-byte column position cp of tile row r (swizzled image)
 __device__ __forceinline__ int slab_off(int r, int cp) { return (r >> 3) * 1024 + (r & 7) * 128 + ((cp ^ (r & 7)) << 4); }
 
 // Verify stage (MODE 1): the screen's [QS][nlists][KT] upper-bound lists -> this query's global top-KT by u
-// in akeys[] (LDS), KT rounds of a wave-wide max per wave, then one wave merges the 8 wave lists.
+// in akeys[] (LDS, descending), by rank selection instead of KT rounds of wave-wide maxima:
+//   1. thread l holds list l (sorted; lists beyond kThreads folded into thread l % kThreads's list);
+//   2. H = the KT-th largest list head (its rank among the heads is KT - 1; 0 when fewer than KT heads are
+//      non-empty). Every key of the global top-KT is >= H: KT distinct heads are >= H, so a key below H has
+//      rank >= KT. Only the <= KT lists whose head is >= H can hold such keys: <= KT x KT candidates;
+//   3. the non-empty keys >= H are appended to an LDS array, and the candidate of rank r < KT is akeys[r].
+// Keys are unique (distinct row indices), so ranks are distinct. Scratch: LDS free in MODE 1 (the slab ring):
+// [kThreads] heads, [KT * KT] candidates, H, count.
 template <int KT>
 __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict__ in, int nlists, int qslots, int q,
-                                                      uint64_t* W, uint64_t* akeys) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+                                                      uint64_t* scratch, uint64_t* akeys) {
+  const int tid = threadIdx.x;
+  uint64_t* heads = scratch;
+  uint64_t* cand = scratch + kThreads;
+  uint64_t* hs = cand + KT * KT;
+  int* cnt = (int*)(hs + 1);
   TopK<KT> tk;
   if (tid < nlists) {
     const uint64_t* src = in + ((size_t)q * nlists + tid) * KT;   // query-major screen lists
@@ -221,7 +234,7 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
   } else {
     tk.init();
   }
-  for (int l = tid + kThreads; l < nlists; l += kThreads) {   // lists beyond 512 folded in (sorted input)
+  for (int l = tid + kThreads; l < nlists; l += kThreads) {   // lists beyond kThreads folded in (sorted input)
     const uint64_t* src = in + ((size_t)q * nlists + l) * KT;
     for (int i = 0; i < KT; ++i) {
       const uint64_t key = src[i];
@@ -229,26 +242,38 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
       tk.insert(key);
     }
   }
-  for (int rnd = 0; rnd < KT; ++rnd) {
-    const uint64_t m = wave_max_u64(tk.v[0]);
-    if (lane == 0) W[wid * KT + rnd] = m;
-    if (m != 0 && tk.v[0] == m) tk.pop();   // keys are unique: exactly one owner
+  const int nl = nlists < kThreads ? nlists : kThreads;
+  if (tid == 0) {
+    hs[0] = 0;
+    cnt[0] = 0;
+  }
+  if (tid < nl) heads[tid] = tk.v[0];
+  __syncthreads();
+  if (tid < nl && tk.v[0] != 0) {
+    const uint64_t me = tk.v[0];
+    int rank = 0;
+    for (int j = 0; j < nl; ++j) rank += heads[j] > me ? 1 : 0;   // (broadcast LDS reads)
+    if (rank == KT - 1) hs[0] = me;
   }
   __syncthreads();
-  if (wid == 0) {
-    constexpr int PER = (kWaves * KT + 63) / 64;   // per-wave winners held per lane
-    uint64_t e[PER];
+  const uint64_t th = hs[0];
+  if (tid < nl && tk.v[0] != 0 && tk.v[0] >= th) {
+    int c = 0;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) e[i] = lane + 64 * i < kWaves * KT ? W[lane + 64 * i] : 0;
-    for (int rnd = 0; rnd < KT; ++rnd) {
-      uint64_t best = 0;
+    for (int i = 0; i < KT; ++i) c += tk.v[i] != 0 && tk.v[i] >= th ? 1 : 0;   // a prefix of the sorted list
+    const int pos = atomicAdd(cnt, c);
 #pragma unroll
-      for (int i = 0; i < PER; ++i) best = umax64(best, e[i]);
-      best = wave_max_u64(best);
-#pragma unroll
-      for (int i = 0; i < PER; ++i) e[i] = (best != 0 && e[i] == best) ? 0 : e[i];
-      if (lane == 0) akeys[rnd] = best;
-    }
+    for (int i = 0; i < KT; ++i)
+      if (i < c) cand[pos + i] = tk.v[i];
+  }
+  __syncthreads();
+  const int m = cnt[0];
+  if (tid < KT && tid >= m) akeys[tid] = 0;   // fewer than KT keys in all: empty tail
+  for (int c = tid; c < m; c += kThreads) {
+    const uint64_t me = cand[c];
+    int rank = 0;
+    for (int j = 0; j < m; ++j) rank += cand[j] > me ? 1 : 0;
+    if (rank < KT) akeys[rank] = me;
   }
   __syncthreads();
 }
@@ -451,9 +476,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const float x = e < 4 ? va[e] : vb[e - 4];
-              const _Float16 c0 = (_Float16)x;
-              qf.c0[j][t][e] = c0;
-              qf.c1[j][t][e] = (_Float16)(x - (float)c0);
+              qf.c0[j][t][e] = (_Float16)x;
               scr_ss = fmaf(x, x, scr_ss);
               scr_sa += fabsf(x);
             }
@@ -522,7 +545,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
             asm volatile("" : "+v"(qfs[qh].c0[j][t]), "+v"(qfs[qh].c1[j][t]), "+v"(qfs[qh].c2[j][t]));
         } else if constexpr (DT == 7) {
 #pragma unroll
-          for (int t = 0; t < 4; ++t) asm volatile("" : "+v"(qfs[qh].c0[j][t]), "+v"(qfs[qh].c1[j][t]));
+          for (int t = 0; t < 4; ++t) asm volatile("" : "+v"(qfs[qh].c0[j][t]));
         } else {
 #pragma unroll
           for (int t = 0; t < 2; ++t) asm volatile("" : "+v"(qfs[qh].c0[j][t]), "+v"(qfs[qh].c1[j][t]));
@@ -634,8 +657,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // ---- MODE 1: this query's candidates (the queries' fragments and scalars above are already built, so
   // their loads overlapped the list loads), then their rows straight into registers ---------------------------
   if constexpr (MODE == 1) {
+    static_assert((size_t)(kThreads + KT * KT + 2) * 8 <= ring_bytes(RS), "verify merge scratch in the slab ring");
     SK_PROBE(6);
-    merge_lists_for_query<KT>(a.vin, a.nlists, QS, vq, vW, akeys);
+    merge_lists_for_query<KT>(a.vin, a.nlists, QS, vq, (uint64_t*)smem, akeys);
     SK_PROBE(7);
     if (tid < 32) {
       const uint64_t k0 = akeys[0];
@@ -783,7 +807,6 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[t], qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
-          for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[t], qfs[qh].c1[j][t], accs[qh], 0, 0, 0);
         }
       } else if constexpr (DT == 2) {
         f16x8 ah[2], al[2];

@@ -41,7 +41,7 @@ RR_KERNEL_AUTO = 0
 RR_KERNEL_FUSED = 1
 RR_KERNEL_EXACT = 2
 RR_KERNEL_SCREEN_FALLBACK = 3
-RR_ABI_VERSION = 3
+RR_ABI_VERSION = 4
 
 DTYPES = {"fp32": RR_DTYPE_F32, "float32": RR_DTYPE_F32, "f32": RR_DTYPE_F32,
           "bf16": RR_DTYPE_BF16, "bfloat16": RR_DTYPE_BF16, "fp32-split": RR_DTYPE_F32_SPLIT}
@@ -77,6 +77,7 @@ SIGNATURES = {
     "rr_screen_stats": (_c_int, [_vp, _i64p, _i64p]),
     "rr_set_schedule": (_c_int, [_vp, _c_int]),
     "rr_screen_copy": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_i32)]),
+    "rr_set_compute_streams": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_i32)]),
     "rr_last_shape": (_c_int, [_vp, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32)]),
     "rr_dist_info": (_c_int, [_vp, _ip, _ip]),
 }
@@ -306,6 +307,13 @@ class Index:
     def set_schedule(self, dynamic: bool) -> None:
         """Split-K work schedule: dynamic chunk counter (default) or static round-robin chunks."""
         _check(self._lib.rr_set_schedule(self._h, 1 if dynamic else 0))
+
+    def compute_streams(self, n: Optional[int] = None) -> int:
+        """Screened search blocks on 2 alternating compute streams, 1, or 0 = by shard size (the default; results
+        identical); None leaves the setting. Returns the streams shard 0 uses (1 or 2)."""
+        u = _c_i32()
+        _check(self._lib.rr_set_compute_streams(self._h, -1 if n is None else int(n), ctypes.byref(u)))
+        return u.value
 
     def screen_copy(self, use: Optional[bool] = None) -> bool:
         """The screened search's f16 copy of fp32 rows (half the bytes per screen pass; results unchanged):

@@ -253,3 +253,42 @@ def test_narrow_lists_switch_to_wide(Index):
     assert blocks == 80 and 64 <= flagged <= 70 and flagged == flagged70     # none after the switch
     ix.close()
     ex.close()
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0]])
+def test_two_compute_streams_match_one(Index, devices):
+    """Screened blocks alternate between two compute streams (the default): a mixed sequence of staged searches
+    (several back to back, then fetched), multi-block batches, other k, another kind of search in between, and
+    four asynchronous searches in flight gives, step by step, exactly the one-stream results."""
+    corpus = synth.unit_norm_gaussian(31, 40000, 1024)
+    qa = synth.unit_norm_gaussian(32, 32, 1024)
+    qb = synth.unit_norm_gaussian(33, 77, 1024)
+    qs = [synth.unit_norm_gaussian(34 + i, 1 + 19 * i, 1024) for i in range(6)]
+
+    def run(streams):
+        ix = Index(devices=devices, dtype="fp32", metric="cosine")
+        ix.load(corpus)
+        assert ix.compute_streams(streams) == streams
+        out = []
+        ix.set_queries(qa)
+        for k in (5, 5, 7):
+            ix.search_staged(k)
+        out.append(ix.fetch())
+        ix.set_queries(qb)
+        ix.search_staged(10)
+        ix.search_staged(3)
+        out.append(ix.fetch())
+        out.append(ix.search(qa, 40))            # large k: another kind of search between screened ones
+        out.append(ix.search(qb, 12))
+        tickets = [ix.search_async(q, 4 + i) for i, q in enumerate(qs[:4])]
+        out += [ix.wait(t) for t in tickets]
+        tickets = [ix.search_async(q, 9) for q in qs[4:]]
+        ix.set_queries(qa)
+        ix.search_staged(2)
+        out += [ix.wait(t) for t in tickets]
+        out.append(ix.fetch())
+        ix.close()
+        return out
+
+    for (s1, i1), (s2, i2) in zip(run(1), run(2)):
+        assert np.array_equal(i1, i2) and np.array_equal(s1, s2)
