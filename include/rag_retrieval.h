@@ -195,12 +195,12 @@ int rr_set_kernel(rr_handle* h, int kernel);
  * (chunks dealt round-robin). Results are identical; for A/B measurements. */
 int rr_set_schedule(rr_handle* h, int dynamic);
 
-/* Compute streams of the screened search (fp32 storage): 2 = consecutive search blocks alternate between two
- * streams, so one block's screen starts while the previous block's screen drains its last chunks and its
- * exact verify runs (verifies that write the same results still follow each other); 1 = every block on one
- * stream; 0 (default) = 2 on shards of up to 600 000 rows, else 1; -1 = leave as is. Results are identical.
- * *in_use (may be null): the streams local shard 0's screened blocks use (1 or 2). Synchronises the handle's
- * streams when the setting changes. */
+/* Compute streams of the screened search (fp32 storage): 2 (default) = consecutive search blocks alternate
+ * between two streams, so one block's screen starts while the previous block's screen drains its last chunks
+ * and its exact verify runs (the screen then leaves 32 CUs to the verify; verifies that write the same results
+ * still follow each other); 1 = every block on one stream, every CU screening; -1 = leave as is. Results are
+ * identical. *in_use (may be null): the streams in use (1 or 2). Synchronises the handle's streams when the
+ * setting changes. */
 int rr_set_compute_streams(rr_handle* h, int32_t n, int32_t* in_use);
 
 /* The screened search's f16 copy (fp32 storage): the screen pass reads an f16 copy of the rows — exactly the

@@ -63,17 +63,24 @@ struct Shard {
   float* qbuf[2] = {nullptr, nullptr};   // staged queries, double-buffered ([q_cap][d] fp32 each): a new
                                          // batch is copied into one while verifies may still read the other
   hipEvent_t ev_scr[2] = {nullptr, nullptr};     // compute stream: a block's verify done ([0]: the flag-count copy)
-  // Two compute streams (rr_set_compute_streams): screened blocks of parity 1 run on cstream2, so block i + 1's
-  // screen starts while block i's screen drains its last chunks and its verify runs. Everything else stays on
-  // `stream`; the two meet through events: ev_fork (stream -> cstream2: queries staged, other searches' work),
-  // ev_join (cstream2 -> stream), ev_vdone[p] (the last verify on parity p's stream: verifies that write the same
-  // results follow each other).
+  // Two compute streams (rr_set_compute_streams): screened blocks of parity 1 run on cstream2 (stream index 1),
+  // so block i + 1's screen starts while block i's screen drains its last chunks and its verify runs. Other work
+  // runs on `stream` (index 0). Ordering between the two, by events:
+  //   ev_q[t][i]  the last screened verify on stream i that read query buffer t: a new batch written into buffer t
+  //               on the other stream waits for it; the next verify on the other stream waits for the last one
+  //               (they write the same result rows; a pending async D2H of those rows re-records it);
+  //   ev_stage    the current batch's copy into its query buffer, on the stream of the first block after it: the
+  //               other stream's first block waits for it;
+  //   ev_fork     `stream` -> cstream2 after other kinds of search; ev_join cstream2 -> `stream` before them.
   hipStream_t cstream2 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  hipEvent_t ev_vdone[2] = {nullptr, nullptr};
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_stage = nullptr;
+  hipEvent_t ev_q[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  bool q_rd[2][2] = {{false, false}, {false, false}};   // ev_q[t][i] recorded, no writer of buffer t waited on it yet
   bool fork_pending = false;   // ev_fork was recorded since cstream2 last waited on it
   bool c2_busy = false;        // cstream2 holds work `stream` has not joined
-  int last_vpar = -1;          // parity of the last screened verify (results written in place)
+  int stage_si = 0;            // stream index that staged the current batch
+  bool stage_pending = false;  // ... and the other stream has not waited on ev_stage yet
+  int last_vsi = -1, last_vq = 0;   // the last screened verify: its stream index and query buffer
   int q_cap = 0;
   uint64_t* cand = nullptr;              // 2 x [grid][64][32] per-workgroup candidates (the screened search
   int cand_grid = 0;                     // alternates the halves by parity; the other paths use half 0)
@@ -170,12 +177,14 @@ struct rr_handle {
   int last_qpar = 0;            // ... and the query buffer it read
   int qpar = 0;                 // the staged queries live in every shard's qbuf[qpar]
   int dyn_sched = 1;            // split-K kernels: dynamic chunk schedule (rr_set_schedule)
-  int streams = 0;              // compute streams for screened blocks (rr_set_compute_streams; 0 = by shard size)
+  int streams = 2;              // compute streams for screened blocks (rr_set_compute_streams)
+  int screen_grid = 1 << 30;    // screen workgroups at most (A/B: RR_SCREEN_GRID)
   int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy)
   int64_t narrow_blocks = 0;    // screened blocks run with 16-entry lists where 2k + 2 wanted 32 (screen_kt)
   int64_t narrow_reruns = 0;    // ... and re-runs of such searches
   bool screen_wide = false;     // narrow lists re-ran too often on this corpus: use the wide ones
   bool last_narrow = false;     // the last search ran narrow lists
+  bool last_scr_block = false;  // the last block enqueued was a screened one
 };
 
 namespace {
@@ -240,7 +249,7 @@ int free_shard(Shard& s) {
   for (hipEvent_t e : {s.ev_keys[0], s.ev_keys[1], s.ev_xdone[0], s.ev_xdone[1], s.ev_cdone, s.ev_scr[0],
                        s.ev_scr[1]})
     if (e) hipEventDestroy(e);
-  for (hipEvent_t e : {s.ev_fork, s.ev_join, s.ev_vdone[0], s.ev_vdone[1]})
+  for (hipEvent_t e : {s.ev_fork, s.ev_join, s.ev_stage, s.ev_q[0][0], s.ev_q[0][1], s.ev_q[1][0], s.ev_q[1][1]})
     if (e) hipEventDestroy(e);
   if (s.xstream) hipStreamDestroy(s.xstream);
   if (s.cstream2) hipStreamDestroy(s.cstream2);
@@ -409,8 +418,9 @@ int drop_work_buffers(rr_handle* h) {
     HIP_TRY(hipStreamSynchronize(s.stream));
     HIP_TRY(hipStreamSynchronize(s.xstream));
     HIP_TRY(hipStreamSynchronize(s.cstream2));
-    s.c2_busy = s.fork_pending = false;
-    s.last_vpar = -1;
+    s.c2_busy = s.fork_pending = s.stage_pending = false;
+    s.q_rd[0][0] = s.q_rd[0][1] = s.q_rd[1][0] = s.q_rd[1][1] = false;
+    s.last_vsi = -1;
     void** ptrs[] = {(void**)&s.qbuf[0], (void**)&s.qbuf[1], (void**)&s.cand, (void**)&s.scount, (void**)&s.ctr, (void**)&s.shard_keys, (void**)&s.gathered,
                      (void**)&s.out_base, (void**)&s.full_keys, (void**)&s.sorted, &s.sort_temp,
                      (void**)&s.wcand, (void**)&s.wfloor, (void**)&s.wsel,
@@ -639,18 +649,24 @@ int collect_timing(rr_handle* h) {
   return RR_OK;
 }
 
-// Screened blocks alternate between two compute streams on shards of at most this many rows (rr_set_compute_streams
-// 0): there a block's fixed costs — start-up, the last chunks, the verify — are a large part of the step and the
-// next block's screen fills them; on larger shards two screens in flight at once streamed slower than one after
-// the other (profiles/r02/ab/ab_streams.txt).
-constexpr int64_t kTwoStreamRows = 600000;
-bool two_streams(const rr_handle* h, const Shard& s) {
-  return h->streams == 2 || (h->streams == 0 && s.rows() <= kTwoStreamRows);
+// Screened blocks alternate between two compute streams (rr_set_compute_streams 2, the default): block i + 1's screen
+// runs into block i's last chunks and verify. The screen then leaves kVerifyCUs CUs to the verify (one workgroup per
+// query slot, each needing a whole CU's LDS): it runs at once beside the next screen instead of waiting for CUs.
+// Measured against one stream and every CU screening (profiles/r02/ab/ab_screen_grid*.txt): +23-45 % per step at
+// 125k-250k rows, +2-5 % at 1M-2M.
+constexpr int kVerifyCUs = 32;
+bool two_streams(const rr_handle* h, const Shard&) { return h->streams == 2; }
+// Screen workgroups on shard s; `alone`: no screened block is in flight on the other stream (its last verify has
+// completed: a single search, or the first of a burst), so nothing overlaps this one and every CU screens.
+int screen_grid(const rr_handle* h, const Shard& s, bool alone) {
+  int g = s.cand_grid;
+  if (two_streams(h, s) && !alone) g = std::max(g / 2, g - kVerifyCUs);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(std::min(g, h->screen_grid), (s.rows() + 31) / 32));
 }
-// The compute stream of a screened block of parity p.
-hipStream_t cstream(const rr_handle* h, const Shard& s, int p) {
-  return p == 1 && two_streams(h, s) ? s.cstream2 : s.stream;
-}
+// Stream index of a screened block of parity p, and a stream by index.
+int block_si(const rr_handle* h, const Shard& s, int p) { return p == 1 && two_streams(h, s) ? 1 : 0; }
+hipStream_t stream_of(const Shard& s, int si) { return si ? s.cstream2 : s.stream; }
+hipStream_t cstream(const rr_handle* h, const Shard& s, int p) { return stream_of(s, block_si(h, s, p)); }
 // `stream` follows everything enqueued on cstream2 so far (current device = s.dev).
 int join_main(Shard& s) {
   if (!s.c2_busy) return RR_OK;
@@ -669,6 +685,39 @@ int fork_all(rr_handle* h) {
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
     if (int rc = fork_point(s)) return rc;
+  }
+  return RR_OK;
+}
+
+// Copy a batch of queries into every shard's query buffer t, on the stream of the next screened block: from pinned
+// host memory (src_dev < 0) or device memory on src_dev. pin_ev: record each shard's pin_q_free after its copy.
+int stage_queries(rr_handle* h, int t, const void* src, size_t bytes, int src_dev, bool pin_ev) {
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    const bool two = two_streams(h, s);
+    const int x = block_si(h, s, h->parity);
+    const hipStream_t xs = stream_of(s, x);
+    if (two) {
+      if (s.q_rd[t][x ^ 1]) HIP_TRY(hipStreamWaitEvent(xs, s.ev_q[t][x ^ 1], 0));   // its last readers there
+      s.q_rd[t][x ^ 1] = false;
+      if (x == 1) {   // after other kinds of search on `stream` (they read query buffers too)
+        if (s.fork_pending) HIP_TRY(hipStreamWaitEvent(xs, s.ev_fork, 0));
+        s.fork_pending = false;
+        s.c2_busy = true;
+      }
+    }
+    if (src_dev < 0)
+      HIP_TRY(hipMemcpyAsync(s.qbuf[t], src, bytes, hipMemcpyHostToDevice, xs));
+    else if (s.dev == src_dev)
+      HIP_TRY(hipMemcpyAsync(s.qbuf[t], src, bytes, hipMemcpyDeviceToDevice, xs));
+    else
+      HIP_TRY(hipMemcpyPeerAsync(s.qbuf[t], s.dev, src, src_dev, bytes, xs));
+    if (pin_ev) HIP_TRY(hipEventRecord(s.pin_q_free, xs));
+    if (two) {
+      HIP_TRY(hipEventRecord(s.ev_stage, xs));
+      s.stage_si = x;
+      s.stage_pending = true;
+    }
   }
   return RR_OK;
 }
@@ -799,16 +848,24 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       // follows in-stream: a cross-stream hand-off costs ~20-25 us of dispatch latency on MI355X
       // (profiles/r02/steps/), more than the ~17 us verify that running it on the exchange stream overlapped.
       // With an exchange, px_keys[p] is rewritten only after its previous exchange (two blocks back) is done.
-      // (two compute streams: parity 1 on cstream2, after the work of `stream` it must follow)
-      const hipStream_t cs = cstream(h, s, p), vs = cs;
-      if (cs != s.stream) {
-        if (s.fork_pending) HIP_TRY(hipStreamWaitEvent(cs, s.ev_fork, 0));
-        s.fork_pending = false;
-        s.c2_busy = true;
+      // (two compute streams: parity 1 on cstream2, after the work of the other stream it must follow)
+      const bool two = two_streams(h, s);
+      const int bsi = block_si(h, s, p), t = h->qpar;
+      const hipStream_t cs = stream_of(s, bsi), vs = cs;
+      if (two) {
+        if (s.stage_pending && bsi != s.stage_si) HIP_TRY(hipStreamWaitEvent(cs, s.ev_stage, 0));
+        if (bsi != s.stage_si) s.stage_pending = false;
+        if (bsi == 1) {
+          if (s.fork_pending) HIP_TRY(hipStreamWaitEvent(cs, s.ev_fork, 0));
+          s.fork_pending = false;
+          s.c2_busy = true;
+        }
       }
       if (multi) HIP_TRY(wait_px(p, cs));
       uint64_t* candp = s.cand + (size_t)p * cand_half(s);
-      const int sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(s.cand_grid, (s.rows() + 31) / 32));
+      const bool alone = !two || s.last_vsi < 0 || s.last_vsi == bsi ||
+                         hipEventQuery(s.ev_q[s.last_vq][s.last_vsi]) == hipSuccess;
+      const int sgrid = screen_grid(h, s, alone);
       if (timed) HIP_TRY(hipEventRecord(e0, cs));
       if (s.rows() > 0) {
         rr::SkArgs a = sk_base(h, s, qb, bb);
@@ -826,8 +883,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       if (timed) HIP_TRY(hipEventRecord(e1, cs));
       // results written in place (no exchange): this verify follows the previous one when that ran on the other
       // stream (the same rows of the result buffer)
-      const bool chain = !multi && two_streams(h, s);
-      if (chain && s.last_vpar >= 0 && s.last_vpar != p) HIP_TRY(hipStreamWaitEvent(vs, s.ev_vdone[s.last_vpar], 0));
+      if (two && !multi && s.last_vsi >= 0 && s.last_vsi != bsi)
+        HIP_TRY(hipStreamWaitEvent(vs, s.ev_q[s.last_vq][s.last_vsi], 0));
       if (s.rows() > 0) {
         rr::SkArgs v = sk_base(h, s, qb, bb);
         v.vin = candp;
@@ -845,9 +902,11 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       } else {   // a shard without rows contributes empty lists
         HIP_TRY(hipMemsetAsync(s.px_keys[p], 0, (size_t)slots * kt * 8, vs));
       }
-      if (chain) {
-        HIP_TRY(hipEventRecord(s.ev_vdone[p], vs));
-        s.last_vpar = p;
+      if (two) {   // this verify (the last reader of query buffer t on this stream)
+        HIP_TRY(hipEventRecord(s.ev_q[t][bsi], vs));
+        s.q_rd[t][bsi] = true;
+        s.last_vsi = bsi;
+        s.last_vq = t;
       }
       // the flagged-block count reaches the host without a sync (read a block or two late by check_narrow), every
       // 8th block, on the exchange stream so that the copy gates nothing on the compute stream. (No event is
@@ -1044,9 +1103,10 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
     for (Shard& s : h->shards) {
       HIP_TRY(hipSetDevice(s.dev));
       if (int rc = join_main(s)) return rc;
-      s.last_vpar = -1;
+      s.last_vsi = -1;
     }
   if (int rc = enqueue_block_body(h, q0, bb, k, slots)) return rc;
+  h->last_scr_block = scr;
   return scr ? RR_OK : fork_all(h);
 }
 
@@ -1058,10 +1118,7 @@ int begin_stage(rr_handle* h, int* nq) {
   const int t = h->qpar ^ 1;
   if (h->last_screened && !h->last_settled && h->last_qpar == t)
     if (int rc = rr_synchronize(h)) return rc;
-  for (Shard& s : h->shards) {   // cstream2 blocks may still read that buffer
-    HIP_TRY(hipSetDevice(s.dev));
-    if (int rc = join_main(s)) return rc;
-  }
+
   *nq = t;
   return RR_OK;
 }
@@ -1119,14 +1176,16 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.xstream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.cstream2, hipStreamNonBlocking);
     for (hipEvent_t* ev : {&s.ev_keys[0], &s.ev_keys[1], &s.ev_xdone[0], &s.ev_xdone[1], &s.ev_cdone, &s.ev_scr[0],
-                           &s.ev_scr[1], &s.ev_fork, &s.ev_join, &s.ev_vdone[0], &s.ev_vdone[1]})
+                           &s.ev_scr[1], &s.ev_fork, &s.ev_join, &s.ev_stage, &s.ev_q[0][0], &s.ev_q[0][1],
+                           &s.ev_q[1][0], &s.ev_q[1][1]})
       if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e != hipSuccess) {
       rr_destroy(h);
       return fail(RR_E_HIP, "event setup failed: %s", hipGetErrorString(e));
     }
   }
-  if (const char* e = getenv("RR_COMPUTE_STREAMS")) h->streams = std::min(2, std::max(0, atoi(e)));   // (A/B)
+  if (const char* e = getenv("RR_COMPUTE_STREAMS")) h->streams = atoi(e) == 1 ? 1 : 2;   // (A/B)
+  if (const char* e = getenv("RR_SCREEN_GRID")) h->screen_grid = std::max(1, atoi(e));               // (A/B)
   *out = h;
   return RR_OK;
 }
@@ -1315,12 +1374,7 @@ int rr_set_queries(rr_handle* h, const float* host_q, int32_t b, int32_t d) {
   memcpy(h->pin_q, host_q, qbytes);
   int nq = 0;
   if (int rc = begin_stage(h, &nq)) return rc;
-  for (Shard& s : h->shards) {
-    HIP_TRY(hipSetDevice(s.dev));
-    HIP_TRY(hipMemcpyAsync(s.qbuf[nq], h->pin_q, qbytes, hipMemcpyHostToDevice, s.stream));
-    HIP_TRY(hipEventRecord(s.pin_q_free, s.stream));
-  }
-  if (int rc = fork_all(h)) return rc;
+  if (int rc = stage_queries(h, nq, h->pin_q, qbytes, -1, true)) return rc;
   h->qpar = nq;
   h->cur_b = b;
   return RR_OK;
@@ -1335,14 +1389,7 @@ int rr_set_queries_device(rr_handle* h, const float* dev_q, int32_t b, int32_t d
   const int src_dev = h->shards[0].dev;
   int nq = 0;
   if (int rc = begin_stage(h, &nq)) return rc;
-  for (Shard& s : h->shards) {
-    HIP_TRY(hipSetDevice(s.dev));
-    if (s.dev == src_dev)
-      HIP_TRY(hipMemcpyAsync(s.qbuf[nq], dev_q, (size_t)b * d * 4, hipMemcpyDeviceToDevice, s.stream));
-    else
-      HIP_TRY(hipMemcpyPeerAsync(s.qbuf[nq], s.dev, dev_q, src_dev, (size_t)b * d * 4, s.stream));
-  }
-  if (int rc = fork_all(h)) return rc;
+  if (int rc = stage_queries(h, nq, dev_q, (size_t)b * d * 4, src_dev, false)) return rc;
   h->qpar = nq;
   h->cur_b = b;
   return RR_OK;
@@ -1504,11 +1551,7 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
   memcpy(a.pin, host_q, qbytes);
   int nq = 0;
   if (int rc = begin_stage(h, &nq)) return rc;
-  for (Shard& s : h->shards) {
-    HIP_TRY(hipSetDevice(s.dev));
-    HIP_TRY(hipMemcpyAsync(s.qbuf[nq], a.pin, qbytes, hipMemcpyHostToDevice, s.stream));
-  }
-  if (int rc = fork_all(h)) return rc;
+  if (int rc = stage_queries(h, nq, a.pin, qbytes, -1, false)) return rc;
   h->qpar = nq;
   h->cur_b = b;
   if (int rc = rr_search_staged(h, k)) return rc;
@@ -1517,13 +1560,17 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
   Shard& s0 = h->shards[0];
   HIP_TRY(hipSetDevice(s0.dev));
   const bool xchg = h->world > 1 || h->dist;
-  hipStream_t rs = xchg ? s0.xstream : s0.stream;
-  if (!xchg)
-    if (int rc = join_main(s0)) return rc;   // the last verify may have run on cstream2
+  // without an exchange: after a screened search, on the stream of its last verify (the copy then holds back the
+  // next verify on the other stream, which rewrites the rows: ev_q re-recorded below); else on `stream`
+  const bool on_v = !xchg && h->last_scr_block && s0.last_vsi >= 0;
+  hipStream_t rs = xchg ? s0.xstream : on_v ? stream_of(s0, s0.last_vsi) : s0.stream;
+  if (!xchg && !on_v)
+    if (int rc = join_main(s0)) return rc;
   HIP_TRY(hipMemcpyAsync(a.pin + res_off, s0.out_base, kOutHead, hipMemcpyDeviceToHost, rs));
   HIP_TRY(hipMemcpyAsync(a.pin + res_off + kOutHead, s0.out_scores, cnt * 4, hipMemcpyDeviceToHost, rs));
   HIP_TRY(hipMemcpyAsync(a.pin + idx_off, s0.out_idx, cnt * 8, hipMemcpyDeviceToHost, rs));
   HIP_TRY(hipEventRecord(a.done, rs));
+  if (on_v) HIP_TRY(hipEventRecord(s0.ev_q[s0.last_vq][s0.last_vsi], rs));
   a.b = b;
   a.k = k;
   a.ticket = t;
@@ -1554,11 +1601,7 @@ int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx) {
     if (int rc = sync_streams(h)) return rc;
     int nq = 0;
     if (int rc = begin_stage(h, &nq)) return rc;
-    for (Shard& s : h->shards) {
-      HIP_TRY(hipSetDevice(s.dev));
-      HIP_TRY(hipMemcpyAsync(s.qbuf[nq], a.pin, qbytes, hipMemcpyHostToDevice, s.stream));
-    }
-    if (int rc = fork_all(h)) return rc;
+    if (int rc = stage_queries(h, nq, a.pin, qbytes, -1, false)) return rc;
     h->qpar = nq;
     h->cur_b = a.b;
     const int saved = h->kernel;
@@ -1607,10 +1650,10 @@ int rr_set_schedule(rr_handle* h, int dynamic) {
 
 int rr_set_compute_streams(rr_handle* h, int32_t n, int32_t* in_use) {
   if (!h) return fail(RR_E_INVALID, "null handle");
-  if (n < -1 || n > 2) return fail(RR_E_INVALID, "compute streams %d (-1 = as is, 0 = by shard size, 1, 2)", n);
-  if (n >= 0 && n != h->streams) {
+  if (n < -1 || n == 0 || n > 2) return fail(RR_E_INVALID, "compute streams %d (-1 = as is, 1, 2)", n);
+  if (n > 0 && n != h->streams) {
     if (int rc = rr_synchronize(h)) return rc;
-    for (Shard& s : h->shards) s.last_vpar = -1;
+    for (Shard& s : h->shards) s.last_vsi = -1;
     h->streams = n;
   }
   if (in_use) *in_use = h->shards.empty() ? 1 : (two_streams(h, h->shards[0]) ? 2 : 1);

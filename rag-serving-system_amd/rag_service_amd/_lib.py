@@ -309,8 +309,8 @@ class Index:
         _check(self._lib.rr_set_schedule(self._h, 1 if dynamic else 0))
 
     def compute_streams(self, n: Optional[int] = None) -> int:
-        """Screened search blocks on 2 alternating compute streams, 1, or 0 = by shard size (the default; results
-        identical); None leaves the setting. Returns the streams shard 0 uses (1 or 2)."""
+        """Screened search blocks on 2 alternating compute streams (the default) or 1 (results identical); None
+        leaves the setting. Returns the streams in use."""
         u = _c_i32()
         _check(self._lib.rr_set_compute_streams(self._h, -1 if n is None else int(n), ctypes.byref(u)))
         return u.value

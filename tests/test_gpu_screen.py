@@ -287,6 +287,16 @@ def test_two_compute_streams_match_one(Index, devices):
         ix.search_staged(2)
         out += [ix.wait(t) for t in tickets]
         out.append(ix.fetch())
+        ix.set_kernel("screen-fallback")          # every block flagged: rr_wait re-stages and re-runs exactly
+        tickets = [ix.search_async(q, 6) for q in qs[:3]]
+        out += [ix.wait(t) for t in tickets]
+        ix.set_kernel("auto")
+        tickets = []
+        for q in qs:                               # the serving pattern: a new batch per search, 2 in flight
+            tickets.append(ix.search_async(q, 5))
+            if len(tickets) > 2:
+                out.append(ix.wait(tickets.pop(0)))
+        out += [ix.wait(t) for t in tickets]
         ix.close()
         return out
 

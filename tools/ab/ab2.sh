@@ -7,12 +7,12 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/$1
 read DOCS B K DT <<< "$2"
 shift 2
-W="--docs $DOCS --dtype $DT --batch $B --k $K --no-cpu-baseline --variants= --ingest-rows 0 --no-pmc --steps ${STEPS:-20} --warmup ${WARMUP:-5} --latency-steps 5 --steady-steps ${STEADY:-200}"
+W="--docs $DOCS --dtype $DT --batch $B --k $K --no-cpu-baseline --variants= --ingest-rows 0 --no-pmc --steps ${STEPS:-20} --warmup ${WARMUP:-5} --latency-steps ${LAT:-5} --steady-steps ${STEADY:-200}"
 echo "# $DOCS rows, batch $B, k $K, $DT: window value ms kernel_us | steady value ms kernel_us" >> "$OUT"
 for rep in $(seq ${REPS:-2}); do
   for arm in "$@"; do
     IFS=: read NAME DIR ENVS <<< "$arm"
     ( cd "$R/$DIR" && env ${ENVS//,/ } timeout -k 10 200 python3 bench.py --gpus 1 $W > /tmp/ab.json 2>/tmp/ab.err ) || { echo "$NAME FAILED" >> "$OUT"; tail -5 /tmp/ab.err >> "$OUT"; exit 1; }
-    python3 -c "import json; d=json.loads(open('/tmp/ab.json').read().strip().splitlines()[-1]); s=d['steady_state']; r=d['roofline']; print('$NAME', d['value'], d['ms_per_step'], r['kernel_avg_us'], '| steady', s['value'], s['ms_per_step'], s['kernel_avg_us'], '| fb', r.get('screen_fallbacks'), '/', r.get('screened_blocks'))" >> "$OUT"
+    python3 -c "import json; d=json.loads(open('/tmp/ab.json').read().strip().splitlines()[-1]); s=d['steady_state']; r=d['roofline']; print('$NAME', d['value'], d['ms_per_step'], r['kernel_avg_us'], '| steady', s['value'], s['ms_per_step'], s['kernel_avg_us'], '| p50/p99', d['p50_ms'], d['p99_ms'], '| pipe', d['host_pipelined']['value'], '| fb', r.get('screen_fallbacks'), '/', r.get('screened_blocks'))" >> "$OUT"
   done
 done
