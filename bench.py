@@ -181,6 +181,9 @@ def main() -> None:
                     help="back-to-back steps timed again after the latency loop (steady-state rate, reported "
                          "beside value)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exchange-1rank", action="store_true",
+                    help="N=1: run the multi-GPU data path anyway (a 1-rank RCCL communicator: per-block all-gather "
+                         "of the candidates and the device merge), for measuring the exchange's cost on one GPU")
     ap.add_argument("--ingest-rows", type=int, default=262_144,
                     help="rows of a host fp32 array timed through rr_load (N=1 only; 0 = skip)")
     ap.add_argument("--cpu-budget", type=float, default=12.0,
@@ -226,6 +229,9 @@ def main() -> None:
     if world > 1:
         uid = broadcast_bytes(dist, get_unique_id() if rank == 0 else None)
         ix.init_dist(world, rank, uid)
+        rccl_ranks = ix.dist_info()[0]
+    elif args.exchange_1rank:
+        ix.init_dist(1, 0, get_unique_id())
         rccl_ranks = ix.dist_info()[0]
     ix.fill_synthetic(_lib.RR_SYNTH_UNIT_NORM, 1234, args.docs, args.dim)
     sb, se = ix.shard_range(0)
@@ -377,7 +383,7 @@ def main() -> None:
                              "note": "the same staged loop after the latency loops (GPU long out of idle); "
                                      "value above is the first K steps after W warm-up steps from idle"},
             "exchange": ("rccl ncclAllGather of per-shard top-k keys, device merge on every rank"
-                         if world > 1 else "none (one shard)"),
+                         if world > 1 or rccl_ranks else "none (one shard)"),
             "rccl_ranks": rccl_ranks,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -51,6 +51,8 @@ int fail(int code, const char* fmt, ...) {
                   __LINE__);                                                                 \
   } while (0)
 
+constexpr int kXSlots = 4;   // pipelined-exchange buffer sets (Shard::px_keys)
+
 struct Shard {
   int dev = 0;
   int cus = 256;
@@ -92,12 +94,21 @@ struct Shard {
   uint64_t* gathered = nullptr;          // [world][32][k_cap] (all-gather receive buffer)
   // pipelined exchange (k <= RR_FUSED_KMAX, world > 1): the exchange of search i (all-gather + final
   // merge) runs on xstream while the compute stream already scores search i + 1; buffers alternate by
-  // parity. px_keys[p] / px_gathered[p] are [32][KMAX] / [world][32][KMAX].
+  // slot (kXSlots of them, in turn: with two compute streams a block's verify ends about a step and a half after its
+  // screen began, so a slot is rewritten only after its exchange has had two more steps to finish). px_keys[x] /
+  // px_gathered[x] are [64][KMAX] + tail / [world][...].
   hipStream_t xstream = nullptr;
-  uint64_t* px_keys[2] = {nullptr, nullptr};
-  uint64_t* px_gathered[2] = {nullptr, nullptr};
-  hipEvent_t ev_keys[2] = {nullptr, nullptr};   // compute stream: px_keys[p] written
-  hipEvent_t ev_xdone[2] = {nullptr, nullptr};  // xstream: exchange of parity p finished (buffers free)
+  // Exchanges alternate between two lanes (slot x on lane x & 1): xstream + comm, xstream2 + comm2 (a split of comm),
+  // so two exchanges are in flight — each waits for its block's keys on another stream and for its peers, longer
+  // than a step on small shards. Their merges write the same result rows: a merge follows the previous one when that
+  // ran on the other lane (ev_xdone of last_x).
+  hipStream_t xstream2 = nullptr;
+  ncclComm_t comm2 = nullptr;
+  int last_x = -1;
+  uint64_t* px_keys[kXSlots] = {};
+  uint64_t* px_gathered[kXSlots] = {};
+  hipEvent_t ev_keys[kXSlots] = {};    // compute stream: px_keys[x] written
+  hipEvent_t ev_xdone[kXSlots] = {};   // xstream: exchange of slot x finished (buffers free)
   hipEvent_t ev_cdone = nullptr;                // compute stream: a serial (k > KMAX) exchange finished
   char* out_base = nullptr;              // one allocation: flag word at 0, scores at kOutHead, indices at out_off
   float* out_scores = nullptr;           // [q_cap][k_cap]
@@ -155,7 +166,8 @@ struct rr_handle {
   int32_t last_b = 0;   // batch of the last search (the shape rr_fetch_results writes)
   bool timing = false;
   int kernel = RR_KERNEL_AUTO;   // rr_set_kernel
-  int parity = 0;                // pipelined exchange: buffer set of the next search block
+  int parity = 0;                // the next search block's parity (candidate half, compute stream)
+  int xslot = 0;                 // the next pipelined exchange's buffer set (Shard::px_keys)
   double t_ms = 0.0;
   int64_t t_count = 0;
   // pinned host staging for the synchronous search path (rr_set_queries / rr_fetch_results): the queries
@@ -179,6 +191,8 @@ struct rr_handle {
   int dyn_sched = 1;            // split-K kernels: dynamic chunk schedule (rr_set_schedule)
   int streams = 2;              // compute streams for screened blocks (rr_set_compute_streams)
   int screen_grid = 1 << 30;    // screen workgroups at most (A/B: RR_SCREEN_GRID)
+  int xslots = kXSlots;         // pipelined-exchange buffer sets in use (A/B: RR_X_SLOTS, 2..kXSlots)
+  int x_delay_us = 0;           // A/B: RR_X_EXCHANGE_DELAY_US, a stand-in for a slower exchange
   int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy)
   int64_t narrow_blocks = 0;    // screened blocks run with 16-entry lists where 2k + 2 wanted 32 (screen_kt)
   int64_t narrow_reruns = 0;    // ... and re-runs of such searches
@@ -237,21 +251,29 @@ int dmalloc(T** p, size_t bytes) {
 int free_shard(Shard& s) {
   hipSetDevice(s.dev);
   void* ptrs[] = {s.corpus, s.scr16, s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.ctr, s.shard_keys, s.gathered, s.out_base,
-                  s.full_keys, s.sorted, s.sort_temp, s.wcand, s.wfloor, s.wsel, s.px_keys[0], s.px_keys[1], s.px_gathered[0], s.px_gathered[1]};
+                  s.full_keys, s.sorted, s.sort_temp, s.wcand, s.wfloor, s.wsel};
   for (void* p : ptrs)
     if (p) hipFree(p);
+  for (int x = 0; x < kXSlots; ++x) {
+    if (s.px_keys[x]) hipFree(s.px_keys[x]);
+    if (s.px_gathered[x]) hipFree(s.px_gathered[x]);
+    if (s.ev_keys[x]) hipEventDestroy(s.ev_keys[x]);
+    if (s.ev_xdone[x]) hipEventDestroy(s.ev_xdone[x]);
+  }
   for (hipEvent_t e : s.ev) hipEventDestroy(e);
   s.ev.clear();
   if (s.pin_scount) hipHostFree(s.pin_scount);
   if (s.keys_ready) hipEventDestroy(s.keys_ready);
   if (s.pin_q_free) hipEventDestroy(s.pin_q_free);
   if (s.copies_done) hipEventDestroy(s.copies_done);
-  for (hipEvent_t e : {s.ev_keys[0], s.ev_keys[1], s.ev_xdone[0], s.ev_xdone[1], s.ev_cdone, s.ev_scr[0],
+  for (hipEvent_t e : {s.ev_cdone, s.ev_scr[0],
                        s.ev_scr[1]})
     if (e) hipEventDestroy(e);
   for (hipEvent_t e : {s.ev_fork, s.ev_join, s.ev_stage, s.ev_q[0][0], s.ev_q[0][1], s.ev_q[1][0], s.ev_q[1][1]})
     if (e) hipEventDestroy(e);
   if (s.xstream) hipStreamDestroy(s.xstream);
+  if (s.xstream2) hipStreamDestroy(s.xstream2);
+  if (s.comm2) ncclCommDestroy(s.comm2);
   if (s.cstream2) hipStreamDestroy(s.cstream2);
   if (s.comm) ncclCommDestroy(s.comm);
   if (s.stream) hipStreamDestroy(s.stream);
@@ -417,19 +439,24 @@ int drop_work_buffers(rr_handle* h) {
     HIP_TRY(hipSetDevice(s.dev));
     HIP_TRY(hipStreamSynchronize(s.stream));
     HIP_TRY(hipStreamSynchronize(s.xstream));
+    HIP_TRY(hipStreamSynchronize(s.xstream2));
     HIP_TRY(hipStreamSynchronize(s.cstream2));
     s.c2_busy = s.fork_pending = s.stage_pending = false;
+    s.last_x = -1;
     s.q_rd[0][0] = s.q_rd[0][1] = s.q_rd[1][0] = s.q_rd[1][1] = false;
     s.last_vsi = -1;
     void** ptrs[] = {(void**)&s.qbuf[0], (void**)&s.qbuf[1], (void**)&s.cand, (void**)&s.scount, (void**)&s.ctr, (void**)&s.shard_keys, (void**)&s.gathered,
                      (void**)&s.out_base, (void**)&s.full_keys, (void**)&s.sorted, &s.sort_temp,
-                     (void**)&s.wcand, (void**)&s.wfloor, (void**)&s.wsel,
-                     (void**)&s.px_keys[0], (void**)&s.px_keys[1], (void**)&s.px_gathered[0],
-                     (void**)&s.px_gathered[1]};
+                     (void**)&s.wcand, (void**)&s.wfloor, (void**)&s.wsel};
     for (void** p : ptrs) {
       if (*p) HIP_TRY(hipFree(*p));
       *p = nullptr;
     }
+    for (int x = 0; x < kXSlots; ++x)
+      for (uint64_t** p : {&s.px_keys[x], &s.px_gathered[x]}) {
+        if (*p) HIP_TRY(hipFree(*p));
+        *p = nullptr;
+      }
     s.q_cap = s.k_cap = s.cand_grid = 0;
     s.full_cap = s.sort_temp_bytes = 0;
     s.out_scores = nullptr;
@@ -440,6 +467,7 @@ int drop_work_buffers(rr_handle* h) {
   h->last_k = 0;
   h->last_b = 0;
   h->parity = 0;
+  h->xslot = 0;
   h->screen_blocks = 0;   // the flagged-block counters (scount) were freed above
   h->screen_reruns = 0;
   h->narrow_blocks = h->narrow_reruns = 0;
@@ -502,7 +530,7 @@ int ensure_buffers(rr_handle* h, int b, int k) {
       HIP_TRY(hipMemset(s.ctr, 0, 2 * kCtrStride * sizeof(uint32_t)));
     }
     if ((h->world > 1 || h->dist) && !s.px_keys[0]) {
-      for (int p = 0; p < 2; ++p) {
+      for (int p = 0; p < kXSlots; ++p) {
         // each exchanged list carries its shard's screened-search flag word after the keys
         const size_t per = (size_t)kMaxSlots * RR_FUSED_KMAX + kXTail;
         if (int rc = dmalloc(&s.px_keys[p], per * 8)) return rc;
@@ -744,34 +772,37 @@ int local_gather(rr_handle* h, size_t per) {
   return RR_OK;
 }
 
-// Pipelined exchange (k <= RR_FUSED_KMAX, world > 1) of the search block just scored into px_keys[p]:
+// Pipelined exchange (k <= RR_FUSED_KMAX, world > 1) of the search block just scored into px_keys[x]:
 // each shard's xstream gathers every shard's [32][kt] list (one RCCL all-gather over xGMI with one
-// process per GPU, peer copies within one process) into px_gathered[p] and merges it into the results,
-// while the compute stream goes on with the next block. px_keys[p] is rewritten two blocks later and only
-// after ev_xdone[p] of every shard that read it (enqueue_block).
-int enqueue_exchange_px(rr_handle* h, int p, int q0, int bb, int k, int kt, int slots, bool scr) {
+// process per GPU, peer copies within one process) into px_gathered[x] and merges it into the results,
+// while the compute stream goes on with the next block. px_keys[x] is rewritten kXSlots blocks later and only
+// after ev_xdone[x] of every shard that read it (enqueue_block).
+int enqueue_exchange_px(rr_handle* h, int p, int x, int q0, int bb, int k, int kt, int slots, bool scr) {
   const size_t slot = (size_t)slots * kt + kXTail;   // keys + the shard's flag word
-  for (Shard& s : h->shards) {   // px_keys[p] is written on the block's compute stream (a screened block: its parity's)
+  for (Shard& s : h->shards) {   // px_keys[x] is written on the block's compute stream (a screened block: its parity's)
     HIP_TRY(hipSetDevice(s.dev));
-    HIP_TRY(hipEventRecord(s.ev_keys[p], scr ? cstream(h, s, p) : s.stream));
+    HIP_TRY(hipEventRecord(s.ev_keys[x], scr ? cstream(h, s, p) : s.stream));
   }
+  const int lane = x & 1;
   for (Shard& dst : h->shards) {
     HIP_TRY(hipSetDevice(dst.dev));
+    const hipStream_t xs = lane ? dst.xstream2 : dst.xstream;
     if (h->dist) {
-      HIP_TRY(hipStreamWaitEvent(dst.xstream, dst.ev_keys[p], 0));
-      NCCL_TRY(ncclAllGather(dst.px_keys[p], dst.px_gathered[p], slot, ncclUint64, dst.comm, dst.xstream));
+      HIP_TRY(hipStreamWaitEvent(xs, dst.ev_keys[x], 0));
+      NCCL_TRY(ncclAllGather(dst.px_keys[x], dst.px_gathered[x], slot, ncclUint64, lane ? dst.comm2 : dst.comm, xs));
     } else {
       for (size_t i = 0; i < h->shards.size(); ++i) {
         const Shard& src = h->shards[i];
-        HIP_TRY(hipStreamWaitEvent(dst.xstream, src.ev_keys[p], 0));
-        HIP_TRY(hipMemcpyPeerAsync(dst.px_gathered[p] + i * slot, dst.dev, src.px_keys[p], src.dev, slot * 8,
-                                   dst.xstream));
+        HIP_TRY(hipStreamWaitEvent(xs, src.ev_keys[x], 0));
+        HIP_TRY(hipMemcpyPeerAsync(dst.px_gathered[x] + i * slot, dst.dev, src.px_keys[x], src.dev, slot * 8, xs));
       }
     }
-    HIP_TRY(rr::launch_merge(kt, dst.px_gathered[p], h->world, kt, bb, k, nullptr, dst.out_scores + (size_t)q0 * k,
-                             dst.out_idx + (size_t)q0 * k, dst.xstream, slots, (int64_t)slot,
-                             (uint64_t*)dst.out_base));
-    HIP_TRY(hipEventRecord(dst.ev_xdone[p], dst.xstream));
+    if (h->x_delay_us > 0) HIP_TRY(rr::launch_delay(h->x_delay_us, xs));   // (A/B: a slower exchange)
+    if (dst.last_x >= 0 && (dst.last_x & 1) != lane) HIP_TRY(hipStreamWaitEvent(xs, dst.ev_xdone[dst.last_x], 0));
+    HIP_TRY(rr::launch_merge(kt, dst.px_gathered[x], h->world, kt, bb, k, nullptr, dst.out_scores + (size_t)q0 * k,
+                             dst.out_idx + (size_t)q0 * k, xs, slots, (int64_t)slot, (uint64_t*)dst.out_base));
+    HIP_TRY(hipEventRecord(dst.ev_xdone[x], xs));
+    dst.last_x = x;
   }
   return RR_OK;
 }
@@ -808,6 +839,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
   const bool multi = h->world > 1 || h->dist;   // an exchange step (RCCL with any world, peer copies)
   const bool local_multi = multi && !h->dist;
   const int p = h->parity;
+  const int x = h->xslot;   // pipelined-exchange buffer set of this block
   if (scr || wk) {
     ++h->screen_seq;
     ++h->screen_blocks;
@@ -825,12 +857,14 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
             if (hipError_t e = hipStreamWaitEvent(s.stream, o.copies_done, 0)) return e;
       return hipSuccess;
     };
-    // pipelined exchange: px_keys[p] is rewritten only after every exchange that read it has finished
-    // (its own all-gather; within one process also the other shards' peer copies of it)
-    auto wait_px = [&](int par, hipStream_t ws) -> hipError_t {
-      for (const Shard& o : h->shards)
-        if (&o == &s || local_multi)
-          if (hipError_t e = hipStreamWaitEvent(ws, o.ev_xdone[par], 0)) return e;
+    // pipelined exchange: px_keys[x] is rewritten only after every exchange that read it has finished
+    // (its own all-gather; within one process also the other shards' peer copies of it); -1: every slot
+    auto wait_px = [&](int slot, hipStream_t ws) -> hipError_t {
+      for (int xs = 0; xs < kXSlots; ++xs)
+        if (slot < 0 || xs == slot)
+          for (const Shard& o : h->shards)
+            if (&o == &s || local_multi)
+              if (hipError_t e = hipStreamWaitEvent(ws, o.ev_xdone[xs], 0)) return e;
       return hipSuccess;
     };
     const float* qb = s.qbuf[h->qpar] + (size_t)q0 * d;
@@ -847,7 +881,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       // block's flag word when the bound cannot prove completeness: settle_screen re-runs then). The verify
       // follows in-stream: a cross-stream hand-off costs ~20-25 us of dispatch latency on MI355X
       // (profiles/r02/steps/), more than the ~17 us verify that running it on the exchange stream overlapped.
-      // With an exchange, px_keys[p] is rewritten only after its previous exchange (two blocks back) is done.
+      // With an exchange, px_keys[x] is rewritten only after its previous exchange (kXSlots blocks back) is done.
       // (two compute streams: parity 1 on cstream2, after the work of the other stream it must follow)
       const bool two = two_streams(h, s);
       const int bsi = block_si(h, s, p), t = h->qpar;
@@ -861,7 +895,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
           s.c2_busy = true;
         }
       }
-      if (multi) HIP_TRY(wait_px(p, cs));
+      if (multi) HIP_TRY(wait_px(x, cs));
       uint64_t* candp = s.cand + (size_t)p * cand_half(s);
       const bool alone = !two || s.last_vsi < 0 || s.last_vsi == bsi ||
                          hipEventQuery(s.ev_q[s.last_vq][s.last_vsi]) == hipSuccess;
@@ -892,15 +926,15 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         v.k_out = k;
         v.out_scores = multi ? nullptr : osc;
         v.out_idx = multi ? nullptr : oix;
-        v.out_keys = multi ? s.px_keys[p] : nullptr;
+        v.out_keys = multi ? s.px_keys[x] : nullptr;
         // the block's flag word: the result buffer's head, or (exchange) the word after this shard's keys
-        v.flag = multi ? s.px_keys[p] + (size_t)slots * kt : (uint64_t*)s.out_base;
+        v.flag = multi ? s.px_keys[x] + (size_t)slots * kt : (uint64_t*)s.out_base;
         v.count = s.scount;
         v.seq = seq;
         v.force_incomplete = h->kernel == RR_KERNEL_SCREEN_FALLBACK;
         HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 1, rr::kQSlots, rr::kQSlots, v, vs));
       } else {   // a shard without rows contributes empty lists
-        HIP_TRY(hipMemsetAsync(s.px_keys[p], 0, (size_t)slots * kt * 8, vs));
+        HIP_TRY(hipMemsetAsync(s.px_keys[x], 0, (size_t)slots * kt * 8, vs));
       }
       if (two) {   // this verify (the last reader of query buffer t on this stream)
         HIP_TRY(hipEventRecord(s.ev_q[t][bsi], vs));
@@ -918,8 +952,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       }
     } else if (kt) {
       int grid = fused_grid(s);
-      HIP_TRY(wait_px(0, s.stream));   // no screened verify still reads cand or writes the results
-      HIP_TRY(wait_px(1, s.stream));
+      HIP_TRY(wait_px(-1, s.stream));   // no screened verify still reads cand or writes the results
       if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
       if (s.rows() > 0) {
         if (use_sk(h)) {
@@ -938,16 +971,15 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       if (!multi) {
         HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, nullptr, osc, oix, s.stream, slots));
       } else {
-        HIP_TRY(wait_px(p, s.stream));
-        HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, s.px_keys[p], nullptr, nullptr, s.stream, slots));
+        HIP_TRY(wait_px(x, s.stream));
+        HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, s.px_keys[x], nullptr, nullptr, s.stream, slots));
       }
     } else if (wk) {
       // 32 < k <= kWideMax: the split-K kernel keeps per workgroup and query the top-k of its lane lists
       // (wide output, with a floor above everything it dropped), then a radix select over those lists — one
       // stage, or kSelParts groups then their union — gives the shard's top-k and checks it against the
       // floors: unproven -> the block's flag word (the host re-runs the search with the full sort).
-      HIP_TRY(wait_px(0, s.stream));
-      HIP_TRY(wait_px(1, s.stream));
+      HIP_TRY(wait_px(-1, s.stream));
       HIP_TRY(wait_copies());
       if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
       uint64_t* flagw = multi ? s.shard_keys + (size_t)rr::kQSlots * k : (uint64_t*)s.out_base;
@@ -1005,6 +1037,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       if (!multi) {   // results read back on the exchange stream (rr_search_async) come after these
         HIP_TRY(hipEventRecord(s.ev_cdone, s.stream));
         HIP_TRY(hipStreamWaitEvent(s.xstream, s.ev_cdone, 0));
+        HIP_TRY(hipStreamWaitEvent(s.xstream2, s.ev_cdone, 0));
       }
     } else {
       // k > RR_FUSED_KMAX: all keys of this shard, segmented radix sort, keep the first k. The exchange
@@ -1012,8 +1045,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       const int64_t rows = s.rows();
       if (int rc = ensure_full_sort(h, s, k)) return rc;
       if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
-      HIP_TRY(wait_px(0, s.stream));   // no pipelined exchange or screened verify still uses the buffers
-      HIP_TRY(wait_px(1, s.stream));
+      HIP_TRY(wait_px(-1, s.stream));   // no pipelined exchange or screened verify still uses the buffers
       HIP_TRY(wait_copies());
       HIP_TRY(hipMemsetAsync(s.shard_keys, 0, (size_t)rr::kQSlots * k * 8, s.stream));
       if (rows > 0) {
@@ -1045,8 +1077,9 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
     return RR_OK;
   }
   if (kt) {
-    if (int rc = enqueue_exchange_px(h, p, q0, bb, k, kt, slots, scr)) return rc;
+    if (int rc = enqueue_exchange_px(h, p, x, q0, bb, k, kt, slots, scr)) return rc;
     h->parity ^= 1;
+    h->xslot = (x + 1) % h->xslots;
     return RR_OK;
   }
 
@@ -1091,6 +1124,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
     // later pipelined exchanges write the results after this one
     HIP_TRY(hipEventRecord(s.ev_cdone, s.stream));
     HIP_TRY(hipStreamWaitEvent(s.xstream, s.ev_cdone, 0));
+    HIP_TRY(hipStreamWaitEvent(s.xstream2, s.ev_cdone, 0));
+    s.last_x = -1;
   }
   return RR_OK;
 }
@@ -1174,8 +1209,13 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.keys_ready, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.copies_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.xstream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.xstream2, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.cstream2, hipStreamNonBlocking);
-    for (hipEvent_t* ev : {&s.ev_keys[0], &s.ev_keys[1], &s.ev_xdone[0], &s.ev_xdone[1], &s.ev_cdone, &s.ev_scr[0],
+    for (int x = 0; x < kXSlots && e == hipSuccess; ++x) {
+      e = hipEventCreateWithFlags(&s.ev_keys[x], hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev_xdone[x], hipEventDisableTiming);
+    }
+    for (hipEvent_t* ev : {&s.ev_cdone, &s.ev_scr[0],
                            &s.ev_scr[1], &s.ev_fork, &s.ev_join, &s.ev_stage, &s.ev_q[0][0], &s.ev_q[0][1],
                            &s.ev_q[1][0], &s.ev_q[1][1]})
       if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
@@ -1186,6 +1226,8 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   }
   if (const char* e = getenv("RR_COMPUTE_STREAMS")) h->streams = atoi(e) == 1 ? 1 : 2;   // (A/B)
   if (const char* e = getenv("RR_SCREEN_GRID")) h->screen_grid = std::max(1, atoi(e));               // (A/B)
+  if (const char* e = getenv("RR_X_SLOTS")) h->xslots = std::min(kXSlots, std::max(2, atoi(e)));     // (A/B)
+  if (const char* e = getenv("RR_X_EXCHANGE_DELAY_US")) h->x_delay_us = std::min(1000, std::max(0, atoi(e)));
   *out = h;
   return RR_OK;
 }
@@ -1225,6 +1267,7 @@ int rr_init_dist(rr_handle* h, int world, int rank, const char* unique_id) {
   ncclUniqueId id;
   memcpy(id.internal, unique_id, RR_UNIQUE_ID_BYTES);
   NCCL_TRY(ncclCommInitRank(&s.comm, world, id, rank));
+  NCCL_TRY(ncclCommSplit(s.comm, 0, rank, &s.comm2, nullptr));   // the second exchange lane's communicator
   h->world = world;
   h->shard_base = rank;
   h->dist = true;
@@ -1431,6 +1474,7 @@ int sync_streams(rr_handle* h) {
     HIP_TRY(hipSetDevice(s.dev));
     HIP_TRY(hipStreamSynchronize(s.stream));
     HIP_TRY(hipStreamSynchronize(s.xstream));
+    HIP_TRY(hipStreamSynchronize(s.xstream2));
     HIP_TRY(hipStreamSynchronize(s.cstream2));
     s.c2_busy = false;
   }
@@ -1563,7 +1607,8 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
   // without an exchange: after a screened search, on the stream of its last verify (the copy then holds back the
   // next verify on the other stream, which rewrites the rows: ev_q re-recorded below); else on `stream`
   const bool on_v = !xchg && h->last_scr_block && s0.last_vsi >= 0;
-  hipStream_t rs = xchg ? s0.xstream : on_v ? stream_of(s0, s0.last_vsi) : s0.stream;
+  hipStream_t rs = xchg ? (s0.last_x > 0 && (s0.last_x & 1) ? s0.xstream2 : s0.xstream)   // the last merge's lane
+                        : on_v ? stream_of(s0, s0.last_vsi) : s0.stream;
   if (!xchg && !on_v)
     if (int rc = join_main(s0)) return rc;
   HIP_TRY(hipMemcpyAsync(a.pin + res_off, s0.out_base, kOutHead, hipMemcpyDeviceToHost, rs));

@@ -1101,6 +1101,18 @@ hipError_t launch_absmax(const float* x, int64_t n, float* out, hipStream_t s) {
   return hipGetLastError();
 }
 
+// A/B stand-in for a slower exchange (the 8-GPU all-gather's latency, on one GPU): one workgroup that occupies a CU
+// for `ticks` of the 100 MHz wall clock (bounded: it ends after ticks whatever happens), as an RCCL kernel does.
+__global__ void delay_kernel(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+hipError_t launch_delay(int us, hipStream_t s) {
+  hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, s, (uint64_t)us * 100);
+  return hipGetLastError();
+}
+
 hipError_t launch_synth(int kind, uint64_t seed, int64_t row_begin, int64_t n_rows, int d, float* out,
                         hipStream_t s) {
   const int64_t count = n_rows * (int64_t)d;

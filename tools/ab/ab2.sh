@@ -7,7 +7,7 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/$1
 read DOCS B K DT <<< "$2"
 shift 2
-W="--docs $DOCS --dtype $DT --batch $B --k $K --no-cpu-baseline --variants= --ingest-rows 0 --no-pmc --steps ${STEPS:-20} --warmup ${WARMUP:-5} --latency-steps ${LAT:-5} --steady-steps ${STEADY:-200}"
+W="${EXTRA:-} --docs $DOCS --dtype $DT --batch $B --k $K --no-cpu-baseline --variants= --ingest-rows 0 --no-pmc --steps ${STEPS:-20} --warmup ${WARMUP:-5} --latency-steps ${LAT:-5} --steady-steps ${STEADY:-200}"
 echo "# $DOCS rows, batch $B, k $K, $DT: window value ms kernel_us | steady value ms kernel_us" >> "$OUT"
 for rep in $(seq ${REPS:-2}); do
   for arm in "$@"; do
