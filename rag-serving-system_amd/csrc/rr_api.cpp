@@ -1709,11 +1709,12 @@ int rr_screen_copy(rr_handle* h, int32_t use, int32_t* present) {
   if (!h) return fail(RR_E_INVALID, "null handle");
   if (use >= 0) {
     h->screen_copy = use ? 1 : 0;
+    if (!use)   // every stream of the handle may still be screening from the copy
+      if (int rc = sync_streams(h)) return rc;
     if (!use)
       for (Shard& s : h->shards)
         if (s.scr16) {
           HIP_TRY(hipSetDevice(s.dev));
-          HIP_TRY(hipStreamSynchronize(s.stream));
           HIP_TRY(hipFree(s.scr16));
           s.scr16 = nullptr;
         }
