@@ -16,7 +16,8 @@
 //     MFMA-shaped ds_read_b128 of 32 rows is conflict-free.
 //   * Two slab slots per wave: slab s + 1 is in flight while slab s is read and multiplied (counted
 //     vmcnt; LDS-DMA has no VGPR destination, so nothing hipcc allocates can be hit by a landing load).
-//   * Per tile the 8 K-partials are summed through LDS (double-buffered, one raw s_barrier per tile)
+//   * Per tile the 8 K-partials are summed through LDS (XOR-swizzled rows, conflict-free; double-buffered, one raw
+//     s_barrier per tile)
 //     in a fixed order; wave w then runs the metric epilogue for queries 4w..4w+3 (2 rows x 1 query
 //     per lane) and a per-lane top-KT insert. At the end each query's 16 lane lists are merged with
 //     shuffles.
@@ -77,7 +78,8 @@ __device__ unsigned long long probe[4096 * 8];
 
 constexpr int kSlabRowBytes = 128;                // contiguous bytes of one row per slab
 constexpr int kSlabBytes = 32 * kSlabRowBytes;    // 4 KiB
-constexpr int kRedStride = 36;                    // floats per (wave, query) block of 32 rows (+4 pad)
+constexpr int kRedStride = 36;                    // floats allocated per (wave, query) block of 32 rows
+constexpr int kRedRow = 32;                       // ... of which the XOR-swizzled partial sums use 32
 
 // Ring of RS slab slots per wave: RS - 1 slabs stay in flight while one is multiplied. With RS = 2 the
 // K-partial block is double-buffered (one barrier per tile); with RS = 3 (2 x 32 KiB more ring) it is
@@ -863,7 +865,11 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #pragma unroll
       for (int a4 = 0; a4 < 4; ++a4) {   // C/D map: acc[4a + i] = (doc 8a + 4h + i, query r)
         const f32x4 v = {accs[qh][4 * a4], accs[qh][4 * a4 + 1], accs[qh][4 * a4 + 2], accs[qh][4 * a4 + 3]};
-        *(f32x4*)(rb + (w * QS + 32 * qh + r) * kRedStride + 8 * a4 + 4 * h) = v;
+        // 32 floats per (wave, query) row, its eight 16-byte chunks XOR-swizzled by the query index: the 8-lane
+        // groups of this ds_write_b128 and the epilogue's ds_read_b64 / ds_read_b128 groups are conflict-free
+        // (the +4-float padding it replaced left the reads 2-way conflicted: 1.6e8 of 5.0e8 LDS cycles at B = 64)
+        const int rq = 32 * qh + r;
+        *(f32x4*)(rb + (w * QS + rq) * kRedRow + 4 * ((2 * a4 + h) ^ (rq & 7))) = v;
       }
     lds_barrier();   // (also publishes wave 0's LDS-DMA factors and its next-chunk word)
     float sv[DPL];
@@ -871,7 +877,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     for (int e = 0; e < DPL; ++e) sv[e] = 0.f;
 #pragma unroll
     for (int ww = 0; ww < kWaves; ++ww) {   // fixed wave order: the same sums for any QH
-      const float* src = rb + (ww * QS + qe) * kRedStride + er;
+      const float* src = rb + (ww * QS + qe) * kRedRow + 4 * ((er >> 2) ^ (qe & 7)) + (er & 3);
       if constexpr (DPL == 2) {
         const float2 p = *(const float2*)src;
         sv[0] += p.x;
