@@ -874,18 +874,16 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     lds_barrier();   // (also publishes wave 0's LDS-DMA factors and its next-chunk word)
     float sv[DPL];
 #pragma unroll
-    for (int e = 0; e < DPL; ++e) sv[e] = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < kWaves; ++ww) {   // fixed wave order: the same sums for any QH
+    for (int ww = 0; ww < kWaves; ++ww) {   // fixed wave order: the same sums for any QH (wave 0's partial first)
       const float* src = rb + (ww * QS + qe) * kRedRow + 4 * ((er >> 2) ^ (qe & 7)) + (er & 3);
       if constexpr (DPL == 2) {
         const float2 p = *(const float2*)src;
-        sv[0] += p.x;
-        sv[1] += p.y;
+        sv[0] = ww ? sv[0] + p.x : p.x;
+        sv[1] = ww ? sv[1] + p.y : p.y;
       } else {
         const f32x4 p = *(const f32x4*)src;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) sv[e] += p[e];
+        for (int e = 0; e < 4; ++e) sv[e] = ww ? sv[e] + p[e] : p[e];
       }
     }
     // Cosine prefilter: a score whose estimate dot * rcp(den) (within a few ulp of the quotient) is below
@@ -920,7 +918,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         if constexpr (COS) nd = gnorm[er + e];
       } else {
         row = base + er + e;
-        valid = qev && row < n;
+        valid = qev && (base + 32 <= n || row < n);   // (whole tiles: a scalar test)
         const float* tf = trow + ts * 64 + er + e;   // factor 0 at tf[0], factor 1 at tf[32]
         if constexpr (DT == 2) s = s * (COS ? tf[32] : tf[0]) * qs;   // exact 2^e rescales
         if constexpr (COS || SCR) nd = tf[0];
