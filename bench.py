@@ -33,6 +33,7 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "rag-serving-system_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "retrieval queries/sec + p99 latency, batch=32, 1M docs d=1024, 1/2/4/8 GPU"
 SCORE_KERNEL_DOC = ("the corpus-streaming kernel: sk_score_kernel MODE 0 (split-K, LDS-DMA; for fp32 storage the "
                     "screened search's screen — DT 7 over the f16 screening copy of the rows when the handle keeps "
                     "one, else DT 6 over the fp32 rows — whose exact fp32 verify of the candidates runs overlapped "
@@ -115,15 +116,24 @@ def algorithmic_bytes(rows: int, d: int, batch: int, dtype: str, metric: str, sc
     return rows * (d * elem + per_row) + batch * d * 4
 
 
-def timed_steps(ix, k, steps, warmup, dist, cuda_sync, every=1):
+def timed_steps(ix, k, steps, warmup, dist, cuda_sync, every=1, acct=None):
     """W untimed warmup steps, then exactly K steps between barrier + device sync on both sides.
     HIP events bracket the similarity kernel of every `every`-th step (event markers cost GPU time
     between kernels; sampling keeps the duration measurement inside the timed region).
+
+    Screened searches (fp32 storage) whose bound could not prove the top-k are flagged on the device and owe an
+    exact re-run; a staged search nobody fetches is superseded by the next one and never re-run by the library. So
+    INSIDE the timed region, after the K steps, the flagged blocks of the window are counted (rr_screen_counts) and
+    every one the library did not already re-run is paid for with one exact search (RR_KERNEL_EXACT) before the
+    closing sync. Multi-process: the ranks' counts are summed (a block flagged on any rank is re-run by all; the
+    sum may over-pay, never under-pay) and every rank runs that many exact searches (their all-gathers pair up).
+    `acct` (dict, optional) receives {"flagged": F, "reruns_library": R, "reruns_paid": P, "blocks": B}.
     Returns (wall seconds, fused-kernel event ms summed, fused launches timed)."""
-    from rag_service_amd.dist import barrier
+    from rag_service_amd.dist import barrier, sum_over_ranks
     for _ in range(warmup):
         ix.search_staged(k)
     ix.synchronize()
+    b0, f0, r0 = ix.screen_counts()
     ix.set_timing(True)
     ix.kernel_time(reset=True)
     barrier(dist)
@@ -134,12 +144,22 @@ def timed_steps(ix, k, steps, warmup, dist, cuda_sync, every=1):
         if every > 1:
             ix.set_timing(i % every == 0)
         ix.search_staged(k)
+    b1, f1, r1 = ix.screen_counts()            # synchronises (and settles the last search)
+    owed = int(sum_over_ranks(dist, float(max(0, (f1 - f0) - (r1 - r0)))))
+    if owed:
+        ix.set_timing(False)
+        ix.set_kernel("exact")
+        for _ in range(owed):
+            ix.search_staged(k)
+        ix.set_kernel("auto")
     ix.synchronize()
     cuda_sync()
     barrier(dist)
     elapsed = time.perf_counter() - t0
     kern_ms, launches = ix.kernel_time(reset=True)
     ix.set_timing(False)
+    if acct is not None:
+        acct.update({"blocks": b1 - b0, "flagged": f1 - f0, "reruns_library": r1 - r0, "reruns_paid": owed})
     return elapsed, kern_ms, launches
 
 
@@ -194,9 +214,31 @@ def main() -> None:
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / control-plane check without a GPU: every rank joins the gloo group, "
                          "reaches the timed-loop barrier and rank 0 prints one JSON line")
+    ap.add_argument("--dist-timeout-s", type=float, default=300.0,
+                    help="N>1: deadline of every cross-rank wait — the gloo control plane's collectives and (a "
+                         "third of it, at most 120 s) the library's waits on RCCL work; a miss ends the rank with a "
+                         "JSON error line naming the rank and stage, and a non-zero exit status")
+    ap.add_argument("--dry-run-stall-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
+    from rag_service_amd.dist import env_rank_world
+    rank, world, _ = env_rank_world()
+    stage = {"stage": "start"}
+    try:
+        run(args, stage)
+    except Exception as e:   # a missed deadline (RCCL or gloo) or any failure: say which rank and where, exit != 0
+        from rag_service_amd._lib import HipRetrievalError
+        code = e.code if isinstance(e, HipRetrievalError) else None
+        print(json.dumps({"metric": METRIC, "value": None, "error": f"{type(e).__name__}: {e}"[:600],
+                          "error_code": code, "rank": rank, "n_gpus": world, "stage": stage["stage"]}), flush=True)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        # no interpreter teardown: destructors would wait on device work that may never finish (a peer is gone)
+        os._exit(3)
+
+
+def run(args, stage: dict) -> None:
     every = args.timing_every or (1 if args.steps < 100 else 10)
 
     from rag_service_amd import Index, get_unique_id
@@ -205,8 +247,12 @@ def main() -> None:
                                       max_over_ranks)
 
     rank, world, local = env_rank_world()
-    dist = init_control_plane(world, rank)
+    stage["stage"] = "control-plane init"
+    dist = init_control_plane(world, rank, timeout_s=max(1, int(args.dist_timeout_s)))
     if args.dry_run:
+        if rank == args.dry_run_stall_rank:   # (test hook: a rank that never reaches the barrier in time)
+            time.sleep(args.dist_timeout_s + 3)
+        stage["stage"] = "dry-run barrier"
         barrier(dist)
         ranks_seen = max_over_ranks(dist, float(rank)) + 1
         if rank == 0:
@@ -224,6 +270,7 @@ def main() -> None:
         def cuda_sync():
             return None
 
+    stage["stage"] = "handle + RCCL communicator"
     ix = Index(devices=[local], dtype=args.dtype, metric=args.metric)
     rccl_ranks = 0
     if world > 1:
@@ -233,6 +280,9 @@ def main() -> None:
     elif args.exchange_1rank:
         ix.init_dist(1, 0, get_unique_id())
         rccl_ranks = ix.dist_info()[0]
+    if world > 1:   # the library's waits on RCCL work: a third of the control-plane deadline, at most 120 s
+        ix.set_timeout(int(min(120.0, args.dist_timeout_s / 3) * 1000))
+    stage["stage"] = "corpus fill"
     ix.fill_synthetic(_lib.RR_SYNTH_UNIT_NORM, 1234, args.docs, args.dim)
     sb, se = ix.shard_range(0)
     rng = np.random.default_rng(5678)
@@ -240,9 +290,12 @@ def main() -> None:
     q /= np.linalg.norm(q, axis=1, keepdims=True)
 
     # ---- throughput: queries resident in HBM, K back-to-back steps --------------------------------
+    stage["stage"] = "timed steps"
     ix.set_queries(q)
-    elapsed, kern_ms, launches = timed_steps(ix, args.k, args.steps, args.warmup, dist, cuda_sync, every)
+    acct = {}
+    elapsed, kern_ms, launches = timed_steps(ix, args.k, args.steps, args.warmup, dist, cuda_sync, every, acct)
     elapsed = max_over_ranks(dist, elapsed)
+    stage["stage"] = "latency loops"
 
     # ---- latency: host queries in -> host results out, one batch at a time ------------------------
     lat = []
@@ -271,15 +324,19 @@ def main() -> None:
     host_pipe_s = max_over_ranks(dist, time.perf_counter() - t)
 
     # ---- steady state: the same staged loop again, long after the GPU left idle ---------------------
-    st_el, st_ms, st_n = timed_steps(ix, args.k, args.steady_steps, 0, dist, cuda_sync, 10)
+    stage["stage"] = "steady-state steps"
+    st_acct = {}
+    st_el, st_ms, st_n = timed_steps(ix, args.k, args.steady_steps, 0, dist, cuda_sync, 10, st_acct)
     st_el = max_over_ranks(dist, st_el)
     scr_blocks, scr_fallbacks = ix.screen_stats()
+    stage["stage"] = "single-stream and exact-kernel loops"
 
     # ---- roofline of the fused kernel (rank 0's shard) ---------------------------------------------
     n_local = se - sb
     # the fp32 screened search (k <= 29) streams the f16 screening copy when the handle keeps one
     screen16 = args.dtype == "fp32" and args.k <= 29 and ix.screen_copy()
     alg_bytes = algorithmic_bytes(n_local, args.dim, args.batch, args.dtype, args.metric, screen16)
+    fp32_floor = n_local * args.dim * 4 + args.batch * args.dim * 4
     avg_kernel_s = (kern_ms / max(launches, 1)) / 1e3
     step_s = elapsed / args.steps
     # screened blocks on two compute streams (the fp32 default): block i + 1's screen starts while block i's screen
@@ -326,6 +383,24 @@ def main() -> None:
         del host
 
     variants = {}
+    if world == 1 and args.dtype == "fp32" and args.variant_steps > 0:
+        # the one-pass exact fp32 kernel (RR_KERNEL_EXACT, DT 3) on the same handle: it streams the fp32 rows the
+        # reference streams (retriever.py:600), and it is what a flagged block's re-run and any corpus the screen
+        # cannot prune cost
+        ix.set_kernel("exact")
+        e_el, e_ms, e_n = timed_steps(ix, args.k, args.variant_steps, args.warmup, dist, cuda_sync, 10)
+        _, e_idx = ix.search(q, args.k)
+        ix.set_kernel("auto")
+        e_kern = e_ms / max(e_n, 1) / 1e3
+        e_ach = algorithmic_bytes(n_local, args.dim, args.batch, "fp32", args.metric) / e_kern / 1e9
+        variants["exact_fp32"] = {
+            "value": round(args.batch * args.variant_steps / e_el, 2), "unit": "queries/s",
+            "ms_per_step": round(e_el / args.variant_steps * 1e3, 4), "kernel_avg_us": round(e_kern * 1e6, 2),
+            "achieved_GBps": round(e_ach, 1), "frac": round(e_ach / HBM_PEAK_GBS, 4), "steps": args.variant_steps,
+            "alg_bytes_per_launch": algorithmic_bytes(n_local, args.dim, args.batch, "fp32", args.metric),
+            "index_agreement_with_headline": round(float(np.mean(e_idx == head_idx)), 4),
+            "note": "RR_KERNEL_EXACT: sk_score_kernel DT 3 (fp32 rows, each value split exactly into 3 bf16, 6 bf16 "
+                    "MFMAs) over the fp32 rows, one pass, no screen; HIP events on every 10th launch"}
     if world == 1 and args.variants:
         for vd in [v for v in args.variants.split(",") if v and v != args.dtype]:
             vx = Index(devices=[local], dtype=vd, metric=args.metric)
@@ -352,7 +427,7 @@ def main() -> None:
             cpu = cpu_baseline(args.docs, args.dim, args.batch, args.k, args.cpu_budget)
         value = args.batch * args.steps / elapsed
         out = {
-            "metric": "retrieval queries/sec + p99 latency, batch=32, 1M docs d=1024, 1/2/4/8 GPU",
+            "metric": METRIC,
             "value": round(value, 2),
             "unit": "queries/s",
             "n_gpus": world,
@@ -408,7 +483,26 @@ def main() -> None:
                                            "peak over the timed steps (with two compute streams the launches overlap "
                                            "and a launch's own span overstates its time)",
                          "alg_bytes_per_launch": alg_bytes,
+                         # §8(d)'s basis: the fp32 rows the reference streams (N·D·4 + the queries), per step
+                         "fp32_floor_bytes": fp32_floor,
+                         "frac_vs_fp32_floor": round(fp32_floor / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                         "frac_vs_fp32_floor_steady": round(fp32_floor / (st_el / args.steady_steps) / 1e9
+                                                            / HBM_PEAK_GBS, 4),
+                         "basis_note": ("frac = the bytes the launch streams (the f16 screening copy + norms) / step "
+                                        "time; frac_vs_fp32_floor = the fp32 corpus bytes SURVEY §8(d) prices (4 B per "
+                                        "element) / step time — above 1 because the screen proves most fp32 rows "
+                                        "need not be read; valid only with every flagged block's exact re-run paid "
+                                        "(screen_fallbacks_timed, reruns_paid)" if screen16 else
+                                        "frac and frac_vs_fp32_floor on the same rows"),
                          "screen_copy": bool(screen16),
+                         "screen_fallbacks_timed": acct.get("flagged"),
+                         "reruns_paid": acct.get("reruns_paid"),
+                         "reruns_by_library_timed": acct.get("reruns_library"),
+                         "screen_fallbacks_steady": st_acct.get("flagged"),
+                         "reruns_paid_steady": st_acct.get("reruns_paid"),
+                         "fallback_note": "blocks whose bound could not prove the top-k inside the timed window; each "
+                                          "not already re-run by the library is paid with one exact search inside "
+                                          "the window (bench.py timed_steps)",
                          "screened_blocks": scr_blocks, "screen_fallbacks": scr_fallbacks},
             "cpu_baseline": cpu,
             "other_dtypes": variants or None,

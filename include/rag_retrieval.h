@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 4
+#define RR_ABI_VERSION 5
 
 /* error codes */
 #define RR_OK             0
@@ -50,6 +50,10 @@ extern "C" {
 #define RR_E_STATE       -4   /* call out of order (search before load, ...) */
 #define RR_E_UNSUPPORTED -5   /* valid request outside what this build implements */
 #define RR_E_OOM         -6   /* device allocation failed */
+#define RR_E_TIMEOUT     -7   /* multi-process mode: device work (an RCCL all-gather waiting for its peers) did not
+                                 complete within the handle's deadline (rr_set_timeout). The handle is then FAILED:
+                                 every later call returns RR_E_STATE; rr_destroy aborts its communicators and
+                                 releases nothing else (the process is expected to exit) */
 
 /* corpus storage dtype in HBM (4 bytes per element for both fp32 forms, 2 for bf16) */
 #define RR_DTYPE_F32       0  /* fp32 rows stored exactly. Split-K kernel (d % 256 == 0): every corpus and
@@ -214,6 +218,20 @@ int rr_screen_copy(rr_handle* h, int32_t use, int32_t* present);
 /* Screened-search counters since the corpus was (re)loaded: search blocks screened (summed over local
  * shards) and how many of them needed the exact fallback pass. Synchronises the handle's streams. */
 int rr_screen_stats(rr_handle* h, int64_t* blocks, int64_t* fallbacks);
+
+/* The same counters plus the exact re-runs the handle actually ran (a staged search whose results are never
+ * fetched is superseded by the next one and is not re-run; benchmarks pay flagged - re-runs exact searches
+ * themselves). Synchronises the handle's streams, which settles the last search. Any pointer may be null. */
+int rr_screen_counts(rr_handle* h, int64_t* blocks, int64_t* flagged, int64_t* reruns);
+
+/* ---- multi-process deadline -------------------------------------------------------------------------- */
+
+/* Deadline (milliseconds, 0 = none) of every host wait on this handle's device work in multi-process mode
+ * (rr_init_dist): synchronisation, result fetches, rr_wait, query staging and the load-time agreement between
+ * ranks. Device work that does not complete in time — an all-gather whose peers never arrive — makes the call
+ * return RR_E_TIMEOUT naming the rank and the search block, and fails the handle. Default 120000; the
+ * environment variable RR_DIST_TIMEOUT_MS overrides it at rr_create. Ignored without rr_init_dist. */
+int rr_set_timeout(rr_handle* h, int32_t ms);
 
 /* ---- timing (benchmarks) ----------------------------------------------------------------------- */
 

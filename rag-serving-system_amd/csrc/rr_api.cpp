@@ -11,6 +11,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cmath>
 #include <cstdarg>
@@ -199,9 +200,62 @@ struct rr_handle {
   bool screen_wide = false;     // narrow lists re-ran too often on this corpus: use the wide ones
   bool last_narrow = false;     // the last search ran narrow lists
   bool last_scr_block = false;  // the last block enqueued was a screened one
+  // multi-process deadline (rr_set_timeout): host waits on device work poll against it; a miss fails the handle
+  int timeout_ms = 120000;
+  bool failed = false;
 };
 
 namespace {
+
+// ---- host waits on device work ---------------------------------------------------------------------------------
+// Without a communicator: the runtime's blocking waits. One process per GPU (rr_init_dist): a polled wait against
+// the handle's deadline, because an all-gather whose peers never arrive would block the caller forever — a miss
+// returns RR_E_TIMEOUT naming this rank and the newest search block, and fails the handle (rr_destroy then aborts
+// the communicators instead of waiting for streams that may never drain).
+template <class Q>
+int poll_until(rr_handle* h, Q&& done, const char* what, int scale = 1) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const int64_t limit_ms = (int64_t)h->timeout_ms * scale;
+  for (int i = 0;; ++i) {
+    const hipError_t e = done();
+    if (e == hipSuccess) return RR_OK;
+    if (e != hipErrorNotReady) return fail(RR_E_HIP, "%s failed: %s", what, hipGetErrorString(e));
+    if ((i & 63) == 63) {   // a short spin first (the common case completes within microseconds), then the clock
+      const int64_t ms =
+          std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+      if (ms >= limit_ms) {
+        (void)hipGetLastError();
+        h->failed = true;
+        return fail(RR_E_TIMEOUT,
+                    "rank %d of %d: %s did not complete within %lld ms (newest search block %d); an all-gather is "
+                    "probably waiting for a peer rank that never joined",
+                    h->shard_base, h->world, what, (long long)limit_ms, h->screen_seq);
+      }
+      if (ms >= 2) std::this_thread::sleep_for(std::chrono::microseconds(20));
+      else std::this_thread::yield();
+    }
+  }
+}
+int failed_handle() {
+  return fail(RR_E_STATE, "the handle failed earlier (device work missed its deadline, RR_E_TIMEOUT): destroy it");
+}
+bool deadline_on(const rr_handle* h) { return h->dist && h->timeout_ms > 0; }
+int wait_stream(rr_handle* h, hipStream_t st, const char* what = "device stream", int scale = 1) {
+  if (!deadline_on(h)) {
+    HIP_TRY(hipStreamSynchronize(st));
+    return RR_OK;
+  }
+  return poll_until(h, [&] { return hipStreamQuery(st); }, what, scale);
+}
+int wait_event(rr_handle* h, hipEvent_t ev, const char* what = "device event") {
+  if (!deadline_on(h)) {
+    HIP_TRY(hipEventSynchronize(ev));
+    return RR_OK;
+  }
+  return poll_until(h, [&] { return hipEventQuery(ev); }, what);
+}
+
+int sync_streams(rr_handle* h);   // every local shard's streams idle (defined with the C-ABI's waits)
 
 size_t elem_bytes(int dtype) { return dtype == RR_DTYPE_BF16 ? 2 : 4; }
 
@@ -334,13 +388,35 @@ int finish_corpus(rr_handle* h, Shard& s, bool* screen_ok) {
   return RR_OK;
 }
 
-// Finish every local shard; the screened search is allowed only when every shard's range allows it.
+// Finish every local shard; the screened search is allowed only when every shard's range allows it — in a
+// multi-process world every rank's shard: the ranks must take the same path, since the screen's list width sizes
+// the all-gather and the re-run decisions issue collectives (an RCCL min over the ranks' verdicts).
 int finish_all(rr_handle* h) {
   bool ok = true;
   for (Shard& s : h->shards) {
     bool sok = false;
     if (int rc = finish_corpus(h, s, &sok)) return rc;
     ok = ok && sok;
+  }
+  if (h->dist) {
+    Shard& s = h->shards[0];
+    HIP_TRY(hipSetDevice(s.dev));
+    int* dv = nullptr;
+    HIP_TRY(hipMalloc((void**)&dv, sizeof(int)));
+    int all = 0;
+    int rc = RR_OK;
+    hipError_t e = hipMemsetD32Async((hipDeviceptr_t)dv, ok ? 1 : 0, 1, s.stream);
+    if (e == hipSuccess) {
+      const ncclResult_t r = ncclAllReduce(dv, dv, 1, ncclInt32, ncclMin, s.comm, s.stream);
+      if (r != ncclSuccess) rc = fail(RR_E_RCCL, "screen-range agreement failed: %s", ncclGetErrorString(r));
+    }
+    // ranks finish loading at different times: a generous multiple of the deadline
+    if (e == hipSuccess && rc == RR_OK) rc = wait_stream(h, s.stream, "the ranks' screen-range agreement", 10);
+    if (e == hipSuccess && rc == RR_OK) e = hipMemcpy(&all, dv, sizeof(int), hipMemcpyDeviceToHost);
+    if (!h->failed) hipFree(dv);
+    if (rc) return rc;
+    if (e != hipSuccess) return fail(RR_E_HIP, "screen-range agreement failed: %s", hipGetErrorString(e));
+    ok = all != 0;
   }
   h->screen_ok = ok;
   return RR_OK;
@@ -437,10 +513,8 @@ int check_shape(const rr_handle* h, int64_t n, int32_t d) {
 int drop_work_buffers(rr_handle* h) {
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
-    HIP_TRY(hipStreamSynchronize(s.stream));
-    HIP_TRY(hipStreamSynchronize(s.xstream));
-    HIP_TRY(hipStreamSynchronize(s.xstream2));
-    HIP_TRY(hipStreamSynchronize(s.cstream2));
+    for (hipStream_t st : {s.stream, s.xstream, s.xstream2, s.cstream2})
+      if (int rc = wait_stream(h, st)) return rc;
     s.c2_busy = s.fork_pending = s.stage_pending = false;
     s.last_x = -1;
     s.q_rd[0][0] = s.q_rd[0][1] = s.q_rd[1][0] = s.q_rd[1][1] = false;
@@ -494,6 +568,14 @@ int prepare_ranges(rr_handle* h, int64_t n, int32_t d) {
 
 // Work buffers sized for (b queries, k results).
 int ensure_buffers(rr_handle* h, int b, int k) {
+  // growing the query buffers (zeroed) and the result head (flag word reset) would drop the last checked search's
+  // queries and flag before anyone settled it: settle it first (its exact re-run, if owed, needs both)
+  bool grow = false;
+  for (const Shard& s : h->shards) grow = grow || b > s.q_cap || k > s.k_cap;
+  if (grow && h->last_screened && !h->last_settled)
+    if (int rc = rr_synchronize(h)) return rc;
+  if (grow)   // no search in flight may still write the buffers about to be replaced
+    if (int rc = sync_streams(h)) return rc;
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
     if (b > s.q_cap || k > s.k_cap) {
@@ -505,10 +587,23 @@ int ensure_buffers(rr_handle* h, int b, int k) {
           HIP_TRY(hipMemset(s.qbuf[i], 0, qb));
         }
       }
-      // scores and indices in one allocation, so a search's results come back in ONE D2H copy
+      // scores and indices in one allocation, so a search's results come back in ONE D2H copy. The last search's
+      // results (and flag word) move to the new allocation: rr_fetch_results after staging a larger batch still
+      // returns them.
+      char* old = s.out_base;
+      const size_t old_off = s.out_off;
+      s.out_base = nullptr;
       s.out_off = (kOutHead + (size_t)qc * kc * 4 + 255) & ~(size_t)255;
       if (int rc = dmalloc(&s.out_base, s.out_off + (size_t)qc * kc * 8)) return rc;
-      HIP_TRY(hipMemset(s.out_base, 0, kOutHead));   // the screened-search flag word starts at 0
+      const size_t cnt = (size_t)h->last_b * h->last_k;
+      if (old && cnt) {
+        HIP_TRY(hipMemcpyAsync(s.out_base, old, kOutHead + cnt * 4, hipMemcpyDeviceToDevice, s.stream));
+        HIP_TRY(hipMemcpyAsync(s.out_base + s.out_off, old + old_off, cnt * 8, hipMemcpyDeviceToDevice, s.stream));
+        if (int rc = wait_stream(h, s.stream)) return rc;
+      } else {
+        HIP_TRY(hipMemset(s.out_base, 0, kOutHead));   // the screened-search flag word starts at 0
+      }
+      if (old) HIP_TRY(hipFree(old));
       s.out_scores = (float*)(s.out_base + kOutHead);
       s.out_idx = (int64_t*)(s.out_base + s.out_off);
       // serial exchange lists: [32][k] keys + a flag word (large-k path)
@@ -555,8 +650,8 @@ int ensure_full_sort(rr_handle* h, Shard& s, int k) {
                 (long long)s.rows());
   const size_t need = (size_t)rr::kQSlots * std::max<int64_t>(s.rows(), (int64_t)h->world * k);
   if (need > s.full_cap) {
-    HIP_TRY(hipStreamSynchronize(s.stream));   // the old buffers may still be in use
-    HIP_TRY(hipStreamSynchronize(s.cstream2));
+    if (int rc = wait_stream(h, s.stream)) return rc;   // the old buffers may still be in use
+    if (int rc = wait_stream(h, s.cstream2)) return rc;
     s.c2_busy = false;
     if (int rc = dmalloc(&s.full_keys, need * 8)) return rc;
     if (int rc = dmalloc(&s.sorted, need * 8)) return rc;
@@ -904,6 +999,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       if (s.rows() > 0) {
         rr::SkArgs a = sk_base(h, s, qb, bb);
         a.out = candp;
+        a.clear_word = multi ? s.px_keys[x] + (size_t)slots * kt : nullptr;   // the verify below may raise it
         a.ctr = s.ctr + (cs == s.stream ? 0 : kCtrStride);
         a.sqrt_d = sqrtf((float)d) * (1.0f + 0x1p-20f);
         // the f16 copy holds exactly the values the fp32-reading screen rounds to: half the bytes
@@ -933,8 +1029,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         v.seq = seq;
         v.force_incomplete = h->kernel == RR_KERNEL_SCREEN_FALLBACK;
         HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 1, rr::kQSlots, rr::kQSlots, v, vs));
-      } else {   // a shard without rows contributes empty lists
-        HIP_TRY(hipMemsetAsync(s.px_keys[x], 0, (size_t)slots * kt * 8, vs));
+      } else {   // a shard without rows contributes empty lists and no flag
+        HIP_TRY(hipMemsetAsync(s.px_keys[x], 0, ((size_t)slots * kt + 1) * 8, vs));
       }
       if (two) {   // this verify (the last reader of query buffer t on this stream)
         HIP_TRY(hipEventRecord(s.ev_q[t][bsi], vs));
@@ -972,7 +1068,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, nullptr, osc, oix, s.stream, slots));
       } else {
         HIP_TRY(wait_px(x, s.stream));
-        HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, s.px_keys[x], nullptr, nullptr, s.stream, slots));
+        HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, s.px_keys[x], nullptr, nullptr, s.stream, slots, 0,
+                                 nullptr, s.px_keys[x] + (size_t)slots * kt));
       }
     } else if (wk) {
       // 32 < k <= kWideMax: the split-K kernel keeps per workgroup and query the top-k of its lane lists
@@ -1228,12 +1325,25 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   if (const char* e = getenv("RR_SCREEN_GRID")) h->screen_grid = std::max(1, atoi(e));               // (A/B)
   if (const char* e = getenv("RR_X_SLOTS")) h->xslots = std::min(kXSlots, std::max(2, atoi(e)));     // (A/B)
   if (const char* e = getenv("RR_X_EXCHANGE_DELAY_US")) h->x_delay_us = std::min(1000, std::max(0, atoi(e)));
+  if (const char* e = getenv("RR_DIST_TIMEOUT_MS")) h->timeout_ms = std::max(0, atoi(e));
   *out = h;
   return RR_OK;
 }
 
 void rr_destroy(rr_handle* h) {
   if (!h) return;
+  if (h->failed) {
+    // device work missed its deadline: an all-gather may still be waiting for a peer. Abort the communicators
+    // (their kernels observe the abort and exit) and release nothing else — freeing buffers or destroying streams
+    // that queued work may still reference would wait for it, or fault. The process is expected to exit.
+    for (Shard& s : h->shards) {
+      hipSetDevice(s.dev);
+      if (s.comm2) ncclCommAbort(s.comm2);
+      if (s.comm) ncclCommAbort(s.comm);
+    }
+    delete h;
+    return;
+  }
   for (Shard& s : h->shards) free_shard(s);
   if (h->pin_out) hipHostFree(h->pin_out);
   if (h->pin_q) hipHostFree(h->pin_q);
@@ -1288,6 +1398,7 @@ int rr_dist_info(const rr_handle* h, int* rccl_ranks, int* rccl_rank) {
 
 int rr_load(rr_handle* h, const float* host_corpus, int64_t n, int32_t d) {
   if (!h || !host_corpus) return fail(RR_E_INVALID, "null argument");
+  if (h->failed) return failed_handle();
   if (int rc = prepare_ranges(h, n, d)) return rc;
   for (Shard& s : h->shards)
     if (s.rows() > 0)
@@ -1300,6 +1411,7 @@ int rr_load(rr_handle* h, const float* host_corpus, int64_t n, int32_t d) {
 int rr_load_rows(rr_handle* h, const float* host_rows, int64_t row_begin, int64_t n_rows, int64_t n_total,
                  int32_t d) {
   if (!h || !host_rows) return fail(RR_E_INVALID, "null argument");
+  if (h->failed) return failed_handle();
   if (int rc = prepare_ranges(h, n_total, d)) return rc;
   for (Shard& s : h->shards) {
     if (s.row_begin < row_begin || s.row_end > row_begin + n_rows)
@@ -1315,6 +1427,7 @@ int rr_load_rows(rr_handle* h, const float* host_rows, int64_t row_begin, int64_
 
 int rr_fill_synthetic(rr_handle* h, int kind, uint64_t seed, int64_t n_total, int32_t d) {
   if (!h) return fail(RR_E_INVALID, "null handle");
+  if (h->failed) return failed_handle();
   if (kind != RR_SYNTH_EXACT_INT && kind != RR_SYNTH_UNIT_NORM) return fail(RR_E_INVALID, "bad kind %d", kind);
   if (int rc = prepare_ranges(h, n_total, d)) return rc;
   for (Shard& s : h->shards) {
@@ -1361,6 +1474,7 @@ int rr_shard_range(const rr_handle* h, int i, int64_t* begin, int64_t* end) {
 
 int rr_read_rows(const rr_handle* h, int64_t row_begin, int64_t n_rows, float* host_out) {
   if (!h || !host_out) return fail(RR_E_INVALID, "null argument");
+  if (h->failed) return failed_handle();
   if (!h->loaded) return fail(RR_E_STATE, "no corpus loaded");
   const int d = h->d;
   int64_t done = 0;
@@ -1395,6 +1509,7 @@ int rr_read_rows(const rr_handle* h, int64_t row_begin, int64_t n_rows, float* h
 
 int rr_set_queries(rr_handle* h, const float* host_q, int32_t b, int32_t d) {
   if (!h || (!host_q && b > 0)) return fail(RR_E_INVALID, "null argument");
+  if (h->failed) return failed_handle();
   if (!h->loaded) return fail(RR_E_STATE, "no corpus loaded");
   if (d != h->d) return fail(RR_E_INVALID, "query dim %d != corpus dim %d", d, h->d);
   if (b < 1) return fail(RR_E_INVALID, "b=%d", b);
@@ -1404,8 +1519,11 @@ int rr_set_queries(rr_handle* h, const float* host_q, int32_t b, int32_t d) {
   const size_t qbytes = (size_t)b * d * 4;
   for (Shard& s : h->shards) {   // every shard's copy out of pin_q has landed before it is rewritten
     HIP_TRY(hipSetDevice(s.dev));
-    if (s.pin_q_free) HIP_TRY(hipEventSynchronize(s.pin_q_free));
-    else HIP_TRY(hipEventCreateWithFlags(&s.pin_q_free, hipEventDisableTiming));
+    if (s.pin_q_free) {
+      if (int rc = wait_event(h, s.pin_q_free, "the previous batch's query copy")) return rc;
+    } else {
+      HIP_TRY(hipEventCreateWithFlags(&s.pin_q_free, hipEventDisableTiming));
+    }
   }
   if (qbytes > h->pin_q_cap) {
     if (h->pin_q) HIP_TRY(hipHostFree(h->pin_q));
@@ -1425,6 +1543,7 @@ int rr_set_queries(rr_handle* h, const float* host_q, int32_t b, int32_t d) {
 
 int rr_set_queries_device(rr_handle* h, const float* dev_q, int32_t b, int32_t d) {
   if (!h || !dev_q) return fail(RR_E_INVALID, "null argument");
+  if (h->failed) return failed_handle();
   if (!h->loaded) return fail(RR_E_STATE, "no corpus loaded");
   if (d != h->d) return fail(RR_E_INVALID, "query dim %d != corpus dim %d", d, h->d);
   if (b < 1) return fail(RR_E_INVALID, "b=%d", b);
@@ -1440,6 +1559,7 @@ int rr_set_queries_device(rr_handle* h, const float* dev_q, int32_t b, int32_t d
 
 int rr_search_staged(rr_handle* h, int32_t k) {
   if (!h) return fail(RR_E_INVALID, "null handle");
+  if (h->failed) return failed_handle();
   if (!h->loaded || h->cur_b < 1) return fail(RR_E_STATE, "no queries staged");
   if (k < 1) return fail(RR_E_INVALID, "k=%d must be >= 1", k);
   const int b = h->cur_b;
@@ -1472,13 +1592,20 @@ namespace {
 int sync_streams(rr_handle* h) {
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
-    HIP_TRY(hipStreamSynchronize(s.stream));
-    HIP_TRY(hipStreamSynchronize(s.xstream));
-    HIP_TRY(hipStreamSynchronize(s.xstream2));
-    HIP_TRY(hipStreamSynchronize(s.cstream2));
+    for (hipStream_t st : {s.stream, s.xstream, s.xstream2, s.cstream2})
+      if (int rc = wait_stream(h, st)) return rc;
     s.c2_busy = false;
   }
   return collect_timing(h);
+}
+
+// D2H of device bytes on local shard 0's `stream` (never the null stream: it would take a hardware queue of its
+// own, and GPU_MAX_HW_QUEUES = 4 are already spoken for by the compute and exchange streams). The streams are idle.
+int copy_out(rr_handle* h, void* dst, const void* src, size_t bytes) {
+  Shard& s = h->shards[0];
+  HIP_TRY(hipSetDevice(s.dev));
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s.stream));
+  return wait_stream(h, s.stream, "result copy");
 }
 
 // Screened search, last step: `flag` is the last search's flag word (shard 0's result head, which after an
@@ -1511,15 +1638,14 @@ int read_flag(rr_handle* h, uint64_t* flag) {
   Shard& s = h->shards[0];
   *flag = 0;
   if (!s.out_base) return RR_OK;
-  HIP_TRY(hipSetDevice(s.dev));
-  HIP_TRY(hipMemcpy(flag, s.out_base, sizeof(uint64_t), hipMemcpyDeviceToHost));
-  return RR_OK;
+  return copy_out(h, flag, s.out_base, sizeof(uint64_t));
 }
 
 }  // namespace
 
 int rr_synchronize(rr_handle* h) {
   if (!h) return fail(RR_E_INVALID, "null handle");
+  if (h->failed) return failed_handle();
   if (int rc = sync_streams(h)) return rc;
   if (!h->last_screened) return RR_OK;
   uint64_t flag = 0;
@@ -1530,6 +1656,7 @@ int rr_synchronize(rr_handle* h) {
 
 int rr_fetch_results(rr_handle* h, float* out_scores, int64_t* out_idx) {
   if (!h || !out_scores || !out_idx) return fail(RR_E_INVALID, "null argument");
+  if (h->failed) return failed_handle();
   if (h->last_k < 1) return fail(RR_E_STATE, "no search has run");
   if (int rc = sync_streams(h)) return rc;
   Shard& s = h->shards[0];
@@ -1539,8 +1666,8 @@ int rr_fetch_results(rr_handle* h, float* out_scores, int64_t* out_idx) {
     HIP_TRY(hipSetDevice(s.dev));
     uint64_t flag = 0;
     if (s.out_off > (1u << 20)) {   // capacity grown far beyond this search: plain copies
-      HIP_TRY(hipMemcpy(out_scores, s.out_scores, cnt * 4, hipMemcpyDeviceToHost));
-      HIP_TRY(hipMemcpy(out_idx, s.out_idx, cnt * 8, hipMemcpyDeviceToHost));
+      if (int rc = copy_out(h, out_scores, s.out_scores, cnt * 4)) return rc;
+      if (int rc = copy_out(h, out_idx, s.out_idx, cnt * 8)) return rc;
       if (int rc = read_flag(h, &flag)) return rc;
     } else {
       if (span > h->pin_out_cap) {
@@ -1551,7 +1678,7 @@ int rr_fetch_results(rr_handle* h, float* out_scores, int64_t* out_idx) {
         h->pin_out_cap = span;
       }
       // one pinned D2H of [flag word | scores | pad | indices] (the streams are idle)
-      HIP_TRY(hipMemcpy(h->pin_out, s.out_base, span, hipMemcpyDeviceToHost));
+      if (int rc = copy_out(h, h->pin_out, s.out_base, span)) return rc;
       memcpy(&flag, h->pin_out, sizeof flag);
       memcpy(out_scores, h->pin_out + kOutHead, cnt * 4);
       memcpy(out_idx, h->pin_out + s.out_off, cnt * 8);
@@ -1572,6 +1699,7 @@ int rr_search(rr_handle* h, const float* host_q, int32_t b, int32_t d, int32_t k
 
 int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int32_t k, int32_t* ticket) {
   if (!h || !host_q || !ticket) return fail(RR_E_INVALID, "null argument");
+  if (h->failed) return failed_handle();
   if (!h->loaded) return fail(RR_E_STATE, "no corpus loaded");
   if (d != h->d) return fail(RR_E_INVALID, "query dim %d != corpus dim %d", d, h->d);
   if (b < 1 || k < 1) return fail(RR_E_INVALID, "b=%d k=%d", b, k);
@@ -1630,10 +1758,11 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
 
 int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx) {
   if (!h || !out_scores || !out_idx) return fail(RR_E_INVALID, "null argument");
+  if (h->failed) return failed_handle();
   if (ticket < 0) return fail(RR_E_INVALID, "bad ticket %d", ticket);
   AsyncSlot& a = h->aslots[ticket % kAsyncSlots];
   if (!a.pending || a.ticket != ticket) return fail(RR_E_STATE, "ticket %d is not in flight", ticket);
-  HIP_TRY(hipEventSynchronize(a.done));
+  if (int rc = wait_event(h, a.done, "an asynchronous search")) return rc;
   a.pending = false;
   const size_t qbytes = (size_t)a.b * h->d * 4, cnt = (size_t)a.b * a.k;
   const size_t res_off = (qbytes + 255) & ~(size_t)255;
@@ -1642,8 +1771,10 @@ int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx) {
   memcpy(&flag, a.pin + res_off, sizeof flag);
   if (a.screened && flag >= (uint64_t)a.seq0) {
     // a block needed the exact pass: this batch again, exactly (every rank of an exchange sees the same
-    // flag here, so all re-run it together)
+    // flag here, so all re-run it together). A batch staged with rr_set_queries before this wait stays the
+    // staged batch (the re-run goes through the other query buffer).
     if (int rc = sync_streams(h)) return rc;
+    const int saved_qpar = h->qpar, saved_b = h->cur_b;
     int nq = 0;
     if (int rc = begin_stage(h, &nq)) return rc;
     if (int rc = stage_queries(h, nq, a.pin, qbytes, -1, false)) return rc;
@@ -1651,31 +1782,48 @@ int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx) {
     h->cur_b = a.b;
     const int saved = h->kernel;
     h->kernel = RR_KERNEL_EXACT;
-    const int rc = rr_search_staged(h, a.k);
+    int rc = rr_search_staged(h, a.k);
     h->kernel = saved;
-    if (rc) return rc;
-    ++h->screen_reruns;
-    note_rerun(h, a.narrow);
-    return rr_fetch_results(h, out_scores, out_idx);
+    if (rc == RR_OK) {
+      ++h->screen_reruns;
+      note_rerun(h, a.narrow);
+      rc = rr_fetch_results(h, out_scores, out_idx);
+    }
+    h->qpar = saved_qpar;
+    h->cur_b = saved_b;
+    return rc;
   }
   memcpy(out_scores, a.pin + res_off + kOutHead, cnt * 4);
   memcpy(out_idx, a.pin + idx_off, cnt * 8);
   return collect_timing(h);
 }
 
-int rr_screen_stats(rr_handle* h, int64_t* blocks, int64_t* fallbacks) {
+int rr_screen_counts(rr_handle* h, int64_t* blocks, int64_t* flagged, int64_t* reruns) {
   if (!h) return fail(RR_E_INVALID, "null handle");
+  if (h->failed) return failed_handle();
   if (int rc = rr_synchronize(h)) return rc;
   int64_t fb = 0;
   for (Shard& s : h->shards) {
     if (!s.scount) continue;
-    int f = 0;
     HIP_TRY(hipSetDevice(s.dev));
-    HIP_TRY(hipMemcpy(&f, s.scount, sizeof f, hipMemcpyDeviceToHost));
-    fb += f;
+    HIP_TRY(hipMemcpyAsync(s.pin_scount, s.scount, sizeof(int), hipMemcpyDeviceToHost, s.stream));
+    if (int rc = wait_stream(h, s.stream, "the flagged-block count")) return rc;
+    fb += *(volatile int*)s.pin_scount;
   }
   if (blocks) *blocks = h->screen_blocks * (int64_t)h->shards.size();
-  if (fallbacks) *fallbacks = fb;
+  if (flagged) *flagged = fb;
+  if (reruns) *reruns = h->screen_reruns;
+  return RR_OK;
+}
+
+int rr_screen_stats(rr_handle* h, int64_t* blocks, int64_t* fallbacks) {
+  return rr_screen_counts(h, blocks, fallbacks, nullptr);
+}
+
+int rr_set_timeout(rr_handle* h, int32_t ms) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  if (ms < 0) return fail(RR_E_INVALID, "timeout %d ms", ms);
+  h->timeout_ms = ms;
   return RR_OK;
 }
 
@@ -1688,6 +1836,7 @@ int rr_set_kernel(rr_handle* h, int kernel) {
 
 int rr_set_schedule(rr_handle* h, int dynamic) {
   if (!h) return fail(RR_E_INVALID, "null handle");
+  if (h->failed) return failed_handle();
   if (int rc = sync_streams(h)) return rc;   // no launch in flight uses the counter
   h->dyn_sched = dynamic ? 1 : 0;
   return RR_OK;
@@ -1695,6 +1844,7 @@ int rr_set_schedule(rr_handle* h, int dynamic) {
 
 int rr_set_compute_streams(rr_handle* h, int32_t n, int32_t* in_use) {
   if (!h) return fail(RR_E_INVALID, "null handle");
+  if (h->failed) return failed_handle();
   if (n < -1 || n == 0 || n > 2) return fail(RR_E_INVALID, "compute streams %d (-1 = as is, 1, 2)", n);
   if (n > 0 && n != h->streams) {
     if (int rc = rr_synchronize(h)) return rc;
@@ -1707,6 +1857,7 @@ int rr_set_compute_streams(rr_handle* h, int32_t n, int32_t* in_use) {
 
 int rr_screen_copy(rr_handle* h, int32_t use, int32_t* present) {
   if (!h) return fail(RR_E_INVALID, "null handle");
+  if (h->failed) return failed_handle();
   if (use >= 0) {
     h->screen_copy = use ? 1 : 0;
     if (!use)   // every stream of the handle may still be screening from the copy
@@ -1735,6 +1886,7 @@ int rr_set_timing(rr_handle* h, int enable) {
 
 int rr_kernel_time(rr_handle* h, double* total_ms, int64_t* launches, int reset) {
   if (!h) return fail(RR_E_INVALID, "null handle");
+  if (h->failed) return failed_handle();
   if (int rc = rr_synchronize(h)) return rc;
   if (total_ms) *total_ms = h->t_ms;
   if (launches) *launches = h->t_count;

@@ -55,6 +55,8 @@ struct SkArgs {
   int d, b;                // dimension, queries in this block
   uint32_t idx_base;       // global index of local row 0
   uint64_t* out;           // MODE 0: [grid][slots][KT] candidate keys
+  uint64_t* clear_word;    // MODE 0 (may be null): zeroed by workgroup 0 — the exchanged flag word the block's verify
+                           // raises (an earlier search with wider lists may have left keys at its position)
   uint32_t* ctr;           // MODE 0, dyn: the shard's chunk counter (0 between launches; the kernel resets it)
   int dyn;                 // MODE 0: 1 = dynamic chunk schedule (ctr), 0 = static (chunks g, g + grid, ...)
   // screen (KDT_SCREEN): upper bound u = s~ + eps_a |x||q| + eps_b (sqrt_d |x| + sum|q|)
@@ -99,10 +101,11 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
 // out_keys [slots][kt] (may be null); out_scores/out_idx [b][k_out] (may be null).
 // list_stride: elements between consecutive lists (0: slots * in_kt). flag_out: when non-null, raised
 // (max) to the largest of the words at in[l * list_stride + slots * in_kt] over the lists — the exchanged
-// screened-search flags of every shard.
+// screened-search flags of every shard. clear_word: when non-null, zeroed (the flag word that follows out_keys in
+// an exchange buffer: this search raises no flag, and an earlier one with wider lists may have left a key there).
 hipError_t launch_merge(int kt, const uint64_t* in, int nlists, int in_kt, int b, int k_out,
                         uint64_t* out_keys, float* out_scores, int64_t* out_idx, hipStream_t s, int slots = 32,
-                        int64_t list_stride = 0, uint64_t* flag_out = nullptr);
+                        int64_t list_stride = 0, uint64_t* flag_out = nullptr, uint64_t* clear_word = nullptr);
 
 // Top-k selection for 32 < k <= 256 (select_kernel, rr_kernels.hip): grid (32 query slots, parts).
 struct SelArgs {

@@ -460,8 +460,10 @@ __global__ __launch_bounds__(256) void merge_kernel(const uint64_t* __restrict__
                                                     int k_out, uint64_t* __restrict__ out_keys,
                                                     float* __restrict__ out_scores,
                                                     int64_t* __restrict__ out_idx, int64_t stride,
-                                                    uint64_t* __restrict__ flag_out) {
+                                                    uint64_t* __restrict__ flag_out,
+                                                    uint64_t* __restrict__ clear_word) {
   const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (clear_word && q == 0 && tid == 0) *clear_word = 0;
   if (flag_out && q == 0 && tid < 64) {   // the shards' screened-search flags (one word after each list)
     uint64_t f = 0;
     for (int l = tid; l < nlists; l += 64) f = umax64(f, in[(size_t)l * stride + (size_t)slots * KT]);
@@ -977,17 +979,17 @@ hipError_t launch_full_keys(int kdt, int metric, int grid, const void* c, const 
 
 hipError_t launch_merge(int kt, const uint64_t* in, int nlists, int in_kt, int b, int k_out, uint64_t* out_keys,
                         float* out_scores, int64_t* out_idx, hipStream_t s, int slots, int64_t list_stride,
-                        uint64_t* flag_out) {
+                        uint64_t* flag_out, uint64_t* clear_word) {
   if (list_stride == 0) list_stride = (int64_t)slots * in_kt;
   if (in_kt != kt) return hipErrorInvalidValue;   // lists are always produced at the kernel's KT
   // Rows >= b of out_keys are still produced (from the zero-filled slots) so the buffer is uniform.
   if (b > slots) return hipErrorInvalidValue;
   const int grid = out_keys ? slots : b;
   switch (kt) {
-    case 4: hipLaunchKernelGGL(merge_kernel<4>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out); break;
-    case 8: hipLaunchKernelGGL(merge_kernel<8>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out); break;
-    case 16: hipLaunchKernelGGL(merge_kernel<16>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out); break;
-    case 32: hipLaunchKernelGGL(merge_kernel<32>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out); break;
+    case 4: hipLaunchKernelGGL(merge_kernel<4>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out, clear_word); break;
+    case 8: hipLaunchKernelGGL(merge_kernel<8>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out, clear_word); break;
+    case 16: hipLaunchKernelGGL(merge_kernel<16>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out, clear_word); break;
+    case 32: hipLaunchKernelGGL(merge_kernel<32>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out, clear_word); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

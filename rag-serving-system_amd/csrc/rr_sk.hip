@@ -293,6 +293,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   constexpr int QS = 32 * QH;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   SK_PROBE(0);
+  if constexpr (MODE == 0) {   // the exchanged flag word this block's verify may raise starts at 0
+    if (a.clear_word && blockIdx.x == 0 && threadIdx.x == 0) *a.clear_word = 0;
+  }
   const char* __restrict__ corpus = a.corpus;
   const float* __restrict__ norms = a.norms;
   const float* __restrict__ rscale = a.rscale;

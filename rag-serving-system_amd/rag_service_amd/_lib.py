@@ -28,6 +28,7 @@ RR_E_RCCL = -3
 RR_E_STATE = -4
 RR_E_UNSUPPORTED = -5
 RR_E_OOM = -6
+RR_E_TIMEOUT = -7
 RR_DTYPE_F32 = 0
 RR_DTYPE_BF16 = 1
 RR_DTYPE_F32_SPLIT = 2
@@ -41,7 +42,7 @@ RR_KERNEL_AUTO = 0
 RR_KERNEL_FUSED = 1
 RR_KERNEL_EXACT = 2
 RR_KERNEL_SCREEN_FALLBACK = 3
-RR_ABI_VERSION = 4
+RR_ABI_VERSION = 5
 
 DTYPES = {"fp32": RR_DTYPE_F32, "float32": RR_DTYPE_F32, "f32": RR_DTYPE_F32,
           "bf16": RR_DTYPE_BF16, "bfloat16": RR_DTYPE_BF16, "fp32-split": RR_DTYPE_F32_SPLIT}
@@ -80,6 +81,8 @@ SIGNATURES = {
     "rr_set_compute_streams": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_i32)]),
     "rr_last_shape": (_c_int, [_vp, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32)]),
     "rr_dist_info": (_c_int, [_vp, _ip, _ip]),
+    "rr_screen_counts": (_c_int, [_vp, _i64p, _i64p, _i64p]),
+    "rr_set_timeout": (_c_int, [_vp, _c_i32]),
 }
 
 
@@ -327,6 +330,19 @@ class Index:
         b, f = _c_i64(), _c_i64()
         _check(self._lib.rr_screen_stats(self._h, ctypes.byref(b), ctypes.byref(f)))
         return b.value, f.value
+
+    def screen_counts(self) -> Tuple[int, int, int]:
+        """(screened search blocks, blocks flagged for the exact pass, exact re-runs the handle ran). Flagged
+        blocks of staged searches that were superseded before anyone fetched them are never re-run; a benchmark
+        pays flagged - re-runs exact searches itself."""
+        b, f, r = _c_i64(), _c_i64(), _c_i64()
+        _check(self._lib.rr_screen_counts(self._h, ctypes.byref(b), ctypes.byref(f), ctypes.byref(r)))
+        return b.value, f.value, r.value
+
+    def set_timeout(self, ms: int) -> None:
+        """Multi-process deadline of every host wait on device work (0 = none); a miss raises
+        HipRetrievalError with code RR_E_TIMEOUT and fails the handle."""
+        _check(self._lib.rr_set_timeout(self._h, int(ms)))
 
     def set_timing(self, enable: bool) -> None:
         _check(self._lib.rr_set_timing(self._h, 1 if enable else 0))

@@ -53,6 +53,15 @@ def max_over_ranks(dist, x: float) -> float:
     return float(t.item())
 
 
+def sum_over_ranks(dist, x: float) -> float:
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
 def barrier(dist) -> None:
     if dist is not None:
         dist.barrier()

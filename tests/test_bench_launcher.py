@@ -22,3 +22,19 @@ def test_plain_launch_reaches_timed_loop(n):
     rec = json.loads(lines[0])
     assert rec["dry_run"] and rec["n_gpus"] == n and rec["ranks_seen"] == n
     assert rec["launched_by"] == ("torch.distributed.run" if n > 1 else "plain")
+
+
+def test_missed_deadline_exits_loudly():
+    """The deadline path of the N > 1 bench: rank 1 stalls past --dist-timeout-s before the
+    barrier every rank must pass. Rank 0's wait times out; it prints a JSON error line naming its rank and the
+    stage, and exits non-zero (no hang, no re-exec); the launcher's exit status is non-zero."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run",
+                          "--dry-run-stall-rank", "1", "--dist-timeout-s", "4"], capture_output=True, text=True,
+                         timeout=240, env=env, cwd=REPO)
+    assert out.returncode != 0
+    recs = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    errs = [r for r in recs if r.get("error")]
+    assert errs, out.stdout + out.stderr[-2000:]
+    r0 = [r for r in errs if r["rank"] == 0]
+    assert r0 and r0[0]["stage"] == "dry-run barrier" and r0[0]["value"] is None and r0[0]["n_gpus"] == 2

@@ -1,0 +1,161 @@
+"""Robustness of the search pipeline's bookkeeping: the exchanged flag word, query buffers that a
+re-run still needs, the ranks' agreement on the screened path, and the multi-process deadline. Every case checks
+results against the one-pass exact kernel (RR_KERNEL_EXACT) of another handle on the same corpus."""
+import os
+import time
+
+import numpy as np
+import pytest
+
+from oracle import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def Index(hip):
+    from rag_service_amd import Index as _Index
+    return _Index
+
+
+def _exact(Index, corpus, metric="cosine"):
+    ex = Index(dtype="fp32", metric=metric)
+    ex.load(corpus)
+    ex.set_kernel("exact")
+    return ex
+
+
+def _same(got, want):
+    return np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
+
+
+def test_exchange_flag_word_cleared_between_list_widths(Index):
+    """Through the RCCL exchange (1-rank communicator): k = 20 screens with 32-entry lists, so its exchanged keys
+    reach past where k = 3's flag word sits (after 32 x 8 keys). Every buffer set is written at k = 20, then read
+    at k = 3: without the per-block clear each k = 3 search would see a stale key as its flag and re-run exactly.
+    No block may be flagged or re-run, and the results are exact."""
+    from rag_service_amd import get_unique_id
+    corpus = synth.unit_norm_gaussian(41, 30000, 1024)
+    q = synth.unit_norm_gaussian(42, 32, 1024)
+    ex = _exact(Index, corpus)
+    rc = Index(dtype="fp32", metric="cosine")
+    rc.init_dist(1, 0, get_unique_id())
+    rc.load(corpus)
+    for k in (20, 3):
+        want = ex.search(q, k)
+        for _ in range(6):                                    # > the 4 exchange buffer sets
+            assert _same(rc.search(q, k), want), k
+    blocks, flagged, reruns = rc.screen_counts()
+    assert (blocks, flagged, reruns) == (12, 0, 0)
+    # the one-pass path (its merge kernel writes the exchange buffer) clears the word too: exact k = 20 then k = 3
+    # searches, then screened ones — a stale key merged into the result head would flag every later search
+    rc.set_kernel("exact")
+    for k in (20, 3):
+        want = ex.search(q, k)
+        for _ in range(6):
+            assert _same(rc.search(q, k), want), k
+    rc.set_kernel("auto")
+    want = ex.search(q, 3)
+    for _ in range(6):
+        assert _same(rc.search(q, 3), want)
+    assert rc.screen_counts() == (18, 0, 0)
+    ex.close()
+    rc.close()
+
+
+def test_rccl_one_rank_range_guard_agreement(Index):
+    """rr_init_dist handles agree on the screened path through an RCCL min at load time (finish_all): a shard with
+    a value >= 2^15 turns screening off. With one rank the agreement still runs through RCCL; results exact."""
+    from rag_service_amd import get_unique_id
+    rng = np.random.default_rng(8)
+    corpus = rng.standard_normal((5000, 512)).astype(np.float32)
+    q = rng.standard_normal((32, 512)).astype(np.float32)
+    ex = _exact(Index, corpus, "dot")
+    rc = Index(dtype="fp32", metric="dot")
+    rc.init_dist(1, 0, get_unique_id())
+    rc.load(corpus)
+    assert _same(rc.search(q, 5), ex.search(q, 5))
+    assert rc.screen_stats() == (1, 0)
+    big = corpus.copy()
+    big[7, 9] = 40000.0
+    rc.load(big)
+    ex.load(big)
+    assert _same(rc.search(q, 5), ex.search(q, 5))
+    assert rc.screen_stats() == (0, 0)
+    rc.close()
+    ex.close()
+
+
+def test_wait_rerun_keeps_the_staged_batch(Index):
+    """rr_wait re-runs a flagged asynchronous search through the other query buffer and restores the staged
+    batch: a batch staged with set_queries BEFORE the wait is the one the next search_staged searches."""
+    corpus = synth.unit_norm_gaussian(51, 20000, 1024)
+    qa = synth.unit_norm_gaussian(52, 32, 1024)
+    qb = synth.unit_norm_gaussian(53, 20, 1024)
+    ex = _exact(Index, corpus)
+    ix = Index(dtype="fp32", metric="cosine")
+    ix.load(corpus)
+    ix.set_kernel("screen-fallback")                           # every block flagged: rr_wait re-runs exactly
+    t = ix.search_async(qb, 4)
+    ix.set_queries(qa)
+    assert _same(ix.wait(t), ex.search(qb, 4))
+    ix.search_staged(6)
+    assert _same(ix.fetch(), ex.search(qa, 6))
+    assert ix.last_shape() == (32, 6)
+    ix.close()
+    ex.close()
+
+
+def test_growing_batch_settles_the_last_search_first(Index):
+    """A staged search whose block is flagged, then a LARGER batch staged (the query buffers grow and are zeroed):
+    the earlier search is settled before its queries are dropped, so fetching it still gives its exact results."""
+    corpus = synth.unit_norm_gaussian(61, 20000, 1024)
+    qa = synth.unit_norm_gaussian(62, 32, 1024)
+    qbig = synth.unit_norm_gaussian(63, 100, 1024)
+    ex = _exact(Index, corpus)
+    ix = Index(dtype="fp32", metric="cosine")
+    ix.load(corpus)
+    ix.set_kernel("screen-fallback")
+    ix.set_queries(qa)
+    ix.search_staged(5)
+    ix.set_queries(qbig)                                       # q_cap 32 -> 100: buffers reallocated
+    assert _same(ix.fetch(), ex.search(qa, 5))
+    ix.search_staged(5)
+    assert _same(ix.fetch(), ex.search(qbig, 5))
+    ix.close()
+    ex.close()
+
+
+def test_dist_deadline_fails_loudly(Index, monkeypatch):
+    """The multi-process deadline (rr_set_timeout): device work that does not finish in time makes the wait return
+    RR_E_TIMEOUT naming the rank, and fails the handle (later calls: RR_E_STATE). The stall is a stand-in kernel
+    holding the exchange stream 1 ms per search block (RR_X_EXCHANGE_DELAY_US), after each block's all-gather, with
+    a 2 ms deadline over 24 blocks; the device is left to drain before the handle is destroyed."""
+    from rag_service_amd import get_unique_id
+    from rag_service_amd._lib import HipRetrievalError, RR_E_STATE, RR_E_TIMEOUT
+    corpus = synth.unit_norm_gaussian(71, 8000, 512)
+    q = synth.unit_norm_gaussian(72, 32, 512)
+    monkeypatch.setenv("RR_X_EXCHANGE_DELAY_US", "1000")
+    ix = Index(dtype="fp32", metric="cosine")
+    monkeypatch.delenv("RR_X_EXCHANGE_DELAY_US")
+    ix.init_dist(1, 0, get_unique_id())
+    ix.load(corpus)
+    ix.search(q, 5)                                            # warm: no deadline yet (default 120 s)
+    ix.set_timeout(2)
+    ix.set_queries(q)
+    for _ in range(24):
+        ix.search_staged(5)
+    t0 = time.perf_counter()
+    with pytest.raises(HipRetrievalError) as e:
+        ix.synchronize()
+    assert e.value.code == RR_E_TIMEOUT and "rank 0 of 1" in str(e.value)
+    assert time.perf_counter() - t0 < 1.0
+    with pytest.raises(HipRetrievalError) as e2:
+        ix.search_staged(5)
+    assert e2.value.code == RR_E_STATE
+    time.sleep(1.0)                                            # 24 ms of stand-in delay: the queues drain
+    ix.close()
+    ok = Index(dtype="fp32", metric="cosine")                  # the device is fine afterwards
+    ok.load(corpus)
+    ok.search(q, 5)
+    ok.close()

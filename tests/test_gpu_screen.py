@@ -2,6 +2,8 @@
 exact rescoring of the KT candidates with the DT 3 arithmetic, and an exact fallback pass when the bound cannot
 prove completeness. Its results must be BIT-IDENTICAL to the one-pass exact kernel (RR_KERNEL_EXACT) in every
 case — screened, forced fallback, shards, cosine and dot — and match the oracle."""
+import functools
+
 import numpy as np
 import pytest
 
@@ -111,6 +113,108 @@ def test_screen_guards_f16_range(Index):
     ix.search(q[:2], 4)
     assert ix.screen_stats() == (0, 0)                          # counters restart at the load; nothing screened
     ix.close()
+
+
+@functools.lru_cache(maxsize=None)
+def _tiny_cases():
+    """Corpora and queries with elements in and below the f16 subnormal range (|x| < 2^-14 = 6.1e-5): there the
+    screen's f16 values keep only a few significant bits (or round to 0), and its bound leans on the absolute
+    rounding term eps_b (<= 2^-25 per element, rr_api.cpp kScreenEpsB) — valid only if neither the conversions nor
+    the f16 MFMA flush subnormal inputs. Each case: (name, corpus, queries)."""
+    rng = np.random.default_rng(2024)
+    n, d, b = 20011, 1024, 32
+    base = rng.standard_normal((n, d)).astype(np.float32)
+    q = rng.standard_normal((b, d)).astype(np.float32)
+    cases = []
+    for e in (14, 18, 22):                                     # every row scaled into / below the subnormal range
+        cases.append((f"rows_2^-{e}", base * np.float32(2.0 ** -e), q))
+    cases.append(("queries_2^-16", base, q * np.float32(2.0 ** -16)))
+    cases.append(("both_2^-12", base * np.float32(2.0 ** -12), q * np.float32(2.0 ** -12)))
+    mixed = base * np.exp2(-rng.integers(0, 25, size=(n, 1))).astype(np.float32)   # 2^0 .. 2^-24 per row
+    cases.append(("mixed_scales", mixed, q))
+    # the top rows are tiny: near-copies of each query scaled by 2^-20 (cosine ranks them first; by dot they sit
+    # among rows of scale 2^-10), plus full-scale rows anti-aligned with the queries
+    top = base * np.float32(2.0 ** -10)
+    for i in range(b):
+        for j in range(3):
+            near = q[i] + 0.05 * rng.standard_normal(d).astype(np.float32)
+            top[97 + 613 * i + 5 * j] = near * np.float32(2.0 ** -20)
+    big = rng.choice(n, 300, replace=False)
+    big = big[(big - 97) % 613 >= 16]
+    top[big] = -q[rng.integers(0, b, big.size)] * np.float32(4.0)
+    cases.append(("tiny_top_rows", top, q))
+    return cases
+
+
+@pytest.mark.parametrize("case", range(7))
+@pytest.mark.parametrize("metric", ["cosine", "dot"])
+def test_screen_subnormal_range(Index, case, metric):
+    """f16-subnormal magnitudes: rows scaled by 2^-14 / 2^-18 / 2^-22, tiny queries, mixed
+    per-row scales and tiny top rows. The screened search (f16 copy, and the fp32-reading screen) must return
+    results BIT-IDENTICAL to the one-pass exact kernel, and the oracle's top-k (fp64 scores; index swaps only
+    between numerically tied documents, relative to the scores' own scale)."""
+    name, corpus, q = _tiny_cases()[case]
+    ex = Index(dtype="fp32", metric=metric)
+    ex.load(corpus)
+    ex.set_kernel("exact")
+    ix = Index(dtype="fp32", metric=metric)
+    ix.load(corpus)
+    assert ix.screen_copy()
+    exact = exact_scores(corpus, q, metric)
+    for k in (1, 5, 10):
+        want = ex.search(q, k)
+        got16 = ix.search(q, k)
+        assert np.array_equal(got16[1], want[1]) and np.array_equal(got16[0], want[0]), (name, k)
+        _, cidx = canonical_topk(exact, k)
+        scale = float(np.max(np.abs(np.take_along_axis(exact, cidx, axis=1))))
+        check_topk(got16[1], got16[0], cidx, corpus, q, metric, near_tie=2e-5 * scale + 1e-30,
+                   score_tol=1e-3 * max(scale, 1e-30) if metric == "dot" else 1e-3)
+    blocks16, flagged16 = ix.screen_stats()
+    ix.screen_copy(False)                                      # DT 6: the fp32 rows rounded to f16 in registers
+    for k in (1, 5, 10):
+        want = ex.search(q, k)
+        got32 = ix.search(q, k)
+        assert np.array_equal(got32[1], want[1]) and np.array_equal(got32[0], want[0]), (name, k)
+    blocks, flagged = ix.screen_stats()
+    assert blocks == 6 and blocks16 == 3
+    print(f"{name} {metric}: flagged {flagged16}/3 (f16 copy), {flagged - flagged16}/3 (fp32 screen)")
+    ix.close()
+    ex.close()
+
+
+def test_screen_f16_conversion_keeps_subnormals(Index):
+    """The property the bound relies on, observed directly: the screen's bound stays valid only if f16 subnormal
+    values are neither flushed by the conversion nor by the MFMA. A corpus of one-hot rows whose single non-zero
+    element is an f16 subnormal (k * 2^-24, k = 1..1023), each queried by the matching one-hot query of a large
+    value, makes the f16 product the ONLY non-zero term of every score. Kept, the screen's top-4 for query c are
+    column c's rows and the exact top-1 (>= 513 * 2^-14) clears the 4th bound (~1.5e-4): no block flagged. Flushed,
+    every u would be the bound's |x|-proportional terms alone, the top-4 would be rows 1019-1022 for every query,
+    their exact scores 0, and the block flagged. Dot, k = 1: results bit-identical to the exact kernel, 0 flagged."""
+    d = 512                                                    # the f16 copy serves d % 512 == 0
+    n = 1023
+    corpus = np.zeros((n, d), dtype=np.float32)
+    col = np.arange(n) % d
+    corpus[np.arange(n), col] = (np.arange(n) + 1).astype(np.float32) * np.float32(2.0 ** -24)
+    q = np.zeros((d, d), dtype=np.float32)
+    q[np.arange(d), np.arange(d)] = 1024.0
+    ex = Index(dtype="fp32", metric="dot")
+    ex.load(corpus)
+    ex.set_kernel("exact")
+    ix = Index(dtype="fp32", metric="dot")
+    ix.load(corpus)
+    want = ex.search(q[:32], 1)
+    got = ix.search(q[:32], 1)
+    assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
+    # query column c: rows c and c + 512 (if < 1023): the last one holds the largest value
+    expect = np.array([max(r for r in range(c, n, d)) for c in range(32)])
+    assert np.array_equal(got[1][:, 0], expect)
+    assert ix.screen_stats() == (1, 0)                         # proven by the screen: subnormals were kept
+    ix.screen_copy(False)                                      # the same through the fp32-reading screen (DT 6)
+    got = ix.search(q[:32], 1)
+    assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
+    assert ix.screen_stats() == (2, 0)
+    ix.close()
+    ex.close()
 
 
 @pytest.mark.parametrize("shards", [2, 8])
