@@ -81,8 +81,15 @@ struct TopK {
 // ------------------------------------------------------------------------------------------------
 template <int CTRL, int ROW_MASK = 0xF>
 __device__ __forceinline__ uint32_t dpp_max_u32(uint32_t v) {
-  const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROW_MASK, 0xF, false);
-  return v > t ? v : t;
+  if constexpr (ROW_MASK == 0xF) {
+    // every lane reads a valid source lane (quad_perm / row mirrors): a plain DPP move, which the compiler folds
+    // into the max itself (v_max_u32_dpp: one VALU instead of a copy, the DPP move and the max)
+    const uint32_t t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+    return v > t ? v : t;
+  } else {
+    const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROW_MASK, 0xF, false);
+    return v > t ? v : t;
+  }
 }
 // max over aligned groups of G lanes (G = 2, 4, 8, 16), every lane of the group gets it
 template <int G>

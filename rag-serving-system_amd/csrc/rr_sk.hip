@@ -218,26 +218,34 @@ __device__ __forceinline__ int slab_off(int r, int cp) { return (r >> 3) * 1024 
 //      non-empty). Every key of the global top-KT is >= H: KT distinct heads are >= H, so a key below H has
 //      rank >= KT. Only the <= KT lists whose head is >= H can hold such keys: <= KT x KT candidates;
 //   3. the non-empty keys >= H are appended to an LDS array, and the candidate of rank r < KT is akeys[r].
-// Keys are unique (distinct row indices), so ranks are distinct. Scratch: LDS free in MODE 1 (the slab ring):
-// [kThreads] heads, [KT * KT] candidates, H, count.
+// Keys are unique (distinct row indices), so ranks are distinct. Each list of the screen carries its workgroup's
+// floor after its KT keys (see KL in sk_score_kernel): their maximum goes to *floor_out (LDS; valid after the return).
+// Lists folded into another thread's list drop keys only below that list's last entry, which stays in the global
+// top-KT's bound (every key left out is at most the KT-th candidate). Scratch: LDS free in MODE 1 (the slab ring):
+// [kThreads] heads, [KT * KT] candidates, H, count, floor maximum.
 template <int KT>
 __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict__ in, int nlists, int qslots, int q,
-                                                      uint64_t* scratch, uint64_t* akeys) {
+                                                      uint64_t* scratch, uint64_t* akeys, uint64_t* floor_out) {
   const int tid = threadIdx.x;
   uint64_t* heads = scratch;
   uint64_t* cand = scratch + kThreads;
   uint64_t* hs = cand + KT * KT;
   int* cnt = (int*)(hs + 1);
+  unsigned long long* fmax = (unsigned long long*)(hs + 2);
+  constexpr int LS = KT + 1;   // list stride: KT keys + the workgroup's floor
   TopK<KT> tk;
+  uint64_t fl = 0;
   if (tid < nlists) {
-    const uint64_t* src = in + ((size_t)q * nlists + tid) * KT;   // query-major screen lists
+    const uint64_t* src = in + ((size_t)q * nlists + tid) * LS;   // query-major screen lists
 #pragma unroll
     for (int i = 0; i < KT; ++i) tk.v[i] = src[i];
+    fl = src[KT];
   } else {
     tk.init();
   }
   for (int l = tid + kThreads; l < nlists; l += kThreads) {   // lists beyond kThreads folded in (sorted input)
-    const uint64_t* src = in + ((size_t)q * nlists + l) * KT;
+    const uint64_t* src = in + ((size_t)q * nlists + l) * LS;
+    fl = umax64(fl, src[KT]);
     for (int i = 0; i < KT; ++i) {
       const uint64_t key = src[i];
       if (key <= tk.last()) break;
@@ -248,9 +256,11 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
   if (tid == 0) {
     hs[0] = 0;
     cnt[0] = 0;
+    *fmax = 0;
   }
   if (tid < nl) heads[tid] = tk.v[0];
   __syncthreads();
+  if (fl != 0) __hip_atomic_fetch_max(fmax, (unsigned long long)fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (tid < nl && tk.v[0] != 0) {
     const uint64_t me = tk.v[0];
     int rank = 0;
@@ -258,6 +268,7 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
     if (rank == KT - 1) hs[0] = me;
   }
   __syncthreads();
+  if (tid == 0) *floor_out = *fmax;
   const uint64_t th = hs[0];
   if (tid < nl && tk.v[0] != 0 && tk.v[0] >= th) {
     int c = 0;
@@ -307,6 +318,11 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
   constexpr bool SCR = DT == 6 || DT == 7;                      // the screen (upper bounds, "Screened search")
+  // The screen's per-lane lists hold KL keys, not KT: a query's LPQ lanes together still hold >= KT, and a lane drops
+  // a key only below its own last entry. The workgroup reports the largest last entry of its full lanes as its FLOOR
+  // (no key missing from its list is above max(the list's KT-th key, the floor)); the verify adds the floors to its
+  // completeness bound. The branch-free insert, the epilogue's largest VALU item, then costs KL compare-selects.
+  constexpr int KL = SCR && KT > 4 ? 4 : KT;
   constexpr int EB = DT == 1 || DT == 7 ? 2 : 4;                // storage bytes per element
   const int row_bytes = d * EB;
   constexpr int KS = NS * kSlabRowBytes;                        // bytes of a row per wave
@@ -329,6 +345,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   float* gnorm = (float*)(grow + 32);
   int* gvalid = (int*)(gnorm + 32);
   uint64_t* xk = (uint64_t*)(gvalid + 32);
+  uint64_t* vfloor = xk + KT;   // MODE 1: the largest floor of the screen's lists (see KL)
   // MODE 1 reads its 32 gathered rows straight into registers (all loads issued at once: one latency), the
   // exact fragments the LDS image would give: lane (r, h) takes 16-byte units 4(i>>1) + 2h + (i&1) of slab j
   f32x4 vrow[MODE == 1 ? NS : 1][4];
@@ -662,9 +679,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // ---- MODE 1: this query's candidates (the queries' fragments and scalars above are already built, so
   // their loads overlapped the list loads), then their rows straight into registers ---------------------------
   if constexpr (MODE == 1) {
-    static_assert((size_t)(kThreads + KT * KT + 2) * 8 <= ring_bytes(RS), "verify merge scratch in the slab ring");
+    static_assert((size_t)(kThreads + KT * KT + 3) * 8 <= ring_bytes(RS), "verify merge scratch in the slab ring");
     SK_PROBE(6);
-    merge_lists_for_query<KT>(a.vin, a.nlists, QS, vq, (uint64_t*)smem, akeys);
+    merge_lists_for_query<KT>(a.vin, a.nlists, QS, vq, (uint64_t*)smem, akeys, vfloor);
     SK_PROBE(7);
     if (tid < 32) {
       const uint64_t k0 = akeys[0];
@@ -706,7 +723,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     qsa = s1 * (1.0f + 0x1p-18f);
   }
 
-  TopK<KT> tk;
+  TopK<KL> tk;
   tk.init();
 
   SK_PROBE(1);
@@ -900,8 +917,17 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     // no lane keeps it — the merged lists are the same as without the bar, but lanes insert ~LPQ x less often
     // (the branch-free insert is the epilogue's largest VALU cost, and it runs for the whole wave whenever
     // any of its lanes inserts). For the large-k floors: a key dropped here is below a full lane's last entry.
-    const uint64_t bar = group_max_u64<LPQ>(tk.last());
+    uint64_t bar = 0;
     float thr = -INFINITY;
+    if constexpr (SCR) {
+      // the screen compares in the bound's own (float) domain: u below the lane group's largest last score cannot
+      // enter (see the bar above; ties on the score go on to the insert, whose 64-bit compares place them exactly),
+      // and only the keys that pass are formed — one compare per score instead of a key and a 64-bit compare
+      const uint32_t bh = group_max_u32<LPQ>((uint32_t)(tk.last() >> 32));
+      if (bh != 0) thr = float_of_ord(bh);
+    } else {
+      bar = group_max_u64<LPQ>(tk.last());
+    }
     if constexpr (COS && !SCR) {
       const uint64_t last = bar;
       if (last != 0) {
@@ -909,6 +935,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         thr = t - fabsf(t) * 0x1p-20f - 0x1p-100f;
       }
     }
+    // rows of this tile (scalar; 32 except in the last tile): the screen's validity test is one 32-bit compare
+    const int rem = MODE == 0 ? (int)(n - base < 32 ? n - base : 32) : 32;
+    const uint32_t key_base = MODE == 0 ? idx_base + (uint32_t)base : 0u;
 #pragma unroll
     for (int e = 0; e < DPL; ++e) {
       int64_t row;
@@ -921,7 +950,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         if constexpr (COS) nd = gnorm[er + e];
       } else {
         row = base + er + e;
-        valid = qev && (base + 32 <= n || row < n);   // (whole tiles: a scalar test)
+        // (the screen keeps lists for padding query slots too: nobody reads them)
+        valid = SCR ? er + e < rem : qev && (base + 32 <= n || row < n);   // (whole tiles: a scalar test)
         const float* tf = trow + ts * 64 + er + e;   // factor 0 at tf[0], factor 1 at tf[32]
         if constexpr (DT == 2) s = s * (COS ? tf[32] : tf[0]) * qs;   // exact 2^e rescales
         if constexpr (COS || SCR) nd = tf[0];
@@ -940,8 +970,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         } else {
           u = v;
         }
-        const uint64_t key = make_key(u, idx_base + (uint32_t)row);
-        if (valid && key > bar) tk.insert(key);
+        if (valid && u >= thr) tk.insert(make_key(u, key_base + (uint32_t)(er + e)));   // (NaN: never)
       } else if constexpr (COS) {
         // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
         const float den = cos_den(qn, nd);
@@ -981,7 +1010,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   SK_PROBE(4);
 
   // ---- per query: merge its LPQ lane lists (KT rounds of an LPQ-lane max; keys are unique) -------------
-  if constexpr (MODE == 0 && KT == 32 && QH == 1 && SCHED == 0) {
+  if constexpr (MODE == 0 && KT == 32 && QH == 1 && SCHED == 0 && !SCR) {
     if (a.all_keys) return;
     if (a.wide_k > 0) {
       // Large k: the query's top-wide_k of its LPQ lane lists. The lists go to LDS (the ring and the partial
@@ -1013,9 +1042,14 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     }
   }
   if constexpr (MODE == 0) {
-    // the screen's lists go query-major, [QS][grid][KT]: each verify workgroup then reads its query's lists as
-    // one contiguous block (the other paths' merge_kernel reads [grid][QS][KT])
-    uint64_t* dst = a.out + (SCR ? ((size_t)qe * G + g) : ((size_t)g * QS + qe)) * KT;
+    // the screen's lists go query-major, [QS][grid][KT + 1] — KT keys, then the workgroup's floor (see KL): each
+    // verify workgroup then reads its query's lists as one contiguous block (the other paths' merge_kernel reads
+    // [grid][QS][KT])
+    uint64_t* dst = a.out + (SCR ? ((size_t)qe * G + g) * (KT + 1) : ((size_t)g * QS + qe) * KT);
+    if constexpr (SCR) {   // before any pop: a full lane's last entry bounds every key it dropped
+      const uint64_t fl = group_max_u64<LPQ>(tk.v[KL - 1]);
+      if (lane % LPQ == 0) dst[KT] = KL < KT ? fl : 0;   // (KL = KT: the lists are the exact top-KT)
+    }
 #pragma unroll 1
     for (int rnd = 0; rnd < KT; ++rnd) {
       const uint64_t m = group_max_u64<LPQ>(tk.v[0]);
@@ -1031,8 +1065,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       if (qe == vq && lane % LPQ == 0) xk[rnd] = m;
     }
     if (qe != vq || lane % LPQ != 0) return;
-    // leader of query slot vq: completeness, then the results
-    const uint64_t ukt = akeys[KT - 1];          // the KT-th upper bound (0: fewer than KT docs here)
+    // leader of query slot vq: completeness, then the results. Every key not rescored is at most the KT-th
+    // candidate's bound or a workgroup's floor (0, 0: fewer than KT docs here and nothing dropped)
+    const uint64_t ukt = umax64(akeys[KT - 1], *vfloor);
     const uint64_t ek = xk[a.k_out - 1];         // the exact k-th key
     bool complete = ukt == 0 || (ek != 0 && (uint32_t)(ek >> 32) > (uint32_t)(ukt >> 32));
     complete = complete && qinfo[QS + vq] < 32768.0f && !a.force_incomplete;   // f16 range of the screen
@@ -1106,8 +1141,8 @@ size_t sk_lds_bytes(int sdt, bool cos, int ring, int qslots) {
   (void)sdt;
   (void)cos;
   // + per-row factors [3][2][32], next-chunk words [4], query scalars [3][qslots], MODE 1 scratch: W [8][32] +
-  // akeys [32] keys, grow / gnorm / gvalid [32], xk [32] keys
-  const size_t verify = (size_t)(kWaves * 32 + 32 + 32) * 8 + 3 * 32 * 4;
+  // akeys [32] keys, grow / gnorm / gvalid [32], xk [32] keys, the floors' maximum
+  const size_t verify = (size_t)(kWaves * 32 + 32 + 32 + 1) * 8 + 3 * 32 * 4;
   return sk::ring_bytes(ring) + sk::red_bytes(ring, qslots / 32) + 3 * 64 * 4 + 4 * 4 + 3 * qslots * 4 + verify;
 }
 

@@ -1,14 +1,15 @@
 """Golden vectors for the embedding half, from the REFERENCE's BatchProcessor._process_batch itself
 (rag_service/core/batch_processor.py:74-125; build container only).
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_embed_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_embed_golden.py [short_facts|squad]
 
 The reference runs on CPU with the deterministic stand-in models of tests/embed_fixture.py, its own
-in-memory RequestQueue and its own CupyRetriever over the short_facts corpus (NumPy stand-in for the
-module-level cupy import, as make_golden.py). A wrapper around the retriever records the (B, 1024) array
-_process_batch hands to batch_retrieve; the LLM stand-in records the prompts. Output
-tests/golden/golden_embed.npz (embeddings per batch) + golden_embed.json (ks, documents, prompts, stored
-results) — data only. `redis` gets an inert stand-in (only RedisRequestQueue touches it).
+in-memory RequestQueue and its own CupyRetriever over the short_facts corpus (or the SQuAD corpus,
+BASELINE config 4's: data/squad_embeddings.npy + squad_contexts.json, with the SQuAD questions) (NumPy
+stand-in for the module-level cupy import, as make_golden.py). A wrapper around the retriever records the
+(B, 1024) array _process_batch hands to batch_retrieve; the LLM stand-in records the prompts. Output
+tests/golden/golden_embed[_squad].npz (embeddings per batch) + golden_embed[_squad].json (ks, documents,
+prompts, stored results) — data only. `redis` gets an inert stand-in (only RedisRequestQueue touches it).
 """
 import json
 import os
@@ -26,7 +27,7 @@ import embed_fixture as fx  # noqa: E402
 from make_golden import import_reference, REF  # noqa: E402
 
 
-def main():
+def main(corpus_name="short_facts"):
     rd = types.ModuleType("redis")
     rd.from_url = lambda *a, **k: None
     sys.modules.setdefault("redis", rd)
@@ -34,9 +35,9 @@ def main():
     import importlib
     bp = importlib.import_module("rag_service.core.batch_processor")
     rq = importlib.import_module("rag_service.core.request_queue")
-    corpus = np.load(os.path.join(HERE, "data", "short_facts_embeddings.npy"))
-    contexts = json.load(open(os.path.join(HERE, "data", "short_facts_contexts.json")))
-    queries = json.load(open(os.path.join(HERE, "data", "short_facts_queries.json")))
+    corpus = np.load(os.path.join(HERE, "data", f"{corpus_name}_embeddings.npy"))
+    contexts = json.load(open(os.path.join(HERE, "data", f"{corpus_name}_contexts.json")))
+    queries = json.load(open(os.path.join(HERE, "data", f"{corpus_name}_queries.json")))
 
     seen = []
 
@@ -69,11 +70,12 @@ def main():
         out_json["batches"][-1]["min_gap"] = float(min(s[i, k - 1] - s[i, k] for i, k in enumerate(ks)
                                                        if 0 < k < s.shape[1]))
         print(f"batch {bi}: B={len(batch)} min gap {out_json['batches'][-1]['min_gap']:.3g}", flush=True)
-    np.savez_compressed(os.path.join(HERE, "golden_embed.npz"), **out_npz)
-    with open(os.path.join(HERE, "golden_embed.json"), "w") as f:
+    tag = "" if corpus_name == "short_facts" else f"_{corpus_name}"
+    np.savez_compressed(os.path.join(HERE, f"golden_embed{tag}.npz"), **out_npz)
+    with open(os.path.join(HERE, f"golden_embed{tag}.json"), "w") as f:
         json.dump(out_json, f)
     print("reference:", REF, "done")
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else "short_facts")

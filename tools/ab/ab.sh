@@ -13,6 +13,6 @@ for rep in 1 2; do
   for arm in "$@"; do
     if [ $arm = new ]; then L=$R/rag-serving-system_amd/librag_retrieval.so; else L=$R/tools/ab/librag_retrieval_$arm.so; fi
     RR_LIBRARY=$L timeout -k 10 200 python3 "$R/bench.py" --gpus 1 $W > /tmp/ab.json 2>/tmp/ab.err || { tail -5 /tmp/ab.err >> "$OUT"; exit 1; }
-    python3 -c "import json; d=json.loads(open('/tmp/ab.json').read().strip().splitlines()[-1]); s=d['steady_state']; print('$arm', d['value'], d['roofline']['kernel_avg_us'], d['roofline']['frac'], '| steady', s['value'], s['kernel_avg_us'], s['frac'], '| fallbacks', d['roofline'].get('screen_fallbacks'), '/', d['roofline'].get('screened_blocks'))" >> "$OUT"
+    python3 -c "import json; d=json.loads(open('/tmp/ab.json').read().strip().splitlines()[-1]); s=d['steady_state']; print('$arm', d['value'], d['roofline']['kernel_avg_us'], d['roofline']['frac'], 'alone', (d['roofline'].get('kernel_alone') or {}).get('kernel_avg_us'), '| steady', s['value'], s['kernel_avg_us'], s['frac'], '| fallbacks', d['roofline'].get('screen_fallbacks'), '/', d['roofline'].get('screened_blocks'))" >> "$OUT"
   done
 done
