@@ -127,13 +127,14 @@ def timed_steps(ix, k, steps, warmup, dist, cuda_sync, every=1, acct=None):
     every one the library did not already re-run is paid for with one exact search (RR_KERNEL_EXACT) before the
     closing sync. Multi-process: the ranks' counts are summed (a block flagged on any rank is re-run by all; the
     sum may over-pay, never under-pay) and every rank runs that many exact searches (their all-gathers pair up).
-    `acct` (dict, optional) receives {"flagged": F, "reruns_library": R, "reruns_paid": P, "blocks": B}.
+    `acct` (dict, optional) receives {"flagged": F, "reruns_library": R, "reruns_paid": P, "blocks": B,
+    "wide_slots": W} (W: query slots the verify proved in its wide phase, no re-run needed).
     Returns (wall seconds, fused-kernel event ms summed, fused launches timed)."""
     from rag_service_amd.dist import barrier, sum_over_ranks
     for _ in range(warmup):
         ix.search_staged(k)
     ix.synchronize()
-    b0, f0, r0 = ix.screen_counts()
+    b0, f0, r0, w0 = ix.screen_counts_all()
     ix.set_timing(True)
     ix.kernel_time(reset=True)
     barrier(dist)
@@ -144,7 +145,7 @@ def timed_steps(ix, k, steps, warmup, dist, cuda_sync, every=1, acct=None):
         if every > 1:
             ix.set_timing(i % every == 0)
         ix.search_staged(k)
-    b1, f1, r1 = ix.screen_counts()            # synchronises (and settles the last search)
+    b1, f1, r1, w1 = ix.screen_counts_all()    # synchronises (and settles the last search)
     owed = int(sum_over_ranks(dist, float(max(0, (f1 - f0) - (r1 - r0)))))
     if owed:
         ix.set_timing(False)
@@ -159,7 +160,8 @@ def timed_steps(ix, k, steps, warmup, dist, cuda_sync, every=1, acct=None):
     kern_ms, launches = ix.kernel_time(reset=True)
     ix.set_timing(False)
     if acct is not None:
-        acct.update({"blocks": b1 - b0, "flagged": f1 - f0, "reruns_library": r1 - r0, "reruns_paid": owed})
+        acct.update({"blocks": b1 - b0, "flagged": f1 - f0, "reruns_library": r1 - r0, "reruns_paid": owed,
+                     "wide_slots": w1 - w0})
     return elapsed, kern_ms, launches
 
 
@@ -498,6 +500,7 @@ def run(args, stage: dict) -> None:
                          "screen_fallbacks_timed": acct.get("flagged"),
                          "reruns_paid": acct.get("reruns_paid"),
                          "reruns_by_library_timed": acct.get("reruns_library"),
+                         "wide_verified_slots_timed": acct.get("wide_slots"),
                          "screen_fallbacks_steady": st_acct.get("flagged"),
                          "reruns_paid_steady": st_acct.get("reruns_paid"),
                          "fallback_note": "blocks whose bound could not prove the top-k inside the timed window; each "

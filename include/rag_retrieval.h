@@ -221,8 +221,16 @@ int rr_screen_stats(rr_handle* h, int64_t* blocks, int64_t* fallbacks);
 
 /* The same counters plus the exact re-runs the handle actually ran (a staged search whose results are never
  * fetched is superseded by the next one and is not re-run; benchmarks pay flagged - re-runs exact searches
- * themselves). Synchronises the handle's streams, which settles the last search. Any pointer may be null. */
-int rr_screen_counts(rr_handle* h, int64_t* blocks, int64_t* flagged, int64_t* reruns);
+ * themselves) and the query slots whose top-k the verify proved only in its wide phase (every screen-list entry
+ * above the largest single-list bound rescored: near-duplicate clusters). Synchronises the handle's streams, which
+ * settles the last search. Any pointer may be null. */
+int rr_screen_counts(rr_handle* h, int64_t* blocks, int64_t* flagged, int64_t* reruns, int64_t* wide_slots);
+
+/* The screen's adaptive state (fp32 storage): *full_lists = 1 once flagged blocks made the handle switch the screen's
+ * per-lane lists from 4 keys (+ a floor) to the full list width; *pause_left = search blocks still to run with the
+ * one-pass exact kernel because the screen could not prune this corpus (one process per world only); *pauses = how
+ * often that happened. Reset at every load. Any pointer may be null. */
+int rr_screen_state(rr_handle* h, int32_t* full_lists, int64_t* pause_left, int64_t* pauses);
 
 /* ---- multi-process deadline -------------------------------------------------------------------------- */
 

@@ -87,8 +87,10 @@ struct Shard {
   int q_cap = 0;
   uint64_t* cand = nullptr;              // 2 x [grid][64][32] per-workgroup candidates (the screened search
   int cand_grid = 0;                     // alternates the halves by parity; the other paths use half 0)
-  int* scount = nullptr;                 // screened search: blocks this shard flagged for the exact pass
-  int* pin_scount = nullptr;             // pinned host copy of scount, refreshed after each verify (no sync)
+  int* scount = nullptr;                 // screened search: [0] blocks this shard flagged for the exact pass,
+                                         // [1] blocks its verify completed
+  int* wcount = nullptr;                 // ... query slots its verify proved in the wide phase
+  int* pin_scount = nullptr;             // pinned host copy of scount[0..1], refreshed every 8th block (no sync)
   uint32_t* ctr = nullptr;               // split-K chunk counters (dynamic schedule), 0 between launches: one per
                                          // compute stream, kCtrStride words apart
   uint64_t* shard_keys = nullptr;        // [32][k_cap] this shard's top-k (all-gather send buffer)
@@ -203,6 +205,15 @@ struct rr_handle {
   // multi-process deadline (rr_set_timeout): host waits on device work poll against it; a miss fails the handle
   int timeout_ms = 120000;
   bool failed = false;
+  int wide_verify = 1;          // the verify's wide phase (A/B: RR_WIDE_VERIFY=0)
+  // adaptive screen (adapt_screen): the screen's per-lane lists grow from 4 keys to KT once blocks flag, and (one
+  // process per handle's world) screening pauses when even that leaves most blocks to the exact pass
+  bool full_lists = false;
+  bool full_lists_env = false;              // (A/B: RR_SCREEN_FULL_LISTS=1, full lists from every load)
+  int64_t win_blocks0 = 0, win_flag0 = 0;   // completed / flagged screened blocks when the current window began
+  bool win_wide = false;                    // screen_wide when it began (a switch starts a fresh window)
+  int64_t screen_pause = 0;                 // search blocks still to run without the screen
+  int64_t pauses = 0;                       // statistics: pauses so far (since the load)
 };
 
 namespace {
@@ -304,7 +315,7 @@ int dmalloc(T** p, size_t bytes) {
 
 int free_shard(Shard& s) {
   hipSetDevice(s.dev);
-  void* ptrs[] = {s.corpus, s.scr16, s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.ctr, s.shard_keys, s.gathered, s.out_base,
+  void* ptrs[] = {s.corpus, s.scr16, s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.wcount, s.ctr, s.shard_keys, s.gathered, s.out_base,
                   s.full_keys, s.sorted, s.sort_temp, s.wcand, s.wfloor, s.wsel};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -519,7 +530,7 @@ int drop_work_buffers(rr_handle* h) {
     s.last_x = -1;
     s.q_rd[0][0] = s.q_rd[0][1] = s.q_rd[1][0] = s.q_rd[1][1] = false;
     s.last_vsi = -1;
-    void** ptrs[] = {(void**)&s.qbuf[0], (void**)&s.qbuf[1], (void**)&s.cand, (void**)&s.scount, (void**)&s.ctr, (void**)&s.shard_keys, (void**)&s.gathered,
+    void** ptrs[] = {(void**)&s.qbuf[0], (void**)&s.qbuf[1], (void**)&s.cand, (void**)&s.scount, (void**)&s.wcount, (void**)&s.ctr, (void**)&s.shard_keys, (void**)&s.gathered,
                      (void**)&s.out_base, (void**)&s.full_keys, (void**)&s.sorted, &s.sort_temp,
                      (void**)&s.wcand, (void**)&s.wfloor, (void**)&s.wsel};
     for (void** p : ptrs) {
@@ -546,6 +557,10 @@ int drop_work_buffers(rr_handle* h) {
   h->screen_reruns = 0;
   h->narrow_blocks = h->narrow_reruns = 0;
   h->screen_wide = false;
+  h->full_lists = h->full_lists_env;
+  h->win_wide = false;
+  h->win_blocks0 = h->win_flag0 = 0;
+  h->screen_pause = h->pauses = 0;
   h->last_screened = false;
   h->last_settled = true;
   h->qpar = 0;
@@ -617,10 +632,12 @@ int ensure_buffers(rr_handle* h, int b, int k) {
     if (!s.cand) {
       s.cand_grid = s.cus;
       if (int rc = dmalloc(&s.cand, 2 * cand_half(s) * 8)) return rc;
-      if (int rc = dmalloc(&s.scount, sizeof(int))) return rc;
-      HIP_TRY(hipMemset(s.scount, 0, sizeof(int)));
-      if (!s.pin_scount) HIP_TRY(hipHostMalloc((void**)&s.pin_scount, sizeof(int), hipHostMallocDefault));
-      *(volatile int*)s.pin_scount = 0;
+      if (int rc = dmalloc(&s.scount, 2 * sizeof(int))) return rc;
+      HIP_TRY(hipMemset(s.scount, 0, 2 * sizeof(int)));
+      if (int rc = dmalloc(&s.wcount, sizeof(int))) return rc;
+      HIP_TRY(hipMemset(s.wcount, 0, sizeof(int)));
+      if (!s.pin_scount) HIP_TRY(hipHostMalloc((void**)&s.pin_scount, 2 * sizeof(int), hipHostMallocDefault));
+      ((volatile int*)s.pin_scount)[0] = ((volatile int*)s.pin_scount)[1] = 0;
       if (int rc = dmalloc(&s.ctr, 2 * kCtrStride * sizeof(uint32_t))) return rc;
       HIP_TRY(hipMemset(s.ctr, 0, 2 * kCtrStride * sizeof(uint32_t)));
     }
@@ -729,7 +746,58 @@ constexpr float kScreen16EpsB = 7.5e-8f;
 
 bool screened(const rr_handle* h, int k, int slots) {
   return (h->kernel == RR_KERNEL_AUTO || h->kernel == RR_KERNEL_SCREEN_FALLBACK) && h->dtype == RR_DTYPE_F32 &&
-         h->screen_ok && slots == rr::kQSlots && screen_kt(h, k) != 0 && use_sk(h);
+         h->screen_ok && slots == rr::kQSlots && screen_kt(h, k) != 0 && use_sk(h) &&
+         (h->screen_pause == 0 || h->kernel == RR_KERNEL_SCREEN_FALLBACK);
+}
+
+// Adaptive screen, at the start of every search, from the flagged-block counts the pinned copies last showed (a block
+// or two late; rr_api.cpp check_narrow reads the same). Windows of >= 32 screened blocks:
+//   * short per-lane lists (4 keys + the workgroup's floor, rr_sk.hip KL) -> full lists (KT keys) when more than 1
+//     in 8 blocks of the window flagged: crowded near-duplicates (a few lanes holding many of them) raise the floors
+//     above what the verify can prove; full lists have no floors. Rank-local (it changes no exchange);
+//   * full lists, and still more than 1 in 2 blocks flagged: the screen cannot prune this corpus (near-duplicate
+//     clusters stored together fill a few workgroups' lists), and each flagged block pays the screen AND the exact
+//     pass — pause screening for 1024 blocks (the one-pass exact kernel alone), then probe again. One process only:
+//     it changes the exchanged list width, which the ranks of a world must agree on. Not while this k still screens
+//     with the narrow 16-entry lists (screen_kt): check_narrow tries the 32-entry ones first.
+// Reset at every load.
+// Windows count blocks the device has COMPLETED (the verify's own count, copied with the flags): a burst of staged
+// searches is enqueued long before the counts of its first blocks reach the host.
+void device_counts(const rr_handle* h, int64_t* flagged, int64_t* done) {
+  *flagged = *done = 0;
+  for (const Shard& s : h->shards)
+    if (s.pin_scount) {
+      *flagged += ((volatile const int*)s.pin_scount)[0];
+      *done += ((volatile const int*)s.pin_scount)[1];
+    }
+}
+void adapt_screen(rr_handle* h, int k) {
+  if (h->screen_pause > 0) return;
+  int64_t flagged = 0, done = 0;
+  device_counts(h, &flagged, &done);
+  const int64_t nb = done - h->win_blocks0, nf = flagged - h->win_flag0;
+  if (h->win_wide != h->screen_wide) {   // the list width just changed (check_narrow): judge the new one afresh
+    h->win_wide = h->screen_wide;
+    h->win_blocks0 = done;
+    h->win_flag0 = flagged;
+    return;
+  }
+  if (nb < 32) return;
+  if (!h->full_lists) {
+    if (nf * 8 > nb) h->full_lists = true;
+  } else if (!h->dist && nf * 2 > nb && !narrow_lists(h, k)) {
+    h->screen_pause = 1024;
+    ++h->pauses;
+  }
+  h->win_blocks0 = done;
+  h->win_flag0 = flagged;
+}
+// After a search of `blocks` blocks: count down a pause; when it ends, the next window starts from here (a window
+// opened while blocks before the pause are still being counted only sees them late: harmless, it flags anyway).
+void pause_tick(rr_handle* h, int blocks) {
+  if (h->screen_pause <= 0) return;
+  h->screen_pause = std::max<int64_t>(0, h->screen_pause - blocks);
+  if (h->screen_pause == 0) device_counts(h, &h->win_flag0, &h->win_blocks0);
 }
 
 // Large k (32 < k <= kWideMax): split-K kernel with wide per-workgroup lists, radix select, completeness check
@@ -1004,6 +1072,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         a.sqrt_d = sqrtf((float)d) * (1.0f + 0x1p-20f);
         // the f16 copy holds exactly the values the fp32-reading screen rounds to: half the bytes
         const bool s16 = s.scr16 && h->screen_copy && rr::sk_slabs(rr::KDT_SCREEN16, d);
+        a.full_lists = h->full_lists ? 1 : 0;
         a.eps_a = s16 ? kScreen16EpsA : kScreenEpsA;
         a.eps_b = s16 ? kScreen16EpsB : kScreenEpsB;
         if (s16) a.corpus = (const char*)s.scr16;
@@ -1028,6 +1097,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         v.count = s.scount;
         v.seq = seq;
         v.force_incomplete = h->kernel == RR_KERNEL_SCREEN_FALLBACK;
+        v.wide_verify = h->wide_verify;
+        v.wide_count = s.wcount;
         HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 1, rr::kQSlots, rr::kQSlots, v, vs));
       } else {   // a shard without rows contributes empty lists and no flag
         HIP_TRY(hipMemsetAsync(s.px_keys[x], 0, ((size_t)slots * kt + 1) * 8, vs));
@@ -1044,7 +1115,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       if (s.rows() > 0 && (h->screen_blocks & 7) == 0) {
         HIP_TRY(hipEventRecord(s.ev_scr[0], vs));
         HIP_TRY(hipStreamWaitEvent(s.xstream, s.ev_scr[0], 0));
-        HIP_TRY(hipMemcpyAsync(s.pin_scount, s.scount, sizeof(int), hipMemcpyDeviceToHost, s.xstream));
+        HIP_TRY(hipMemcpyAsync(s.pin_scount, s.scount, 2 * sizeof(int), hipMemcpyDeviceToHost, s.xstream));
       }
     } else if (kt) {
       int grid = fused_grid(s);
@@ -1326,6 +1397,8 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   if (const char* e = getenv("RR_X_SLOTS")) h->xslots = std::min(kXSlots, std::max(2, atoi(e)));     // (A/B)
   if (const char* e = getenv("RR_X_EXCHANGE_DELAY_US")) h->x_delay_us = std::min(1000, std::max(0, atoi(e)));
   if (const char* e = getenv("RR_DIST_TIMEOUT_MS")) h->timeout_ms = std::max(0, atoi(e));
+  if (const char* e = getenv("RR_WIDE_VERIFY")) h->wide_verify = atoi(e) ? 1 : 0;   // (A/B)
+  if (const char* e = getenv("RR_SCREEN_FULL_LISTS")) h->full_lists_env = atoi(e) != 0;   // (A/B: start with full lists)
   *out = h;
   return RR_OK;
 }
@@ -1566,17 +1639,28 @@ int rr_search_staged(rr_handle* h, int32_t k) {
   if (int rc = ensure_buffers(h, b, k)) return rc;
   const int slots = block_slots(h, b, k);
   check_narrow(h);
+  adapt_screen(h, k);
   h->last_screened = checked(h, k, slots);
   h->last_narrow = screened(h, k, slots) && narrow_lists(h, k);
   h->last_seq0 = h->screen_seq + 1;
   h->last_settled = !h->last_screened;
   h->last_qpar = h->qpar;
+  const bool paused = h->screen_pause > 0 && h->kernel == RR_KERNEL_AUTO;
   for (int q0 = 0; q0 < b; q0 += slots) {
     const int bb = std::min(slots, b - q0);
     if (int rc = enqueue_block(h, q0, bb, k, slots)) return rc;
   }
+  if (paused) pause_tick(h, (b + slots - 1) / slots);
   h->last_k = k;
   h->last_b = b;
+  return RR_OK;
+}
+
+int rr_screen_state(rr_handle* h, int32_t* full_lists, int64_t* pause_left, int64_t* pauses) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  if (full_lists) *full_lists = h->full_lists ? 1 : 0;
+  if (pause_left) *pause_left = h->screen_pause;
+  if (pauses) *pauses = h->pauses;
   return RR_OK;
 }
 
@@ -1798,26 +1882,35 @@ int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx) {
   return collect_timing(h);
 }
 
-int rr_screen_counts(rr_handle* h, int64_t* blocks, int64_t* flagged, int64_t* reruns) {
+int rr_screen_counts(rr_handle* h, int64_t* blocks, int64_t* flagged, int64_t* reruns, int64_t* wide_slots) {
   if (!h) return fail(RR_E_INVALID, "null handle");
   if (h->failed) return failed_handle();
   if (int rc = rr_synchronize(h)) return rc;
-  int64_t fb = 0;
+  int64_t fb = 0, ws = 0;
   for (Shard& s : h->shards) {
     if (!s.scount) continue;
     HIP_TRY(hipSetDevice(s.dev));
+    int wv = 0;
     HIP_TRY(hipMemcpyAsync(s.pin_scount, s.scount, sizeof(int), hipMemcpyDeviceToHost, s.stream));
     if (int rc = wait_stream(h, s.stream, "the flagged-block count")) return rc;
     fb += *(volatile int*)s.pin_scount;
+    HIP_TRY(hipMemcpyAsync(s.pin_scount, s.wcount, sizeof(int), hipMemcpyDeviceToHost, s.stream));
+    if (int rc = wait_stream(h, s.stream, "the wide-verify count")) return rc;
+    wv = *(volatile int*)s.pin_scount;
+    ws += wv;
+    // pin_scount is the counts' host copy (check_narrow, adapt_screen read it): restore it
+    HIP_TRY(hipMemcpyAsync(s.pin_scount, s.scount, 2 * sizeof(int), hipMemcpyDeviceToHost, s.stream));
+    if (int rc = wait_stream(h, s.stream, "the flagged-block count")) return rc;
   }
   if (blocks) *blocks = h->screen_blocks * (int64_t)h->shards.size();
   if (flagged) *flagged = fb;
   if (reruns) *reruns = h->screen_reruns;
+  if (wide_slots) *wide_slots = ws;
   return RR_OK;
 }
 
 int rr_screen_stats(rr_handle* h, int64_t* blocks, int64_t* fallbacks) {
-  return rr_screen_counts(h, blocks, fallbacks, nullptr);
+  return rr_screen_counts(h, blocks, fallbacks, nullptr, nullptr);
 }
 
 int rr_set_timeout(rr_handle* h, int32_t ms) {

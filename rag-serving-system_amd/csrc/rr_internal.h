@@ -61,6 +61,7 @@ struct SkArgs {
   int dyn;                 // MODE 0: 1 = dynamic chunk schedule (ctr), 0 = static (chunks g, g + grid, ...)
   // screen (KDT_SCREEN): upper bound u = s~ + eps_a |x||q| + eps_b (sqrt_d |x| + sum|q|)
   float eps_a, eps_b, sqrt_d;
+  int full_lists;          // screen: per-lane lists of KT keys (else 4, with a floor; rr_sk.hip KL)
   // MODE 1 (verify, one workgroup per query slot)
   const uint64_t* vin;     // [nlists][slots][KT] screen keys
   int nlists, k_out;
@@ -68,9 +69,12 @@ struct SkArgs {
   int64_t* out_idx;        // [b][k_out]
   uint64_t* out_keys;      // [slots][KT] exact keys (may be null)
   uint64_t* flag;          // MODE 1: raised (atomic max) to seq when the block needs the exact pass
-  int* count;              // MODE 1: blocks flagged so far (statistics)
+  int* count;              // MODE 1: [0] blocks flagged so far, [1] blocks verified (slot 0 counts; statistics)
   int seq;                 // this search block's sequence number (> every earlier one)
   int force_incomplete;    // MODE 1 test hook: report the block incomplete
+  int wide_verify;         // MODE 1: when the KT candidates cannot prove the top-k, try the wide phase (rescore every
+                           // list entry above the largest single-list bound) before raising the flag
+  int* wide_count;         // MODE 1: query slots the wide phase proved (statistics; may be null)
   // MODE 0, KT 32, 32 slots, large k (32 < wide_k <= 256): out is [grid][slots][wide_k] — per query the
   // workgroup's top-wide_k of its lane lists — and floors [grid][slots]: no key it dropped is above the floor
   int wide_k;

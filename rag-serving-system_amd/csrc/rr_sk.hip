@@ -75,11 +75,27 @@ __device__ unsigned long long probe[4096 * 8];
   do {              \
   } while (0)
 #endif
+// Verify diagnostics (A/B builds with -DRR_VERIFY_DIAG only): per query slot of the last verify launch, [the k-th
+// largest bound, the largest single-list bound, phase-1 exact k-th, phase-2 exact k-th, |R|, decision, complete]
+#ifdef RR_VERIFY_DIAG
+__device__ unsigned long long vdiag[32 * 8];
+#define VDIAG(i, v)                                        \
+  do {                                                     \
+    vdiag[vq * 8 + (i)] = (unsigned long long)(v);         \
+  } while (0)
+#else
+#define VDIAG(i, v) \
+  do {              \
+  } while (0)
+#endif
 
 constexpr int kSlabRowBytes = 128;                // contiguous bytes of one row per slab
 constexpr int kSlabBytes = 32 * kSlabRowBytes;    // 4 KiB
 constexpr int kRedStride = 36;                    // floats allocated per (wave, query) block of 32 rows
 constexpr int kRedRow = 32;                       // ... of which the XOR-swizzled partial sums use 32
+// MODE 1 wide verify: its candidate rows R (int32 local rows) in the slab ring after the list-merge scratch
+constexpr int kWideListOff = 16384;
+constexpr int kWideCap = (2 * 8 * kSlabBytes - kWideListOff) / 4;   // ring_bytes(2) - the offset, in rows
 
 // Ring of RS slab slots per wave: RS - 1 slabs stay in flight while one is multiplied. With RS = 2 the
 // K-partial block is double-buffered (one barrier per tile); with RS = 3 (2 x 32 KiB more ring) it is
@@ -225,27 +241,31 @@ __device__ __forceinline__ int slab_off(int r, int cp) { return (r >> 3) * 1024 
 // [kThreads] heads, [KT * KT] candidates, H, count, floor maximum.
 template <int KT>
 __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict__ in, int nlists, int qslots, int q,
-                                                      uint64_t* scratch, uint64_t* akeys, uint64_t* floor_out) {
+                                                      uint64_t* scratch, uint64_t* akeys, uint64_t* floor_out,
+                                                      uint64_t* tail_out) {
   const int tid = threadIdx.x;
   uint64_t* heads = scratch;
   uint64_t* cand = scratch + kThreads;
   uint64_t* hs = cand + KT * KT;
   int* cnt = (int*)(hs + 1);
   unsigned long long* fmax = (unsigned long long*)(hs + 2);
+  unsigned long long* tmax = (unsigned long long*)(hs + 3);
   constexpr int LS = KT + 1;   // list stride: KT keys + the workgroup's floor
   TopK<KT> tk;
-  uint64_t fl = 0;
+  uint64_t fl = 0, tl = 0;     // floors; and every list's own bound, max(its KT-th key, its floor) (wide verify)
   if (tid < nlists) {
     const uint64_t* src = in + ((size_t)q * nlists + tid) * LS;   // query-major screen lists
 #pragma unroll
     for (int i = 0; i < KT; ++i) tk.v[i] = src[i];
     fl = src[KT];
+    tl = umax64(fl, tk.v[KT - 1]);
   } else {
     tk.init();
   }
   for (int l = tid + kThreads; l < nlists; l += kThreads) {   // lists beyond kThreads folded in (sorted input)
     const uint64_t* src = in + ((size_t)q * nlists + l) * LS;
     fl = umax64(fl, src[KT]);
+    tl = umax64(tl, umax64(src[KT], src[KT - 1]));
     for (int i = 0; i < KT; ++i) {
       const uint64_t key = src[i];
       if (key <= tk.last()) break;
@@ -257,10 +277,12 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
     hs[0] = 0;
     cnt[0] = 0;
     *fmax = 0;
+    *tmax = 0;
   }
   if (tid < nl) heads[tid] = tk.v[0];
   __syncthreads();
   if (fl != 0) __hip_atomic_fetch_max(fmax, (unsigned long long)fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (tl != 0) __hip_atomic_fetch_max(tmax, (unsigned long long)tl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (tid < nl && tk.v[0] != 0) {
     const uint64_t me = tk.v[0];
     int rank = 0;
@@ -268,7 +290,10 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
     if (rank == KT - 1) hs[0] = me;
   }
   __syncthreads();
-  if (tid == 0) *floor_out = *fmax;
+  if (tid == 0) {
+    *floor_out = *fmax;
+    *tail_out = *tmax;
+  }
   const uint64_t th = hs[0];
   if (tid < nl && tk.v[0] != 0 && tk.v[0] >= th) {
     int c = 0;
@@ -295,7 +320,7 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
 // them all; each A fragment then feeds the MFMAs of both halves).
 // MODE 0: top-KT per query over this workgroup's rows (DT 6: by upper bound).
 // MODE 1: verify (DT 3, QH 1): block q = query slot q; see "Screened search" above.
-template <int DT, int NS, int KT, bool COS, int RS, int QH, int MODE, int SCHED>
+template <int DT, int NS, int KT, bool COS, int RS, int QH, int MODE, int SCHED, int FL>
 __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const SkArgs a) {
   static_assert(RS == 2, "two slab slots per wave: one in flight while one is multiplied (the waits assume it)");
   static_assert(QH == 1 || QH == 2, "32 or 64 query slots");
@@ -322,7 +347,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // a key only below its own last entry. The workgroup reports the largest last entry of its full lanes as its FLOOR
   // (no key missing from its list is above max(the list's KT-th key, the floor)); the verify adds the floors to its
   // completeness bound. The branch-free insert, the epilogue's largest VALU item, then costs KL compare-selects.
-  constexpr int KL = SCR && KT > 4 ? 4 : KT;
+  // (FL = 1: full lists, KL = KT — the handle switches to them when the short lists' floors stop the verify's
+  // proofs, e.g. near-duplicate clusters whose copies crowd a few lanes; rr_api.cpp adapt_screen)
+  constexpr int KL = SCR && KT > 4 && !FL ? 4 : KT;
   constexpr int EB = DT == 1 || DT == 7 ? 2 : 4;                // storage bytes per element
   const int row_bytes = d * EB;
   constexpr int KS = NS * kSlabRowBytes;                        // bytes of a row per wave
@@ -346,6 +373,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   int* gvalid = (int*)(gnorm + 32);
   uint64_t* xk = (uint64_t*)(gvalid + 32);
   uint64_t* vfloor = xk + KT;   // MODE 1: the largest floor of the screen's lists (see KL)
+  uint64_t* vtail = vfloor + 1; // MODE 1: the largest bound of any single list, max(KT-th key, floor) (wide verify)
+  int* vstate = (int*)(vtail + 1);   // MODE 1: [0] what the leader decided after the first check, [1] |R|
   // MODE 1 reads its 32 gathered rows straight into registers (all loads issued at once: one latency), the
   // exact fragments the LDS image would give: lane (r, h) takes 16-byte units 4(i>>1) + 2h + (i&1) of slab j
   f32x4 vrow[MODE == 1 ? NS : 1][4];
@@ -679,9 +708,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // ---- MODE 1: this query's candidates (the queries' fragments and scalars above are already built, so
   // their loads overlapped the list loads), then their rows straight into registers ---------------------------
   if constexpr (MODE == 1) {
-    static_assert((size_t)(kThreads + KT * KT + 3) * 8 <= ring_bytes(RS), "verify merge scratch in the slab ring");
+    static_assert((size_t)(kThreads + KT * KT + 4) * 8 <= kWideListOff, "verify merge scratch in the slab ring");
     SK_PROBE(6);
-    merge_lists_for_query<KT>(a.vin, a.nlists, QS, vq, (uint64_t*)smem, akeys, vfloor);
+    merge_lists_for_query<KT>(a.vin, a.nlists, QS, vq, (uint64_t*)smem, akeys, vfloor, vtail);
     SK_PROBE(7);
     if (tid < 32) {
       const uint64_t k0 = akeys[0];
@@ -1056,41 +1085,183 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       if (m != 0 && tk.v[0] == m) tk.pop();
       if (lane % LPQ == 0) dst[rnd] = m;
     }
-  } else {
-    if (w != vq / 4) return;   // the wave that owns query slot vq (QH 1: queries 4w..4w+3)
+  } else if constexpr (MODE == 1) {
+    // The wave that owns query slot vq (QH 1: queries 4w..4w+3) merges its lanes' lists into xk; its leader lane
+    // checks completeness and writes the results. Every wave stays: a second, wide phase may follow.
+    const bool owner = w == vq / 4;
+    const bool leader = owner && qe == vq && lane % LPQ == 0;
+    auto lane_merge = [&]() {
+      if (owner) {
 #pragma unroll 1
-    for (int rnd = 0; rnd < KT; ++rnd) {
-      const uint64_t m = group_max_u64<LPQ>(tk.v[0]);
-      if (m != 0 && tk.v[0] == m) tk.pop();
-      if (qe == vq && lane % LPQ == 0) xk[rnd] = m;
-    }
-    if (qe != vq || lane % LPQ != 0) return;
-    // leader of query slot vq: completeness, then the results. Every key not rescored is at most the KT-th
-    // candidate's bound or a workgroup's floor (0, 0: fewer than KT docs here and nothing dropped)
-    const uint64_t ukt = umax64(akeys[KT - 1], *vfloor);
-    const uint64_t ek = xk[a.k_out - 1];         // the exact k-th key
-    bool complete = ukt == 0 || (ek != 0 && (uint32_t)(ek >> 32) > (uint32_t)(ukt >> 32));
-    complete = complete && qinfo[QS + vq] < 32768.0f && !a.force_incomplete;   // f16 range of the screen
-    if (!complete) {   // the first query slot to flag the block also counts it
-      if (__hip_atomic_fetch_max(a.flag, (uint64_t)a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-          (uint64_t)a.seq)
-        __hip_atomic_fetch_add(a.count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (a.out_keys)
-      for (int i = 0; i < KT; ++i) a.out_keys[(size_t)vq * KT + i] = xk[i];
-    if (a.out_scores)
-      for (int i = 0; i < a.k_out; ++i) {
-        const uint64_t key = xk[i];
-        a.out_scores[(size_t)vq * a.k_out + i] = key ? float_of_ord((uint32_t)(key >> 32)) : -INFINITY;
-        a.out_idx[(size_t)vq * a.k_out + i] = key ? (int64_t)(0xFFFFFFFFu - (uint32_t)key) : -1;
+        for (int rnd = 0; rnd < KT; ++rnd) {
+          const uint64_t m = group_max_u64<LPQ>(tk.v[0]);
+          if (m != 0 && tk.v[0] == m) tk.pop();
+          if (qe == vq && lane % LPQ == 0) xk[rnd] = m;
+        }
       }
+    };
+    // the leader's verdict and the results (xk); an incomplete block raises the flag word (the host re-runs it)
+    auto finish = [&](bool complete) {
+      complete = complete && qinfo[QS + vq] < 32768.0f && !a.force_incomplete;   // f16 range of the screen
+      if (!complete) {   // the first query slot to flag the block also counts it
+        if (__hip_atomic_fetch_max(a.flag, (uint64_t)a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+            (uint64_t)a.seq)
+          __hip_atomic_fetch_add(a.count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (vq == 0) __hip_atomic_fetch_add(a.count + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // done
+      if (a.out_keys)
+        for (int i = 0; i < KT; ++i) a.out_keys[(size_t)vq * KT + i] = xk[i];
+      if (a.out_scores)
+        for (int i = 0; i < a.k_out; ++i) {
+          const uint64_t key = xk[i];
+          a.out_scores[(size_t)vq * a.k_out + i] = key ? float_of_ord((uint32_t)(key >> 32)) : -INFINITY;
+          a.out_idx[(size_t)vq * a.k_out + i] = key ? (int64_t)(0xFFFFFFFFu - (uint32_t)key) : -1;
+        }
+    };
+    lane_merge();
+    if (leader) {
+      // Every key not rescored is at most the KT-th candidate's bound or a workgroup's floor (0, 0: fewer than KT
+      // docs here and nothing dropped).
+      const uint64_t ukt = umax64(akeys[KT - 1], *vfloor);
+      const uint64_t ek = xk[a.k_out - 1];         // the exact k-th key
+      const bool complete = ukt == 0 || (ek != 0 && (uint32_t)(ek >> 32) > (uint32_t)(ukt >> 32));
+      // Not proven: the wide phase can still prove it when the k-th largest bound of all lies above the largest
+      // bound of any single list (vtail): every key left out of every list is below that.
+      const uint64_t tb = *vtail;
+      const bool wide = !complete && a.wide_verify && !a.force_incomplete && qinfo[QS + vq] < 32768.0f &&
+                        (uint32_t)(akeys[a.k_out - 1] >> 32) > (uint32_t)(tb >> 32);
+      vstate[0] = wide ? 1 : 0;
+      VDIAG(0, akeys[a.k_out - 1]);
+      VDIAG(1, tb);
+      VDIAG(2, ek);
+      VDIAG(3, 0);
+      VDIAG(4, 0);
+      VDIAG(5, complete ? 0 : wide ? 1 : 2);
+      VDIAG(6, complete);
+      if (!wide) finish(complete);
+    }
+    __syncthreads();
+    if (vstate[0] != 1) return;
+
+    // ---- wide phase: R = every list entry whose bound is above vtail (the rest: exact <= bound <= vtail), rescored
+    // with exactly the arithmetic of the first tile (same K split, MFMA order, wave order, epilogue), 32 rows a
+    // tile; complete when the exact k-th key is above vtail. Lists are disjoint (each workgroup its own rows).
+    int* wl = (int*)(smem + kWideListOff);
+    const uint32_t tb_ord = (uint32_t)(*vtail >> 32);
+    if (tid == 0) vstate[1] = 0;
+    __syncthreads();
+    for (int l = tid; l < a.nlists; l += kThreads) {
+      const uint64_t* src = a.vin + ((size_t)vq * a.nlists + l) * (KT + 1);
+      int c = 0;
+      while (c < KT && (uint32_t)(src[c] >> 32) > tb_ord) ++c;   // a prefix of the sorted list
+      if (c) {
+        const int pos = atomicAdd(&vstate[1], c);
+        for (int i = 0; i < c; ++i)
+          if (pos + i < kWideCap) wl[pos + i] = (int)((int64_t)(0xFFFFFFFFu - (uint32_t)src[i]) - idx_base);
+      }
+    }
+    __syncthreads();
+    const int nr = vstate[1];
+    if (nr > kWideCap) {   // (cannot happen while lists x KT <= kWideCap; kept as a guard)
+      if (leader) finish(false);
+      return;
+    }
+    tk.init();
+    const int ntiles = (nr + 31) / 32;
+    for (int t = 0; t < ntiles; ++t) {
+      // this lane's MFMA row (r) and its epilogue rows (er + e)
+      const int ri = 32 * t + r;
+      const char* src = corpus + (int64_t)wl[ri < nr ? ri : 0] * row_bytes + (size_t)w * KS;
+#pragma unroll
+      for (int j = 0; j < NS; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          vrow[j][i] = *(const f32x4*)(src + j * kSlabRowBytes + ((4 * (i >> 1) + 2 * h + (i & 1)) << 4));
+      int erow[DPL];
+      float end[DPL];
+#pragma unroll
+      for (int e = 0; e < DPL; ++e) {
+        const int ei = 32 * t + er + e;
+        erow[e] = ei < nr ? wl[ei] : -1;
+        end[e] = COS ? norms[erow[e] >= 0 ? erow[e] : 0] : 1.f;
+      }
+      f32x16 acc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          const f32x4 v0 = vrow[j][2 * tt], v1 = vrow[j][2 * tt + 1];
+          const float x[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+          bf16x8 b0, b1, b2;
+          split3(x, b0, b1, b2);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[0].c0[j][tt], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[0].c1[j][tt], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qfs[0].c0[j][tt], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qfs[0].c1[j][tt], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[0].c2[j][tt], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, qfs[0].c0[j][tt], acc, 0, 0, 0);
+        }
+      }
+      // K-partials through LDS in the fixed wave order (the first tile used buffer 0: alternate from 1)
+      float* rb = red + (size_t)((t + 1) & 1) * kWaves * QS * kRedStride;
+#pragma unroll
+      for (int a4 = 0; a4 < 4; ++a4) {
+        const f32x4 v = {acc[4 * a4], acc[4 * a4 + 1], acc[4 * a4 + 2], acc[4 * a4 + 3]};
+        *(f32x4*)(rb + (w * QS + r) * kRedRow + 4 * ((2 * a4 + h) ^ (r & 7))) = v;
+      }
+      lds_barrier();
+      float sv[DPL];
+#pragma unroll
+      for (int ww = 0; ww < kWaves; ++ww) {
+        const float2 p = *(const float2*)(rb + (ww * QS + qe) * kRedRow + 4 * ((er >> 2) ^ (qe & 7)) + (er & 3));
+        sv[0] = ww ? sv[0] + p.x : p.x;
+        sv[1] = ww ? sv[1] + p.y : p.y;
+      }
+      const uint64_t bar = group_max_u64<LPQ>(tk.last());
+      float thr = -INFINITY;
+      if constexpr (COS) {
+        if (bar != 0) {
+          const float tt = float_of_ord((uint32_t)(bar >> 32));
+          thr = tt - fabsf(tt) * 0x1p-20f - 0x1p-100f;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < DPL; ++e) {
+        const bool valid = qev && erow[e] >= 0;
+        const float s = sv[e];
+        if constexpr (COS) {
+          const float den = cos_den(qn, end[e]);
+          if (valid && s * __builtin_amdgcn_rcpf(den) >= thr) {
+            float c = s / den;   // IEEE division, as the first tile and the full pass
+            c = fminf(fmaxf(c, -1.0f), 1.0f);
+            const uint64_t key = make_key(c, idx_base + (uint32_t)erow[e]);
+            if (key > bar) tk.insert(key);
+          }
+        } else {
+          const uint64_t key = make_key(s, idx_base + (uint32_t)erow[e]);
+          if (valid && key > bar) tk.insert(key);
+        }
+      }
+    }
+    lane_merge();
+    if (leader) {
+      const uint64_t ek = xk[a.k_out - 1];
+      const bool complete = tb_ord == 0 || (ek != 0 && (uint32_t)(ek >> 32) > tb_ord);
+      VDIAG(3, ek);
+      VDIAG(4, nr);
+      VDIAG(6, complete);
+      if (complete && a.wide_count) __hip_atomic_fetch_add(a.wide_count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      finish(complete);
+    }
   }
   SK_PROBE(5);
 }
 
-template <int DT, int NS, int KT, bool COS, int RS, int QH, int MODE, int SCHED>
+template <int DT, int NS, int KT, bool COS, int RS, int QH, int MODE, int SCHED, int FL>
 hipError_t launch_t(int grid, const SkArgs& a, hipStream_t s) {
-  auto kern = sk_score_kernel<DT, NS, KT, COS, RS, QH, MODE, SCHED>;
+  auto kern = sk_score_kernel<DT, NS, KT, COS, RS, QH, MODE, SCHED, FL>;
   static bool attr_set = false;   // the dynamic-LDS ceiling is a per-function attribute: set it once
   const size_t lds = sk_lds_bytes(DT, COS, RS, 32 * QH);
   if (!attr_set) {
@@ -1102,37 +1273,37 @@ hipError_t launch_t(int grid, const SkArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int DT, int NS, bool COS, int RS, int QH, int MODE, int SCHED>
+template <int DT, int NS, bool COS, int RS, int QH, int MODE, int SCHED, int FL>
 hipError_t launch_kt(int kt, int grid, const SkArgs& a, hipStream_t s) {
   switch (kt) {
-    case 4: return launch_t<DT, NS, 4, COS, RS, QH, MODE, SCHED>(grid, a, s);
-    case 8: return launch_t<DT, NS, 8, COS, RS, QH, MODE, SCHED>(grid, a, s);
-    case 16: return launch_t<DT, NS, 16, COS, RS, QH, MODE, SCHED>(grid, a, s);
+    case 4: return launch_t<DT, NS, 4, COS, RS, QH, MODE, SCHED, FL>(grid, a, s);
+    case 8: return launch_t<DT, NS, 8, COS, RS, QH, MODE, SCHED, FL>(grid, a, s);
+    case 16: return launch_t<DT, NS, 16, COS, RS, QH, MODE, SCHED, FL>(grid, a, s);
     // 64 slots x KT 32 spills (served as two 32-slot passes); the 9-wave form's register budget (168) does not
     // hold KT 32 lists
-    case 32: if constexpr (QH == 1 && SCHED == 0) return launch_t<DT, NS, 32, COS, RS, QH, MODE, 0>(grid, a, s);
+    case 32: if constexpr (QH == 1 && SCHED == 0) return launch_t<DT, NS, 32, COS, RS, QH, MODE, 0, FL>(grid, a, s);
              else return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }
 
-template <int DT, bool COS, int RS, int QH, int MODE, int SCHED>
+template <int DT, bool COS, int RS, int QH, int MODE, int SCHED, int FL>
 hipError_t launch_ns(int ns, int kt, int grid, const SkArgs& a, hipStream_t s) {
   switch (ns) {
-    case 1: return launch_kt<DT, 1, COS, RS, QH, MODE, SCHED>(kt, grid, a, s);
-    case 2: return launch_kt<DT, 2, COS, RS, QH, MODE, SCHED>(kt, grid, a, s);
-    case 3: if constexpr (DT != 1 && DT != 7) return launch_kt<DT, 3, COS, RS, QH, MODE, SCHED>(kt, grid, a, s);
+    case 1: return launch_kt<DT, 1, COS, RS, QH, MODE, SCHED, FL>(kt, grid, a, s);
+    case 2: return launch_kt<DT, 2, COS, RS, QH, MODE, SCHED, FL>(kt, grid, a, s);
+    case 3: if constexpr (DT != 1 && DT != 7) return launch_kt<DT, 3, COS, RS, QH, MODE, SCHED, FL>(kt, grid, a, s);
             else return hipErrorInvalidValue;
-    case 4: if constexpr (DT != 1 && DT != 7) return launch_kt<DT, 4, COS, RS, QH, MODE, SCHED>(kt, grid, a, s);
+    case 4: if constexpr (DT != 1 && DT != 7) return launch_kt<DT, 4, COS, RS, QH, MODE, SCHED, FL>(kt, grid, a, s);
             else return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }
 
-template <int DT, int RS, int QH, int MODE = 0, int SCHED = 0>
+template <int DT, int RS, int QH, int MODE = 0, int SCHED = 0, int FL = 0>
 hipError_t launch_metric(int metric, int ns, int kt, int grid, const SkArgs& a, hipStream_t s) {
-  return metric ? launch_ns<DT, true, RS, QH, MODE, SCHED>(ns, kt, grid, a, s)
-                : launch_ns<DT, false, RS, QH, MODE, SCHED>(ns, kt, grid, a, s);
+  return metric ? launch_ns<DT, true, RS, QH, MODE, SCHED, FL>(ns, kt, grid, a, s)
+                : launch_ns<DT, false, RS, QH, MODE, SCHED, FL>(ns, kt, grid, a, s);
 }
 
 }  // namespace sk
@@ -1141,8 +1312,8 @@ size_t sk_lds_bytes(int sdt, bool cos, int ring, int qslots) {
   (void)sdt;
   (void)cos;
   // + per-row factors [3][2][32], next-chunk words [4], query scalars [3][qslots], MODE 1 scratch: W [8][32] +
-  // akeys [32] keys, grow / gnorm / gvalid [32], xk [32] keys, the floors' maximum
-  const size_t verify = (size_t)(kWaves * 32 + 32 + 32 + 1) * 8 + 3 * 32 * 4;
+  // akeys [32] keys, grow / gnorm / gvalid [32], xk [32] keys, the floors' and the list bounds' maxima, 2 ints
+  const size_t verify = (size_t)(kWaves * 32 + 32 + 32 + 3) * 8 + 3 * 32 * 4;
   return sk::ring_bytes(ring) + sk::red_bytes(ring, qslots / 32) + 3 * 64 * 4 + 4 * 4 + 3 * qslots * 4 + verify;
 }
 
@@ -1164,16 +1335,26 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
     if (sdt != KDT_F32_X3 || qslots != 32 || ring != 2 || grid != 32) return hipErrorInvalidValue;
     return sk::launch_metric<3, 2, 1, 1>(metric, ns, kt, grid, a, s);
   }
-  if (sdt == KDT_SCREEN) {   // dynamic schedule (9-wave form) when asked for and the lists fit its registers
+  // the screen: dynamic schedule (9-wave form) when asked for and the lists fit its registers; short or full
+  // per-lane lists (a.full_lists)
+  if (sdt == KDT_SCREEN) {
     if (qslots != 32 || ring != 2) return hipErrorInvalidValue;
-    if (a.dyn && a.ctr && kt <= 16) return sk::launch_metric<6, 2, 1, 0, 1>(metric, ns, kt, grid, a, s);
-    return sk::launch_metric<6, 2, 1>(metric, ns, kt, grid, a, s);
+    const bool dyn = a.dyn && a.ctr && kt <= 16;
+    if (a.full_lists)
+      return dyn ? sk::launch_metric<6, 2, 1, 0, 1, 1>(metric, ns, kt, grid, a, s)
+                 : sk::launch_metric<6, 2, 1, 0, 0, 1>(metric, ns, kt, grid, a, s);
+    return dyn ? sk::launch_metric<6, 2, 1, 0, 1>(metric, ns, kt, grid, a, s)
+               : sk::launch_metric<6, 2, 1>(metric, ns, kt, grid, a, s);
   }
   if (sdt == KDT_SCREEN16) {   // the screen over the f16 copy (a.corpus = that copy)
     const int ns16 = sk_slabs(KDT_SCREEN16, a.d);
     if (qslots != 32 || ring != 2 || !ns16) return hipErrorInvalidValue;
-    if (a.dyn && a.ctr && kt <= 16) return sk::launch_metric<7, 2, 1, 0, 1>(metric, ns16, kt, grid, a, s);
-    return sk::launch_metric<7, 2, 1>(metric, ns16, kt, grid, a, s);
+    const bool dyn = a.dyn && a.ctr && kt <= 16;
+    if (a.full_lists)
+      return dyn ? sk::launch_metric<7, 2, 1, 0, 1, 1>(metric, ns16, kt, grid, a, s)
+                 : sk::launch_metric<7, 2, 1, 0, 0, 1>(metric, ns16, kt, grid, a, s);
+    return dyn ? sk::launch_metric<7, 2, 1, 0, 1>(metric, ns16, kt, grid, a, s)
+               : sk::launch_metric<7, 2, 1>(metric, ns16, kt, grid, a, s);
   }
   if (qslots == 64) {   // one corpus pass for up to 64 queries: bf16 and fp32-split storage, ring 2
     if (ring != 2) return hipErrorInvalidValue;
@@ -1215,3 +1396,9 @@ hipError_t launch_sk(int sdt, int metric, int kt, int grid, const void* c, const
 }
 
 }  // namespace rr
+
+#ifdef RR_VERIFY_DIAG
+extern "C" int rr_debug_verify(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(rr::sk::vdiag), sizeof(unsigned long long) * 32 * 8);
+}
+#endif

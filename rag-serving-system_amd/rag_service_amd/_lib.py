@@ -81,8 +81,9 @@ SIGNATURES = {
     "rr_set_compute_streams": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_i32)]),
     "rr_last_shape": (_c_int, [_vp, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32)]),
     "rr_dist_info": (_c_int, [_vp, _ip, _ip]),
-    "rr_screen_counts": (_c_int, [_vp, _i64p, _i64p, _i64p]),
+    "rr_screen_counts": (_c_int, [_vp, _i64p, _i64p, _i64p, _i64p]),
     "rr_set_timeout": (_c_int, [_vp, _c_i32]),
+    "rr_screen_state": (_c_int, [_vp, ctypes.POINTER(_c_i32), _i64p, _i64p]),
 }
 
 
@@ -335,9 +336,20 @@ class Index:
         """(screened search blocks, blocks flagged for the exact pass, exact re-runs the handle ran). Flagged
         blocks of staged searches that were superseded before anyone fetched them are never re-run; a benchmark
         pays flagged - re-runs exact searches itself."""
-        b, f, r = _c_i64(), _c_i64(), _c_i64()
-        _check(self._lib.rr_screen_counts(self._h, ctypes.byref(b), ctypes.byref(f), ctypes.byref(r)))
-        return b.value, f.value, r.value
+        return self.screen_counts_all()[:3]
+
+    def screen_counts_all(self) -> Tuple[int, int, int, int]:
+        """screen_counts() plus the query slots the verify proved only in its wide phase."""
+        b, f, r, w = _c_i64(), _c_i64(), _c_i64(), _c_i64()
+        _check(self._lib.rr_screen_counts(self._h, ctypes.byref(b), ctypes.byref(f), ctypes.byref(r),
+                                          ctypes.byref(w)))
+        return b.value, f.value, r.value, w.value
+
+    def screen_state(self) -> Tuple[bool, int, int]:
+        """(full per-lane lists in use, search blocks still paused to the exact kernel, pauses so far)."""
+        f, p, n = _c_i32(), _c_i64(), _c_i64()
+        _check(self._lib.rr_screen_state(self._h, ctypes.byref(f), ctypes.byref(p), ctypes.byref(n)))
+        return bool(f.value), p.value, n.value
 
     def set_timeout(self, ms: int) -> None:
         """Multi-process deadline of every host wait on device work (0 = none); a miss raises

@@ -69,20 +69,26 @@ def test_screen_rarely_falls_back_on_unit_norm_data(Index):
     ix.close()
 
 
-def test_screen_ties_take_the_exact_pass(Index):
+@pytest.mark.parametrize("wide", [True, False])
+def test_screen_ties_take_the_exact_pass(Index, monkeypatch, wide):
     """40 copies of one row spread over the corpus, queried with that row: 40 exactly tied top scores, more
-    than the screen's candidate list holds, so the bound cannot prove completeness and the search is re-run
-    exactly; the result is the canonical order (equal scores by ascending index), bit-identical to the
-    one-pass exact kernel, for cosine and dot."""
+    than the screen's global candidate list holds. The verify's wide phase rescores every list entry above the
+    largest single-list bound (the copies lie in many workgroups' lists) and proves the top-k; without it
+    (RR_WIDE_VERIFY=0) the bound cannot prove completeness and the search is re-run exactly. Either way the
+    result is the canonical order (equal scores by ascending index), bit-identical to the one-pass exact kernel,
+    for cosine and dot."""
     corpus = synth.unit_norm_gaussian(77, 65536, 1024)
     dup = np.arange(40) * 1601 + 7
     corpus[dup] = corpus[123]
     q = np.concatenate([corpus[123:124], synth.unit_norm_gaussian(78, 31, 1024)])
     for metric in ("cosine", "dot"):
+        monkeypatch.setenv("RR_WIDE_VERIFY", "1" if wide else "0")
         ix = Index(dtype="fp32", metric=metric)
+        monkeypatch.delenv("RR_WIDE_VERIFY")
         ix.load(corpus)
         got = ix.search(q, 5)
-        assert ix.screen_stats() == (1, 1)
+        blocks, flagged, reruns, wide_slots = ix.screen_counts_all()
+        assert (blocks, flagged, reruns, wide_slots) == ((1, 0, 0, 1) if wide else (1, 1, 1, 0))
         assert sorted(got[1][0]) == sorted(np.sort(np.append(dup, 123))[:5])
         ix.set_kernel("exact")
         want = ix.search(q, 5)
@@ -213,6 +219,85 @@ def test_screen_f16_conversion_keeps_subnormals(Index):
     got = ix.search(q[:32], 1)
     assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
     assert ix.screen_stats() == (2, 0)
+    ix.close()
+    ex.close()
+
+
+def _clustered(n, sigma, layout, seed=20260, clusters=1000):
+    """n rows from the reference's real e5 rows (the first `clusters` of data/squad_embeddings.npy) plus seeded
+    noise of relative size sigma, L2-normalised: 'interleaved' (row i from SQuAD row i mod clusters) or
+    'contiguous' (row i from SQuAD row i div (n / clusters))."""
+    import os
+    sq = np.load(os.path.join(os.path.dirname(__file__), "golden", "data", "squad_embeddings.npy")).astype(np.float32)
+    sq = sq[:clusters] / np.linalg.norm(sq[:clusters], axis=1, keepdims=True)
+    rng = np.random.default_rng(seed)
+    m = clusters
+    c = np.arange(n) % m if layout == "interleaved" else np.minimum(np.arange(n) // (n // m), m - 1)
+    x = sq[c] + np.float32(sigma) * rng.standard_normal((n, sq.shape[1]), dtype=np.float32) / np.float32(32.0)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    qc = rng.integers(0, m, 32)
+    q = sq[qc] + np.float32(sigma) * rng.standard_normal((32, sq.shape[1]), dtype=np.float32) / np.float32(32.0)
+    return x, q / np.linalg.norm(q, axis=1, keepdims=True)
+
+
+@pytest.mark.parametrize("metric", ["cosine", "dot"])
+@pytest.mark.parametrize("layout", ["interleaved", "contiguous"])
+def test_wide_verify_on_clustered_embeddings(Index, metric, layout):
+    """Near-duplicate clusters: 60 noisy copies (sigma 0.01) of each of the 1000 real SQuAD e5
+    rows. Far more than 16 documents lie inside the screen's bound window above each query's k-th score, so the
+    first check fails for every query. Interleaved, each workgroup's list holds its few copies and the wide phase
+    proves the top-k on the device (no flag, no re-run); contiguous, a cluster fills a few workgroups' lists and
+    the block takes the exact pass. Results bit-identical to the exact kernel either way, for k = 5 and 10."""
+    corpus, q = _clustered(60000, 0.01, layout)
+    ex = Index(dtype="fp32", metric=metric)
+    ex.load(corpus)
+    ex.set_kernel("exact")
+    ix = Index(dtype="fp32", metric=metric)
+    ix.load(corpus)
+    for k in (5, 10):
+        want = ex.search(q, k)
+        got = ix.search(q, k)
+        assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), k
+    blocks, flagged, reruns, wide_slots = ix.screen_counts_all()
+    print(layout, metric, {"blocks": blocks, "flagged": flagged, "reruns": reruns, "wide_slots": wide_slots})
+    assert blocks == 2
+    if layout == "interleaved":
+        assert flagged == 0 and reruns == 0 and wide_slots >= 32
+    else:
+        assert flagged == reruns and flagged >= 1
+    ix.close()
+    ex.close()
+
+
+@pytest.mark.parametrize("layout", ["interleaved", "contiguous"])
+def test_screen_adapts_to_clustered_corpora(Index, layout):
+    """The adaptive screen (rr_api.cpp adapt_screen) on 1000 noisy copies of each of 100 SQuAD rows (sigma 0.01):
+    interleaved, every cluster's copies fall on a few lanes of each workgroup (a stride of 100 rows), overflow the
+    short per-lane lists and their floors stop every proof — after one window of flagged blocks the handle switches
+    to full lists, and from then on the wide phase proves every block (no flags). Contiguous, a cluster fills a
+    few workgroups' lists even then: after a second window the handle pauses screening (the exact kernel alone)
+    for 1024 blocks. Results bit-identical to the exact kernel at every step."""
+    corpus, q = _clustered(100000, 0.01, layout, clusters=100)
+    ex = Index(dtype="fp32", metric="cosine")
+    ex.load(corpus)
+    ex.set_kernel("exact")
+    want = ex.search(q, 5)
+    ix = Index(dtype="fp32", metric="cosine")
+    ix.load(corpus)
+    assert ix.screen_state() == (False, 0, 0)
+    hist = []
+    for step in range(140):
+        got = ix.search(q, 5)
+        assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), step
+        hist.append(ix.screen_counts_all() + ix.screen_state())
+    blocks, flagged, reruns, wide_slots, full, pause_left, pauses = hist[-1]
+    print(layout, hist[40], hist[-1])
+    assert full
+    if layout == "interleaved":
+        assert pauses == 0 and blocks == 140
+        assert hist[-1][1] == hist[80][1] and wide_slots >= 32 * 50     # no flags once the lists are full
+    else:
+        assert pauses == 1 and pause_left > 0 and blocks < 140          # screening paused: exact kernel alone
     ix.close()
     ex.close()
 

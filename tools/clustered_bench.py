@@ -8,8 +8,10 @@ layouts: "interleaved" (c(i) = i mod 1000: each cluster spread over the whole co
 (c(i) = i div 1000: each cluster one run of 1000 rows, i.e. inside a few workgroups' chunks).
 
 For each (sigma, layout), k = 5 cosine (the headline's search), on one GPU:
-  * screened (RR_KERNEL_AUTO): q/s over K staged steps with every flagged block's exact re-run paid inside the
-    timed window (bench.timed_steps), the flagged-block rate;
+  * screened (RR_KERNEL_AUTO, after W awaited warm-up steps in which the adaptive screen settles: short -> full
+    per-lane lists, or a pause to the exact kernel): q/s over K staged steps with every flagged block's exact re-run
+    paid inside the timed window (bench.timed_steps), the flagged-block rate, the slots the verify's wide phase
+    proved, the screen's adaptive state;
   * exact (RR_KERNEL_EXACT, one pass over the fp32 rows): q/s;
   * results of a fetched search: screened == exact, bit for bit.
 One JSON line per configuration, then a summary line.
@@ -47,7 +49,8 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--k", type=int, default=5)
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=80,
+                    help="untimed steps first, each awaited: the adaptive screen settles (short -> full lists, pause)")
     ap.add_argument("--sigmas", default="0.01,0.03,0.1,0.3")
     ap.add_argument("--layouts", default="interleaved,contiguous")
     args = ap.parse_args()
@@ -80,8 +83,14 @@ def main() -> None:
             ix.load(corpus)
             del corpus
             ix.set_queries(q)
+            # warm-up paced like a serving loop (each batch's results awaited): the adaptive screen decides from the
+            # counts of COMPLETED blocks, which an unpaced burst of staged searches outruns
+            for _ in range(args.warmup):
+                ix.search_staged(args.k)
+                ix.synchronize()
             acct = {}
-            s_el, _, _ = bench.timed_steps(ix, args.k, args.steps, args.warmup, None, cuda_sync, 10, acct)
+            s_el, _, _ = bench.timed_steps(ix, args.k, args.steps, 0, None, cuda_sync, 10, acct)
+            state = ix.screen_state()
             got = ix.search(q, args.k)
             ix.set_kernel("exact")
             ix.set_queries(q)
@@ -102,6 +111,8 @@ def main() -> None:
                    "flagged_blocks": acct["flagged"], "blocks": acct["blocks"],
                    "reruns_paid": acct["reruns_paid"], "reruns_library": acct["reruns_library"],
                    "flag_rate": round(acct["flagged"] / max(1, acct["blocks"]), 4),
+                   "wide_verified_slots": acct["wide_slots"],
+                   "screen_state_after": dict(zip(("full_lists", "pause_left", "pauses"), state)),
                    "bit_identical_to_exact": same,
                    "median_score_gap_k_to_16": round(gap16, 6), "median_score_gap_k_to_32": round(gap32, 6),
                    "top1_median": round(float(np.median(s32[:, 0])), 5)}
