@@ -1,6 +1,7 @@
 """The C-ABI library: builds for gfx950, loads, and exports exactly what include/rag_retrieval.h declares.
 No compute calls (no GPU here)."""
 import os
+import sys
 import re
 import subprocess
 
@@ -86,16 +87,20 @@ def test_inline_asm_loads_are_hazard_free():
     asm output by one wait state; an MFMA operand needs two) — tools/check_asm_loads.py, the hazards of
     cdna_hip_programming.md §5.7 items 1-2. Needs the gfx950 .s from `make isa`."""
     pkg = _lib.PKG_ROOT
-    checker = os.path.join(os.path.dirname(pkg), "tools", "check_asm_loads.py")
+    sys.path.insert(0, os.path.join(os.path.dirname(pkg), "tools"))
+    from check_asm_loads import check
     for unit, pattern, least in (("rr_kernels", r"_ZN2rr18fused_score_kernel\w+", 16),
                                  ("rr_sk", r"_ZN2rr2sk15sk_score_kernel\w+", 16)):
-        s_file = os.path.join(pkg, "build", "isa", f"{unit}-hip-amdgcn-amd-amdhsa-gfx950.s")
+        # the library build keeps the assembly (Makefile: -save-temps=obj); rebuild it when it is older than the code
+        s_file = os.path.join(pkg, "build", f"{unit}-hip-amdgcn-amd-amdhsa-gfx950.s")
         src = os.path.join(pkg, "csrc", f"{unit}.hip")
-        deps = [src, os.path.join(pkg, "csrc", "rr_device.h")]
+        deps = [src, os.path.join(pkg, "csrc", "rr_device.h"), os.path.join(pkg, "csrc", "rr_internal.h")]
         if not os.path.exists(s_file) or os.path.getmtime(s_file) < max(map(os.path.getmtime, deps)):
-            subprocess.check_call(["make", "-C", pkg, "isa"], stdout=subprocess.DEVNULL)
-        syms = re.findall(rf"^({pattern}):", open(s_file).read(), flags=re.M)
+            subprocess.check_call(["make", "-C", pkg, "-j4"], stdout=subprocess.DEVNULL)
+        text = open(s_file).read()
+        syms = re.findall(rf"^({pattern}):", text, flags=re.M)
         assert len(syms) >= least, (unit, len(syms))
+        lines = text.split("\n")
         for sym in syms:
-            r = subprocess.run(["python3", checker, s_file, sym], capture_output=True, text=True)
-            assert r.returncode == 0, (sym, r.stdout)
+            n_asm, bad = check(lines, sym)
+            assert not bad, (sym, bad[:5])
