@@ -753,7 +753,8 @@ bool screened(const rr_handle* h, int k, int slots) {
 // Adaptive screen, at the start of every search, from the flagged-block counts the pinned copies last showed (a block
 // or two late; rr_api.cpp check_narrow reads the same). Windows of >= 32 screened blocks:
 //   * short per-lane lists (4 keys + the workgroup's floor, rr_sk.hip KL) -> full lists (KT keys) when more than 1
-//     in 8 blocks of the window flagged: crowded near-duplicates (a few lanes holding many of them) raise the floors
+//     in 32 blocks of the window flagged (each costs an exact pass, twice a screen: 3 % flagged cost more than the
+//     full lists do): crowded near-duplicates (a few lanes holding many of them) raise the floors
 //     above what the verify can prove; full lists have no floors. Rank-local (it changes no exchange);
 //   * full lists, and still more than 1 in 2 blocks flagged: the screen cannot prune this corpus (near-duplicate
 //     clusters stored together fill a few workgroups' lists), and each flagged block pays the screen AND the exact
@@ -784,7 +785,7 @@ void adapt_screen(rr_handle* h, int k) {
   }
   if (nb < 32) return;
   if (!h->full_lists) {
-    if (nf * 8 > nb) h->full_lists = true;
+    if (nf * 32 > nb) h->full_lists = true;
   } else if (!h->dist && nf * 2 > nb && !narrow_lists(h, k)) {
     h->screen_pause = 1024;
     ++h->pauses;

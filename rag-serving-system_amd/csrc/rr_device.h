@@ -101,6 +101,21 @@ __device__ __forceinline__ uint32_t group_max_u32(uint32_t v) {
   if constexpr (G >= 16) v = dpp_max_u32<0x140>(v); // row_mirror
   return v;
 }
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_min_u32(uint32_t v) {
+  const uint32_t t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+  return v < t ? v : t;
+}
+// min over aligned groups of G lanes (G = 2, 4, 8, 16), every lane of the group gets it
+template <int G>
+__device__ __forceinline__ uint32_t group_min_u32(uint32_t v) {
+  static_assert(G == 2 || G == 4 || G == 8 || G == 16, "DPP row groups");
+  v = dpp_min_u32<0xB1>(v);
+  if constexpr (G >= 4) v = dpp_min_u32<0x4E>(v);
+  if constexpr (G >= 8) v = dpp_min_u32<0x141>(v);
+  if constexpr (G >= 16) v = dpp_min_u32<0x140>(v);
+  return v;
+}
 // max over the 64 lanes, returned in every lane
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   v = group_max_u32<16>(v);

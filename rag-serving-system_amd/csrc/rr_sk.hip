@@ -735,6 +735,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // epilogue lane mapping: wave w owns queries 4·QH·w + [0, 4·QH); LPQ lanes per query, each with DPL
   // consecutive tile rows (QH 1: 16 lanes x 2 rows, QH 2: 8 lanes x 4 rows)
   constexpr int LPQ = 16 / QH, DPL = 2 * QH;
+  constexpr int J = (KT + LPQ - 1) / LPQ;   // (the epilogue's tighter bar: each lane's J-th list entry)
+  static_assert(J <= KL, "the tighter bar reads each lane's J-th entry");
   const int qe = 4 * QH * w + lane / LPQ, er = DPL * (lane % LPQ);
   const bool qev = MODE == 1 ? qe == vq : qe < b;
   float qn = COS && !SCR ? qinfo[qe] : 0.f;
@@ -946,21 +948,28 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     // no lane keeps it — the merged lists are the same as without the bar, but lanes insert ~LPQ x less often
     // (the branch-free insert is the epilogue's largest VALU cost, and it runs for the whole wave whenever
     // any of its lanes inserts). For the large-k floors: a key dropped here is below a full lane's last entry.
-    uint64_t bar = 0;
+    // A tighter bar, as valid: when each of the group's LPQ lanes holds J = ceil(KT / LPQ) keys of at least y, the
+    // group holds LPQ * J >= KT keys >= y, so no key below y is in the workgroup's top-KT. y = the smallest of the
+    // lanes' J-th entries (0 while a lane holds fewer) — about the group's KT-th key, where the largest last entry
+    // is about its (LPQ x KT)-th: far fewer keys pass, and the insert runs far less often. Not for the large-k output
+    // (its lists must hold the workgroup's top wide_k > KT); the screen's short lists hold J (<= KL) too, and a key it
+    // drops below y is below the workgroup's KT-th key or a full lane's last (its floor): either way inside the
+    // verify's bound.
+    uint32_t th = group_max_u32<LPQ>((uint32_t)(tk.last() >> 32));
+    if (MODE == 1 || a.wide_k == 0) {
+      const uint32_t tmin = group_min_u32<LPQ>((uint32_t)(tk.v[J - 1] >> 32));
+      th = th > tmin ? th : tmin;
+    }
+    // Keys whose score ord is below th are dropped; ties on the score go on to the insert, whose 64-bit compares
+    // place them exactly (inserting a key at or below a list's last leaves it unchanged).
     float thr = -INFINITY;
     if constexpr (SCR) {
-      // the screen compares in the bound's own (float) domain: u below the lane group's largest last score cannot
-      // enter (see the bar above; ties on the score go on to the insert, whose 64-bit compares place them exactly),
-      // and only the keys that pass are formed — one compare per score instead of a key and a 64-bit compare
-      const uint32_t bh = group_max_u32<LPQ>((uint32_t)(tk.last() >> 32));
-      if (bh != 0) thr = float_of_ord(bh);
-    } else {
-      bar = group_max_u64<LPQ>(tk.last());
-    }
-    if constexpr (COS && !SCR) {
-      const uint64_t last = bar;
-      if (last != 0) {
-        const float t = float_of_ord((uint32_t)(last >> 32));
+      // the screen compares in the bound's own (float) domain, and only the keys that pass are formed — one
+      // compare per score instead of a key and a 64-bit compare
+      if (th != 0) thr = float_of_ord(th);
+    } else if constexpr (COS) {
+      if (th != 0) {
+        const float t = float_of_ord(th);
         thr = t - fabsf(t) * 0x1p-20f - 0x1p-100f;
       }
     }
@@ -1009,13 +1018,13 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           float c = s / den;   // IEEE division, as the reference's elementwise kernel
           c = fminf(fmaxf(c, -1.0f), 1.0f);
           const uint64_t key = make_key(c, idx_base + (uint32_t)row);
-          if (key > bar) tk.insert(key);
+          if ((uint32_t)(key >> 32) >= th) tk.insert(key);
         }
       } else {
         const uint64_t key = make_key(s, idx_base + (uint32_t)row);
         if (DUMP && a.all_keys) {
           if (valid) a.all_keys[(size_t)qe * n + row] = key;
-        } else if (valid && key > bar) {
+        } else if (valid && (uint32_t)(key >> 32) >= th) {
           tk.insert(key);
         }
       }
@@ -1219,11 +1228,16 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         sv[0] = ww ? sv[0] + p.x : p.x;
         sv[1] = ww ? sv[1] + p.y : p.y;
       }
-      const uint64_t bar = group_max_u64<LPQ>(tk.last());
+      // the same threshold as the first tile's epilogue (score ords; ties go on to the exact insert)
+      uint32_t th = group_max_u32<LPQ>((uint32_t)(tk.last() >> 32));
+      {
+        const uint32_t tmin = group_min_u32<LPQ>((uint32_t)(tk.v[J - 1] >> 32));
+        th = th > tmin ? th : tmin;
+      }
       float thr = -INFINITY;
       if constexpr (COS) {
-        if (bar != 0) {
-          const float tt = float_of_ord((uint32_t)(bar >> 32));
+        if (th != 0) {
+          const float tt = float_of_ord(th);
           thr = tt - fabsf(tt) * 0x1p-20f - 0x1p-100f;
         }
       }
@@ -1237,11 +1251,11 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
             float c = s / den;   // IEEE division, as the first tile and the full pass
             c = fminf(fmaxf(c, -1.0f), 1.0f);
             const uint64_t key = make_key(c, idx_base + (uint32_t)erow[e]);
-            if (key > bar) tk.insert(key);
+            if ((uint32_t)(key >> 32) >= th) tk.insert(key);
           }
         } else {
           const uint64_t key = make_key(s, idx_base + (uint32_t)erow[e]);
-          if (valid && key > bar) tk.insert(key);
+          if (valid && (uint32_t)(key >> 32) >= th) tk.insert(key);
         }
       }
     }

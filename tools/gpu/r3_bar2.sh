@@ -1,0 +1,9 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu -rA tests/test_gpu_screen.py -k "adapt or clustered or ties" > gpurun_out/t_bar2.log 2>&1 ;
+timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/t_bar.log 2>&1 &&
+rm -f gpurun_out/ab_bar.txt &&
+STEPS=20 WARMUP=5 bash tools/ab/ab.sh gpurun_out/ab_bar.txt "6250000 64 10 bf16" new r3f &&
+STEPS=20 WARMUP=5 bash tools/ab/ab.sh gpurun_out/ab_bar.txt "1000000 32 5 fp32" new r3f
