@@ -226,6 +226,12 @@ def main() -> None:
         sys.exit(spawn_ranks(args.gpus))
     from rag_service_amd.dist import env_rank_world
     rank, world, _ = env_rank_world()
+    if world > 1:
+        # Before the HIP runtime starts (it reads this once): one hardware queue per stream. With the default 4, the
+        # RCCL communicators' internal streams share queues with the compute streams (profiles/r03/trace: the second
+        # lane's communicator landed on the second compute stream's queue), and an all-gather waiting for its peers
+        # at the head of a shared, in-order queue would hold the screens queued behind it.
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
     stage = {"stage": "start"}
     try:
         run(args, stage)
@@ -461,6 +467,7 @@ def run(args, stage: dict) -> None:
                                      "value above is the first K steps after W warm-up steps from idle"},
             "exchange": ("rccl ncclAllGather of per-shard top-k keys, device merge on every rank"
                          if world > 1 or rccl_ranks else "none (one shard)"),
+            "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default (4)"),
             "rccl_ranks": rccl_ranks,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -757,6 +757,104 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   TopK<KL> tk;
   tk.init();
 
+  // The metric epilogue of one tile: its summed scores svp (this lane's DPL rows), its first row bse and its factor
+  // slot tsl. (Issuing it one tile late, in the next tile's MFMA shadow, measured -2 % on the 64-slot bf16 kernel
+  // and neutral on the screen: profiles/r03/a/ab_pipelined_epilogue_rejected.txt.)
+  auto epilogue = [&](const float (&svp)[DPL], int64_t bse, int tsl) {
+      // Cosine prefilter: a score whose estimate dot * rcp(den) (within a few ulp of the quotient) is below
+      // the lane's current k-th score minus a 2^-20 relative margin cannot enter the list, so only the
+      // few that pass pay the exact IEEE division (the list only grows inside the loop: the threshold
+      // taken here is conservative).
+      // full-key output (a.all_keys; the 32-wide instantiation, for the full-sort path): every key goes to HBM
+      constexpr bool DUMP = MODE == 0 && KT == 32 && QH == 1 && SCHED == 0 && !SCR;
+      // The bar a key must clear: the largest last entry of the query's LPQ lane lists (once full). A key at or
+      // below it cannot be in this workgroup's top-KT for the query (that lane alone holds KT keys above it), so
+      // no lane keeps it — the merged lists are the same as without the bar, but lanes insert ~LPQ x less often
+      // (the branch-free insert is the epilogue's largest VALU cost, and it runs for the whole wave whenever
+      // any of its lanes inserts). For the large-k floors: a key dropped here is below a full lane's last entry.
+      // A tighter bar, as valid: when each of the group's LPQ lanes holds J = ceil(KT / LPQ) keys of at least y, the
+      // group holds LPQ * J >= KT keys >= y, so no key below y is in the workgroup's top-KT. y = the smallest of the
+      // lanes' J-th entries (0 while a lane holds fewer) — about the group's KT-th key, where the largest last entry
+      // is about its (LPQ x KT)-th: far fewer keys pass, and the insert runs far less often. Not for the large-k output
+      // (its lists must hold the workgroup's top wide_k > KT); the screen's short lists hold J (<= KL) too, and a key it
+      // drops below y is below the workgroup's KT-th key or a full lane's last (its floor): either way inside the
+      // verify's bound.
+      uint32_t th = group_max_u32<LPQ>((uint32_t)(tk.last() >> 32));
+      if (MODE == 1 || a.wide_k == 0) {
+        const uint32_t tmin = group_min_u32<LPQ>((uint32_t)(tk.v[J - 1] >> 32));
+        th = th > tmin ? th : tmin;
+      }
+      // Keys whose score ord is below th are dropped; ties on the score go on to the insert, whose 64-bit compares
+      // place them exactly (inserting a key at or below a list's last leaves it unchanged).
+      float thr = -INFINITY;
+      if constexpr (SCR) {
+        // the screen compares in the bound's own (float) domain, and only the keys that pass are formed — one
+        // compare per score instead of a key and a 64-bit compare
+        if (th != 0) thr = float_of_ord(th);
+      } else if constexpr (COS) {
+        if (th != 0) {
+          const float t = float_of_ord(th);
+          thr = t - fabsf(t) * 0x1p-20f - 0x1p-100f;
+        }
+      }
+      // rows of this tile (scalar; 32 except in the last tile): the screen's validity test is one 32-bit compare
+      const int rem = MODE == 0 ? (int)(n - bse < 32 ? n - bse : 32) : 32;
+      const uint32_t key_base = MODE == 0 ? idx_base + (uint32_t)bse : 0u;
+  #pragma unroll
+      for (int e = 0; e < DPL; ++e) {
+        int64_t row;
+        bool valid;
+        float nd = 1.f;
+        float s = svp[e];
+        if constexpr (MODE == 1) {
+          row = grow[er + e];
+          valid = qev && gvalid[er + e];
+          if constexpr (COS) nd = gnorm[er + e];
+        } else {
+          row = bse + er + e;
+          // (the screen keeps lists for padding query slots too: nobody reads them)
+          valid = SCR ? er + e < rem : qev && (bse + 32 <= n || row < n);   // (whole tiles: a scalar test)
+          const float* tf = trow + tsl * 64 + er + e;   // factor 0 at tf[0], factor 1 at tf[32]
+          if constexpr (DT == 2) s = s * (COS ? tf[32] : tf[0]) * qs;   // exact 2^e rescales
+          if constexpr (COS || SCR) nd = tf[0];
+        }
+        if constexpr (SCR) {
+          // upper bound of the exact (DT 3) score, see "Screened search"; the relative bumps cover the
+          // roundings of the bound's own arithmetic and of the reciprocal (<= 1 ulp)
+          const float eps = fmaf(a.eps_a * nd, qn, a.eps_b * fmaf(a.sqrt_d, nd, qsa));
+          float v = s + eps;
+          v += fabsf(v) * 0x1p-22f;
+          float u;
+          if constexpr (COS) {
+            u = v * __builtin_amdgcn_rcpf(cos_den(qn, nd));
+            u += fabsf(u) * 0x1p-18f + 0x1p-126f;   // (+ |q| in another summation order than the exact path's)
+            u = fminf(fmaxf(u, -1.0f), 1.0f);   // the exact score is clipped to [-1, 1] (retriever.py:609)
+          } else {
+            u = v;
+          }
+          if (valid && u >= thr) tk.insert(make_key(u, key_base + (uint32_t)(er + e)));   // (NaN: never)
+        } else if constexpr (COS) {
+          // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
+          const float den = cos_den(qn, nd);
+          if (DUMP && a.all_keys) {
+            if (valid) a.all_keys[(size_t)qe * n + row] = make_key(fminf(fmaxf(s / den, -1.0f), 1.0f), idx_base + (uint32_t)row);
+          } else if (valid && s * __builtin_amdgcn_rcpf(den) >= thr) {
+            float c = s / den;   // IEEE division, as the reference's elementwise kernel
+            c = fminf(fmaxf(c, -1.0f), 1.0f);
+            const uint64_t key = make_key(c, idx_base + (uint32_t)row);
+            if ((uint32_t)(key >> 32) >= th) tk.insert(key);
+          }
+        } else {
+          const uint64_t key = make_key(s, idx_base + (uint32_t)row);
+          if (DUMP && a.all_keys) {
+            if (valid) a.all_keys[(size_t)qe * n + row] = key;
+          } else if (valid && (uint32_t)(key >> 32) >= th) {
+            tk.insert(key);
+          }
+        }
+      }
+  };
+
   SK_PROBE(1);
   int slot = 0, ti = 0, cpar = 0, ts = 0;   // ring slot, tile of the chunk, nxt parity, factor slot
   int64_t tcount = 0;                       // tiles done (reduction buffer parity)
@@ -937,98 +1035,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         for (int e = 0; e < 4; ++e) sv[e] = ww ? sv[e] + p[e] : p[e];
       }
     }
-    // Cosine prefilter: a score whose estimate dot * rcp(den) (within a few ulp of the quotient) is below
-    // the lane's current k-th score minus a 2^-20 relative margin cannot enter the list, so only the
-    // few that pass pay the exact IEEE division (the list only grows inside the loop: the threshold
-    // taken here is conservative).
-    // full-key output (a.all_keys; the 32-wide instantiation, for the full-sort path): every key goes to HBM
-    constexpr bool DUMP = MODE == 0 && KT == 32 && QH == 1 && SCHED == 0 && !SCR;
-    // The bar a key must clear: the largest last entry of the query's LPQ lane lists (once full). A key at or
-    // below it cannot be in this workgroup's top-KT for the query (that lane alone holds KT keys above it), so
-    // no lane keeps it — the merged lists are the same as without the bar, but lanes insert ~LPQ x less often
-    // (the branch-free insert is the epilogue's largest VALU cost, and it runs for the whole wave whenever
-    // any of its lanes inserts). For the large-k floors: a key dropped here is below a full lane's last entry.
-    // A tighter bar, as valid: when each of the group's LPQ lanes holds J = ceil(KT / LPQ) keys of at least y, the
-    // group holds LPQ * J >= KT keys >= y, so no key below y is in the workgroup's top-KT. y = the smallest of the
-    // lanes' J-th entries (0 while a lane holds fewer) — about the group's KT-th key, where the largest last entry
-    // is about its (LPQ x KT)-th: far fewer keys pass, and the insert runs far less often. Not for the large-k output
-    // (its lists must hold the workgroup's top wide_k > KT); the screen's short lists hold J (<= KL) too, and a key it
-    // drops below y is below the workgroup's KT-th key or a full lane's last (its floor): either way inside the
-    // verify's bound.
-    uint32_t th = group_max_u32<LPQ>((uint32_t)(tk.last() >> 32));
-    if (MODE == 1 || a.wide_k == 0) {
-      const uint32_t tmin = group_min_u32<LPQ>((uint32_t)(tk.v[J - 1] >> 32));
-      th = th > tmin ? th : tmin;
-    }
-    // Keys whose score ord is below th are dropped; ties on the score go on to the insert, whose 64-bit compares
-    // place them exactly (inserting a key at or below a list's last leaves it unchanged).
-    float thr = -INFINITY;
-    if constexpr (SCR) {
-      // the screen compares in the bound's own (float) domain, and only the keys that pass are formed — one
-      // compare per score instead of a key and a 64-bit compare
-      if (th != 0) thr = float_of_ord(th);
-    } else if constexpr (COS) {
-      if (th != 0) {
-        const float t = float_of_ord(th);
-        thr = t - fabsf(t) * 0x1p-20f - 0x1p-100f;
-      }
-    }
-    // rows of this tile (scalar; 32 except in the last tile): the screen's validity test is one 32-bit compare
-    const int rem = MODE == 0 ? (int)(n - base < 32 ? n - base : 32) : 32;
-    const uint32_t key_base = MODE == 0 ? idx_base + (uint32_t)base : 0u;
-#pragma unroll
-    for (int e = 0; e < DPL; ++e) {
-      int64_t row;
-      bool valid;
-      float nd = 1.f;
-      float s = sv[e];
-      if constexpr (MODE == 1) {
-        row = grow[er + e];
-        valid = qev && gvalid[er + e];
-        if constexpr (COS) nd = gnorm[er + e];
-      } else {
-        row = base + er + e;
-        // (the screen keeps lists for padding query slots too: nobody reads them)
-        valid = SCR ? er + e < rem : qev && (base + 32 <= n || row < n);   // (whole tiles: a scalar test)
-        const float* tf = trow + ts * 64 + er + e;   // factor 0 at tf[0], factor 1 at tf[32]
-        if constexpr (DT == 2) s = s * (COS ? tf[32] : tf[0]) * qs;   // exact 2^e rescales
-        if constexpr (COS || SCR) nd = tf[0];
-      }
-      if constexpr (SCR) {
-        // upper bound of the exact (DT 3) score, see "Screened search"; the relative bumps cover the
-        // roundings of the bound's own arithmetic and of the reciprocal (<= 1 ulp)
-        const float eps = fmaf(a.eps_a * nd, qn, a.eps_b * fmaf(a.sqrt_d, nd, qsa));
-        float v = s + eps;
-        v += fabsf(v) * 0x1p-22f;
-        float u;
-        if constexpr (COS) {
-          u = v * __builtin_amdgcn_rcpf(cos_den(qn, nd));
-          u += fabsf(u) * 0x1p-18f + 0x1p-126f;   // (+ |q| in another summation order than the exact path's)
-          u = fminf(fmaxf(u, -1.0f), 1.0f);   // the exact score is clipped to [-1, 1] (retriever.py:609)
-        } else {
-          u = v;
-        }
-        if (valid && u >= thr) tk.insert(make_key(u, key_base + (uint32_t)(er + e)));   // (NaN: never)
-      } else if constexpr (COS) {
-        // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
-        const float den = cos_den(qn, nd);
-        if (DUMP && a.all_keys) {
-          if (valid) a.all_keys[(size_t)qe * n + row] = make_key(fminf(fmaxf(s / den, -1.0f), 1.0f), idx_base + (uint32_t)row);
-        } else if (valid && s * __builtin_amdgcn_rcpf(den) >= thr) {
-          float c = s / den;   // IEEE division, as the reference's elementwise kernel
-          c = fminf(fmaxf(c, -1.0f), 1.0f);
-          const uint64_t key = make_key(c, idx_base + (uint32_t)row);
-          if ((uint32_t)(key >> 32) >= th) tk.insert(key);
-        }
-      } else {
-        const uint64_t key = make_key(s, idx_base + (uint32_t)row);
-        if (DUMP && a.all_keys) {
-          if (valid) a.all_keys[(size_t)qe * n + row] = key;
-        } else if (valid && (uint32_t)(key >> 32) >= th) {
-          tk.insert(key);
-        }
-      }
-    }
+    epilogue(sv, base, ts);
     if (tcount == 0) SK_PROBE(2);
     if (MODE == 0 && tcount == 1) SK_PROBE(3);
     ++tcount;

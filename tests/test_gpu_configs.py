@@ -127,3 +127,38 @@ def test_config5_bf16_b64_through_rccl(Index, golden_configs, config5):
     if float(golden_configs["c5_cupy_gap"]) > 1e-5:
         assert near == 0
     ix.close()
+
+
+N5 = 50_000_000
+
+
+@pytest.mark.parametrize("metric", ["dot", "cosine"])
+def test_config5_50m_full_size(Index, metric):
+    """BASELINE config 5 at its defining size on one MI355X: 50M x 1024 bf16 rows (102 GB; F2
+    exact-integer rows generated on the device, exact in bf16), B = 64, k = 10, through the 64-slot bf16 kernel.
+    The 64 queries are corpus rows planted at spread-out indices, so each query's top-1 is its own row (its self
+    dot |x|^2 ~ 340 against ~ +-11 for the others, and cosine 1). Every returned score equals the fp64 metric at
+    the returned index — exactly for dot (integer products, |sum| < 2^24: exact in fp32 in any order), within 1e-6
+    for cosine — and one shard and 8 in-process shards (the 8-GPU exchange and merge) give bit-identical results.
+    Property checks in place of a host-side golden: the reference cannot run 50M rows here."""
+    planted = np.arange(64, dtype=np.int64) * 781_249 + 12_345
+    seed = 5
+    q = np.stack([synth.exact_int_rows(seed, int(r), 1, D)[0] for r in planted])
+    one = Index(dtype="bf16", metric=metric)
+    one.fill_synthetic(0, seed, N5, D)
+    s1, i1 = one.search(q, K)
+    one.close()                                          # free the 102 GB before the 8-shard handle
+    assert np.array_equal(i1[:, 0], planted)
+    for i in range(q.shape[0]):
+        rows = np.stack([synth.exact_int_rows(seed, int(r), 1, D)[0] for r in i1[i]])
+        want = exact_scores(rows, q[i:i + 1], metric)[0]
+        if metric == "dot":
+            assert np.array_equal(s1[i].astype(np.float64), want), i
+        else:
+            assert np.max(np.abs(s1[i] - want)) <= 1e-6, i
+        assert np.all(np.diff(s1[i]) <= 0), i            # sorted
+    many = Index(devices=[0] * 8, dtype="bf16", metric=metric)
+    many.fill_synthetic(0, seed, N5, D)
+    s8, i8 = many.search(q, K)
+    many.close()
+    assert np.array_equal(i8, i1) and np.array_equal(s8, s1)
