@@ -358,8 +358,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   float* red = (float*)(smem + ring_bytes(RS));
   constexpr int SW = (COS || SCR ? 1 : 0) + (DT == 2 ? 1 : 0);   // per-row factors (norm, split scale)
   constexpr int FX = SW > 0 ? 1 : 0;                            // LDS-DMA instructions per tile for them
-  float* trow = (float*)(smem + ring_bytes(RS) + red_bytes(RS, QH));   // [3 tiles][2 factors][32 rows]
-  int* nxt = (int*)(trow + 3 * 64);                             // [2] next chunk (dynamic schedule), + pad
+  float* trow = (float*)(smem + ring_bytes(RS) + red_bytes(RS, QH));   // [4 tiles][2 factors][32 rows]
+  int* nxt = (int*)(trow + 4 * 64);                             // [2] next chunk (dynamic schedule), + pad
   float* qinfo = (float*)(nxt + 4);                             // [QS] |q|, [QS] 2^-e / sum|q| / max|q|, [QS] int e
   int* qexp = (int*)(qinfo + 2 * QS);
 
@@ -463,7 +463,10 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #ifndef RR_SK_LOOKAHEAD
 #define RR_SK_LOOKAHEAD 2
 #endif
-  constexpr int LA = NS >= 2 && QH == 1 ? RR_SK_LOOKAHEAD : 1;   // (64 slots: measured faster with 1)
+#ifndef RR_SK_LA64
+#define RR_SK_LA64 1
+#endif
+  constexpr int LA = NS >= 2 ? (QH == 1 ? RR_SK_LOOKAHEAD : RR_SK_LA64) : 1;   // (64 slots: measured faster with 1)
   int pend = 0;   // LA 2: vector-memory ops this wave issued after the slab it waits for next
   int64_t chunk = g, base = chunk * CT * 32;
   if constexpr (MODE == 0) {
@@ -761,6 +764,13 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // slot tsl. (Issuing it one tile late, in the next tile's MFMA shadow, measured -2 % on the 64-slot bf16 kernel
   // and neutral on the screen: profiles/r03/a/ab_pipelined_epilogue_rejected.txt.)
   auto epilogue = [&](const float (&svp)[DPL], int64_t bse, int tsl) {
+#if defined(RR_SK_DIAG) && (RR_SK_DIAG & 1)
+      // diagnostic builds only (tools/kbench_cfg5.hip): no epilogue, the sums kept live by one compare each
+#pragma unroll
+      for (int e = 0; e < DPL; ++e)
+        if (svp[e] > 1e30f) tk.insert(make_key(svp[e], (uint32_t)(bse + er + e)));
+      return;
+#endif
       // Cosine prefilter: a score whose estimate dot * rcp(den) (within a few ulp of the quotient) is below
       // the lane's current k-th score minus a 2^-20 relative margin cannot enter the list, so only the
       // few that pass pay the exact IEEE division (the list only grows inside the loop: the threshold
@@ -800,12 +810,51 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       // rows of this tile (scalar; 32 except in the last tile): the screen's validity test is one 32-bit compare
       const int rem = MODE == 0 ? (int)(n - bse < 32 ? n - bse : 32) : 32;
       const uint32_t key_base = MODE == 0 ? idx_base + (uint32_t)bse : 0u;
-  #pragma unroll
+      // the exact paths' prefilter, rcp-free: s / den >= thr  <=  s >= thr * den (den > 0), evaluated as one fma of
+      // per-tile terms; within 2^-20 relative of the quotient's own rounding, like the margin above
+      float thq = 0.f, th8 = -INFINITY;
+      if constexpr (COS && !SCR) {
+        if (th != 0) {
+          thq = thr * qn;
+          th8 = thr * 1e-8f;
+        }
+      }
+      const float thf = th != 0 ? float_of_ord(th) : -INFINITY;   // dot: the bar's float (ord order = float order)
+      // this lane's per-row factors, one vector LDS read each (factor 0 at [0, 32), factor 1 at [32, 64))
+      float fac0[DPL], fac1[DPL];
+      if constexpr (MODE == 0 && (COS || SCR || DT == 2)) {
+        const float* tf = trow + tsl * 64 + er;
+        if constexpr (DPL == 4) {
+          const f32x4 v0 = *(const f32x4*)tf;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) fac0[e] = v0[e];
+          if constexpr (DT == 2 && COS) {
+            const f32x4 v1 = *(const f32x4*)(tf + 32);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) fac1[e] = v1[e];
+          }
+        } else {
+          const float2 v0 = *(const float2*)tf;
+          fac0[0] = v0.x;
+          fac0[1] = v0.y;
+          if constexpr (DT == 2 && COS) {
+            const float2 v1 = *(const float2*)(tf + 32);
+            fac1[0] = v1.x;
+            fac1[1] = v1.y;
+          }
+        }
+      }
+      bool pass[DPL];
+      float sc[DPL], ndv[DPL];
+      int64_t rows[DPL];
+      bool anyp = false;
+#pragma unroll
       for (int e = 0; e < DPL; ++e) {
         int64_t row;
         bool valid;
         float nd = 1.f;
         float s = svp[e];
+        pass[e] = false;
         if constexpr (MODE == 1) {
           row = grow[er + e];
           valid = qev && gvalid[er + e];
@@ -813,11 +862,13 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         } else {
           row = bse + er + e;
           // (the screen keeps lists for padding query slots too: nobody reads them)
-          valid = SCR ? er + e < rem : qev && (bse + 32 <= n || row < n);   // (whole tiles: a scalar test)
-          const float* tf = trow + tsl * 64 + er + e;   // factor 0 at tf[0], factor 1 at tf[32]
-          if constexpr (DT == 2) s = s * (COS ? tf[32] : tf[0]) * qs;   // exact 2^e rescales
-          if constexpr (COS || SCR) nd = tf[0];
+          valid = SCR ? er + e < rem : qev && er + e < rem;
+          if constexpr (DT == 2) s = s * (COS ? fac1[e] : fac0[e]) * qs;   // exact 2^e rescales
+          if constexpr (COS || SCR) nd = fac0[e];
         }
+        rows[e] = row;
+        sc[e] = s;
+        ndv[e] = nd;
         if constexpr (SCR) {
           // upper bound of the exact (DT 3) score, see "Screened search"; the relative bumps cover the
           // roundings of the bound's own arithmetic and of the reciprocal (<= 1 ulp)
@@ -835,26 +886,104 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           if (valid && u >= thr) tk.insert(make_key(u, key_base + (uint32_t)(er + e)));   // (NaN: never)
         } else if constexpr (COS) {
           // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
-          const float den = cos_den(qn, nd);
           if (DUMP && a.all_keys) {
-            if (valid) a.all_keys[(size_t)qe * n + row] = make_key(fminf(fmaxf(s / den, -1.0f), 1.0f), idx_base + (uint32_t)row);
-          } else if (valid && s * __builtin_amdgcn_rcpf(den) >= thr) {
-            float c = s / den;   // IEEE division, as the reference's elementwise kernel
-            c = fminf(fmaxf(c, -1.0f), 1.0f);
-            const uint64_t key = make_key(c, idx_base + (uint32_t)row);
-            if ((uint32_t)(key >> 32) >= th) tk.insert(key);
+            if (valid) {
+              const float den = cos_den(qn, nd);
+              a.all_keys[(size_t)qe * n + row] = make_key(fminf(fmaxf(s / den, -1.0f), 1.0f), idx_base + (uint32_t)row);
+            }
+          } else {
+            pass[e] = valid && s >= fmaf(thq, nd, th8);
           }
         } else {
-          const uint64_t key = make_key(s, idx_base + (uint32_t)row);
           if (DUMP && a.all_keys) {
-            if (valid) a.all_keys[(size_t)qe * n + row] = key;
-          } else if (valid && (uint32_t)(key >> 32) >= th) {
-            tk.insert(key);
+            if (valid) a.all_keys[(size_t)qe * n + row] = make_key(s, idx_base + (uint32_t)row);
+          } else {
+            pass[e] = valid && s >= thf;
+          }
+        }
+        anyp = anyp || pass[e];
+      }
+      if constexpr (!SCR) {
+        // the few scores that pass: their exact keys (IEEE division for cosine, as the reference's elementwise
+        // kernel), inserted when at or above the bar (ties on the score go on to the insert's 64-bit compares)
+        if (anyp) {
+#pragma unroll
+          for (int e = 0; e < DPL; ++e) {
+            if (pass[e]) {
+              float c = sc[e];
+              if constexpr (COS) {
+                c = c / cos_den(qn, ndv[e]);
+                c = fminf(fmaxf(c, -1.0f), 1.0f);
+              }
+              const uint64_t key = make_key(c, idx_base + (uint32_t)rows[e]);
+              if ((uint32_t)(key >> 32) >= th) tk.insert(key);
+            }
           }
         }
       }
   };
 
+  // Pipelined K-partial exchange (streaming passes; see the loop). The scheduler wave's next-chunk word is read one
+  // barrier later than it is published, which holds for chunks of >= 3 tiles (the dynamic schedule's 2-tile chunks,
+  // 4 slabs per row slice, keep the plain order).
+#ifndef RR_SK_PIPE
+#define RR_SK_PIPE 0   // measured: -2 % on the 64-slot pass (12-16 B of spills), within noise on the screen
+#endif
+  constexpr bool PIPE = MODE == 0 && RR_SK_PIPE && KT <= 16 && !(QH == 2 && DT == 2) && (SCHED == 0 || CT >= 3);   // (else spills)
+  int64_t pbase = 0;   // PIPE: the previous tile's first row and factor slot
+  int pts = 0;
+  // Stagger (streaming passes): waves 4-7 — the SIMD partners of waves 0-3 — run each tile's epilogue one tile
+  // late, after issuing the next tile's MFMAs, its summed scores kept in registers across the barrier. Partners
+  // that reach the same phase together (matrix work, epilogue, barrier) leave the matrix core idle while both run
+  // the epilogue's vector work; staggered, one wave's epilogue runs beside its partner's MFMAs. The lists see the
+  // same inserts in the same order: results are unchanged.
+#ifndef RR_SK_STAGGER
+#define RR_SK_STAGGER 2   // 0 off, 1 the 64-slot pass only, 2 every streaming pass
+#endif
+  constexpr bool STG = MODE == 0 && !PIPE && !(QH == 2 && DT == 2) && DT != 6 &&   // (those two spill with it)
+                       (RR_SK_STAGGER == 2 || (RR_SK_STAGGER == 1 && QH == 2));
+#ifndef RR_SK_STAGGER_PAR
+#define RR_SK_STAGGER_PAR 0   // A/B only: defer the odd waves instead of waves 4-7
+#endif
+  const bool defer = STG && (RR_SK_STAGGER_PAR ? (w & 1) != 0 : w >= 4);
+  float svd[DPL];
+  int64_t bsd = -1;   // first row of the deferred tile (-1: none)
+  int tsd = 0;        // its factor slot (4 slots: wave 0 refills a slot three tiles after its tile at the earliest)
+
+  // ---- sum the 8 K-partials of a tile (fixed order), then the metric epilogue --------------------------
+  auto write_partials = [&](float* rb, const f32x16 (&accs)[QH]) {
+#pragma unroll
+    for (int qh = 0; qh < QH; ++qh)
+#pragma unroll
+      for (int a4 = 0; a4 < 4; ++a4) {   // C/D map: acc[4a + i] = (doc 8a + 4h + i, query r)
+        const f32x4 v = {accs[qh][4 * a4], accs[qh][4 * a4 + 1], accs[qh][4 * a4 + 2], accs[qh][4 * a4 + 3]};
+        // 32 floats per (wave, query) row, its eight 16-byte chunks XOR-swizzled by the query index: the 8-lane
+        // groups of this ds_write_b128 and the epilogue's ds_read_b64 / ds_read_b128 groups are conflict-free
+        // (the +4-float padding it replaced left the reads 2-way conflicted: 1.6e8 of 5.0e8 LDS cycles at B = 64)
+        const int rq = 32 * qh + r;
+        *(f32x4*)(rb + (w * QS + rq) * kRedRow + 4 * ((2 * a4 + h) ^ (rq & 7))) = v;
+      }
+  };
+  // (two-float vectors: packed adds, each element summed in the same wave order)
+  auto read_partials = [&](const float* rb, float (&sv)[DPL]) {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    f32x2 acc2[DPL / 2];
+#pragma unroll
+    for (int ww = 0; ww < kWaves; ++ww) {   // fixed wave order: the same sums for any QH (wave 0's partial first)
+      const float* src = rb + (ww * QS + qe) * kRedRow + 4 * ((er >> 2) ^ (qe & 7)) + (er & 3);
+      if constexpr (DPL == 2) {
+        const f32x2 p = *(const f32x2*)src;
+        acc2[0] = ww ? acc2[0] + p : p;
+      } else {
+        const f32x4 p = *(const f32x4*)src;
+        const f32x2 p0 = {p[0], p[1]}, p1 = {p[2], p[3]};
+        acc2[0] = ww ? acc2[0] + p0 : p0;
+        acc2[1] = ww ? acc2[1] + p1 : p1;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < DPL; ++e) sv[e] = acc2[e >> 1][e & 1];
+  };
   SK_PROBE(1);
   int slot = 0, ti = 0, cpar = 0, ts = 0;   // ring slot, tile of the chunk, nxt parity, factor slot
   int64_t tcount = 0;                       // tiles done (reduction buffer parity)
@@ -886,7 +1015,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         }
         if (next_base >= 0) {
           if (FX && w == 0) {
-            issue_factors(next_base, ts == 2 ? 0 : ts + 1);
+            issue_factors(next_base, (ts + 1) & 3);
             n_is += 1;
           }
           issue(next_base, 0, slot);
@@ -921,7 +1050,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           }
           if (next_base >= 0) {
             if (FX && w == 0) {
-              issue_factors(next_base, ts == 2 ? 0 : ts + 1);
+              issue_factors(next_base, (ts + 1) & 3);
               extra0 += 1;
             }
             issue(next_base, 0, slot ^ 1);
@@ -1003,44 +1132,73 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       }
       slot ^= 1;
     });
+    if (defer && bsd >= 0) {   // the previous tile's epilogue, beside this tile's MFMAs
+      epilogue(svd, bsd, tsd);
+      bsd = -1;
+    }
 
-    // ---- sum the 8 K-partials of this tile (fixed order), then the metric epilogue --------------------
     float* rb = red + (red_bufs(RS, QH) == 2 ? (size_t)(tcount & 1) * kWaves * QS * kRedStride : 0);
-    if constexpr (red_bufs(RS, QH) == 1) {
-      if (tcount > 0) lds_barrier();   // every wave has read the previous tile's partials
-    }
+#if defined(RR_SK_DIAG) && (RR_SK_DIAG & 2)
+    if (MODE == 0) {   // diagnostic builds only: no K-partial exchange (the barrier stays), this wave's own partials
+      lds_barrier();
+      float sv[DPL];
 #pragma unroll
-    for (int qh = 0; qh < QH; ++qh)
-#pragma unroll
-      for (int a4 = 0; a4 < 4; ++a4) {   // C/D map: acc[4a + i] = (doc 8a + 4h + i, query r)
-        const f32x4 v = {accs[qh][4 * a4], accs[qh][4 * a4 + 1], accs[qh][4 * a4 + 2], accs[qh][4 * a4 + 3]};
-        // 32 floats per (wave, query) row, its eight 16-byte chunks XOR-swizzled by the query index: the 8-lane
-        // groups of this ds_write_b128 and the epilogue's ds_read_b64 / ds_read_b128 groups are conflict-free
-        // (the +4-float padding it replaced left the reads 2-way conflicted: 1.6e8 of 5.0e8 LDS cycles at B = 64)
-        const int rq = 32 * qh + r;
-        *(f32x4*)(rb + (w * QS + rq) * kRedRow + 4 * ((2 * a4 + h) ^ (rq & 7))) = v;
+      for (int e = 0; e < DPL; ++e) sv[e] = accs[e % QH][e];
+      epilogue(sv, base, ts);
+      ++tcount;
+      ts = (ts + 1) & 3;
+      if (!last_in_chunk) {
+        ++ti;
+        base += 32;
+        continue;
       }
-    lds_barrier();   // (also publishes wave 0's LDS-DMA factors and its next-chunk word)
-    float sv[DPL];
-#pragma unroll
-    for (int ww = 0; ww < kWaves; ++ww) {   // fixed wave order: the same sums for any QH (wave 0's partial first)
-      const float* src = rb + (ww * QS + qe) * kRedRow + 4 * ((er >> 2) ^ (qe & 7)) + (er & 3);
-      if constexpr (DPL == 2) {
-        const float2 p = *(const float2*)src;
-        sv[0] = ww ? sv[0] + p.x : p.x;
-        sv[1] = ww ? sv[1] + p.y : p.y;
+      if (next_chunk >= C) break;
+      chunk = next_chunk;
+      ti = 0;
+      cpar ^= 1;
+      base = chunk * CT * 32;
+      continue;
+    }
+#endif
+    if constexpr (PIPE) {
+      // Pipelined exchange: this tile's MFMAs are issued; the previous tile's partials are summed and its epilogue
+      // runs while they execute, then this tile's partials go to LDS. The barrier that publishes a tile's partials
+      // is passed one tile later, behind the next tile's matrix work, instead of right after the MFMAs drain.
+      if (tcount > 0) {
+        lds_barrier();   // every wave wrote the previous tile's partials (and wave 0 its LDS-DMA factors / nxt)
+        float sv[DPL];
+        const float* rp = red + (red_bufs(RS, QH) == 2 ? (size_t)((tcount - 1) & 1) * kWaves * QS * kRedStride : 0);
+        read_partials(rp, sv);
+        if constexpr (red_bufs(RS, QH) == 1) lds_barrier();   // every wave has read them: the block is free
+        write_partials(rb, accs);
+        epilogue(sv, pbase, pts);
       } else {
-        const f32x4 p = *(const f32x4*)src;
+        write_partials(rb, accs);
+      }
+      pbase = base;
+      pts = ts;
+    } else {
+      if constexpr (red_bufs(RS, QH) == 1) {
+        if (tcount > 0) lds_barrier();   // every wave has read the previous tile's partials
+      }
+      write_partials(rb, accs);
+      lds_barrier();   // (also publishes wave 0's LDS-DMA factors and its next-chunk word)
+      float sv[DPL];
+      read_partials(rb, sv);
+      if (defer) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) sv[e] = ww ? sv[e] + p[e] : p[e];
+        for (int e = 0; e < DPL; ++e) svd[e] = sv[e];
+        bsd = base;
+        tsd = ts;
+      } else {
+        epilogue(sv, base, ts);
       }
     }
-    epilogue(sv, base, ts);
     if (tcount == 0) SK_PROBE(2);
     if (MODE == 0 && tcount == 1) SK_PROBE(3);
     ++tcount;
     if constexpr (MODE == 1) break;
-    ts = ts == 2 ? 0 : ts + 1;
+    ts = (ts + 1) & 3;
     if (!last_in_chunk) {
       ++ti;
       base += 32;
@@ -1050,6 +1208,15 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       ti = 0;
       cpar ^= 1;
       base = chunk * CT * 32;
+    }
+  }
+  if (defer && bsd >= 0) epilogue(svd, bsd, tsd);   // the last tile's deferred epilogue
+  if constexpr (PIPE) {
+    if (tcount > 0) {   // the last tile's partials
+      lds_barrier();
+      float sv[DPL];
+      read_partials(red + (red_bufs(RS, QH) == 2 ? (size_t)((tcount - 1) & 1) * kWaves * QS * kRedStride : 0), sv);
+      epilogue(sv, pbase, pts);
     }
   }
   SK_PROBE(4);
@@ -1332,10 +1499,10 @@ hipError_t launch_metric(int metric, int ns, int kt, int grid, const SkArgs& a, 
 size_t sk_lds_bytes(int sdt, bool cos, int ring, int qslots) {
   (void)sdt;
   (void)cos;
-  // + per-row factors [3][2][32], next-chunk words [4], query scalars [3][qslots], MODE 1 scratch: W [8][32] +
+  // + per-row factors [4][2][32], next-chunk words [4], query scalars [3][qslots], MODE 1 scratch: W [8][32] +
   // akeys [32] keys, grow / gnorm / gvalid [32], xk [32] keys, the floors' and the list bounds' maxima, 2 ints
   const size_t verify = (size_t)(kWaves * 32 + 32 + 32 + 3) * 8 + 3 * 32 * 4;
-  return sk::ring_bytes(ring) + sk::red_bytes(ring, qslots / 32) + 3 * 64 * 4 + 4 * 4 + 3 * qslots * 4 + verify;
+  return sk::ring_bytes(ring) + sk::red_bytes(ring, qslots / 32) + 4 * 64 * 4 + 4 * 4 + 3 * qslots * 4 + verify;
 }
 
 bool sk_supports_64(int sdt) { return sdt == KDT_BF16 || sdt == KDT_F32_SPLIT; }

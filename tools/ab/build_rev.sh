@@ -1,10 +1,14 @@
 #!/bin/bash
 # Build the library from another git revision's sources into tools/ab/librag_retrieval_<name>.so (A/B arm).
-#   bash tools/ab/build_rev.sh <name> <rev> ["-DFOO=1 ..."]
+#   bash tools/ab/build_rev.sh <name> <rev> ["-DFOO=1 ..."]      (<rev> = . : the working tree's sources)
 set -e
 H=$(cd "$(dirname "$0")/../.." && pwd)
 T=$(mktemp -d)
-git -C "$H" archive "$2" include rag-serving-system_amd/csrc | tar -x -C "$T"
+if [ "$2" = . ]; then
+  mkdir -p "$T/rag-serving-system_amd" && cp -r "$H/include" "$T/" && cp -r "$H/rag-serving-system_amd/csrc" "$T/rag-serving-system_amd/"
+else
+  git -C "$H" archive "$2" include rag-serving-system_amd/csrc | tar -x -C "$T"
+fi
 B=$T/build
 mkdir -p "$B"
 F="-O3 -std=c++17 -Wno-unused-value -Wno-unused-result -fPIC -I$T/include -I$T/rag-serving-system_amd/csrc $3"
