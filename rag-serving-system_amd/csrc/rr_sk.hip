@@ -89,6 +89,19 @@ __device__ unsigned long long vdiag[32 * 8];
   } while (0)
 #endif
 
+// Per-phase cycle counters per wave (diagnostic builds with RR_SK_DIAG & 4 only, tools/kbench_cfg5.hip):
+// [workgroup][wave][slab wait, slab loop rest, barrier A, write + barrier B, partial reads, epilogue, tiles, -]
+#if defined(RR_SK_DIAG) && (RR_SK_DIAG & 4)
+__device__ unsigned long long phase_cycles[4096 * 9 * 8];
+#define PH_NOW() ((unsigned long long)__builtin_amdgcn_s_memtime())
+#define PH_ADD(i, v) (ph[i] += (v))
+#else
+#define PH_NOW() 0ull
+#define PH_ADD(i, v) \
+  do {              \
+  } while (0)
+#endif
+
 constexpr int kSlabRowBytes = 128;                // contiguous bytes of one row per slab
 constexpr int kSlabBytes = 32 * kSlabRowBytes;    // 4 KiB
 constexpr int kRedStride = 36;                    // floats allocated per (wave, query) block of 32 rows
@@ -984,6 +997,11 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #pragma unroll
     for (int e = 0; e < DPL; ++e) sv[e] = acc2[e >> 1][e & 1];
   };
+#if defined(RR_SK_DIAG) && (RR_SK_DIAG & 4)
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  unsigned long long ph_t = PH_NOW();
+  (void)ph_t;
   SK_PROBE(1);
   int slot = 0, ti = 0, cpar = 0, ts = 0;   // ring slot, tile of the chunk, nxt parity, factor slot
   int64_t tcount = 0;                       // tiles done (reduction buffer parity)
@@ -1032,7 +1050,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     static_for<0, NS>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       if constexpr (MODE == 0 && LA == 2) {
+        const unsigned long long pw0 = PH_NOW();
         wait_vm_n(pend);   // slab j landed (loads complete in order; the pend ops issued after it may not have)
+        PH_ADD(0, PH_NOW() - pw0);
       } else if constexpr (MODE == 0) {
         // keep one slab in flight: issue the next slab (of this tile, or slab 0 of the next tile with wave 0
         // issuing that tile's factors first) into the slot consumed last, then wait for this one. Wave 0's
@@ -1058,7 +1078,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           }
         }
         if (nw) nw += w == 0 ? extra0 : 0;
+        const unsigned long long pw0 = PH_NOW();
         wait_vm_n(nw);
+        PH_ADD(0, PH_NOW() - pw0);
       }
       const char* sl = ring + slot * kSlabBytes;
       if constexpr (DT == 0) {
@@ -1132,9 +1154,15 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       }
       slot ^= 1;
     });
+    unsigned long long pt1 = PH_NOW();
+    (void)pt1;
+    PH_ADD(1, pt1 - ph_t);
     if (defer && bsd >= 0) {   // the previous tile's epilogue, beside this tile's MFMAs
       epilogue(svd, bsd, tsd);
       bsd = -1;
+      const unsigned long long pe = PH_NOW();
+      PH_ADD(5, pe - pt1);
+      pt1 = pe;
     }
 
     float* rb = red + (red_bufs(RS, QH) == 2 ? (size_t)(tcount & 1) * kWaves * QS * kRedStride : 0);
@@ -1181,10 +1209,17 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       if constexpr (red_bufs(RS, QH) == 1) {
         if (tcount > 0) lds_barrier();   // every wave has read the previous tile's partials
       }
+      const unsigned long long pt2 = PH_NOW();
       write_partials(rb, accs);
       lds_barrier();   // (also publishes wave 0's LDS-DMA factors and its next-chunk word)
+      const unsigned long long pt3 = PH_NOW();
       float sv[DPL];
       read_partials(rb, sv);
+#if defined(RR_SK_DIAG) && (RR_SK_DIAG & 4)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int e = 0; e < DPL; ++e) asm volatile("" : "+v"(sv[e]));
+#endif
+      const unsigned long long pt4 = PH_NOW();
       if (defer) {
 #pragma unroll
         for (int e = 0; e < DPL; ++e) svd[e] = sv[e];
@@ -1193,6 +1228,13 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       } else {
         epilogue(sv, base, ts);
       }
+      const unsigned long long pt5 = PH_NOW();
+      PH_ADD(2, pt2 - pt1);
+      PH_ADD(3, pt3 - pt2);
+      PH_ADD(4, pt4 - pt3);
+      PH_ADD(5, pt5 - pt4);
+      PH_ADD(6, 1);
+      ph_t = pt5;
     }
     if (tcount == 0) SK_PROBE(2);
     if (MODE == 0 && tcount == 1) SK_PROBE(3);
@@ -1219,6 +1261,10 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       epilogue(sv, pbase, pts);
     }
   }
+#if defined(RR_SK_DIAG) && (RR_SK_DIAG & 4)
+  if (MODE == 0 && lane == 0)
+    for (int i = 0; i < 8; ++i) phase_cycles[((size_t)blockIdx.x * 9 + w) * 8 + i] = ph[i];
+#endif
   SK_PROBE(4);
 
   // ---- per query: merge its LPQ lane lists (KT rounds of an LPQ-lane max; keys are unique) -------------

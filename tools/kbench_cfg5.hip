@@ -136,6 +136,27 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       v.ms.push_back(ms / reps);
     }
+#if defined(RR_SK_DIAG) && (RR_SK_DIAG & 4)
+  // per-phase cycles per tile and wave (s_memtime around each phase; the timers themselves cost a little)
+  for (int vi = 0; vi < 2; ++vi) {
+    CK(vs[vi].run());
+    CK(hipStreamSynchronize(s));
+    std::vector<unsigned long long> h((size_t)grid * 9 * 8);
+    CK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(rr::sk::phase_cycles), h.size() * 8));
+    for (int grp = 0; grp < 2; ++grp) {   // waves 0-3, waves 4-7 (the stagger defers the second group)
+      double acc[8] = {0};
+      for (int g = 0; g < grid; ++g)
+        for (int w = 4 * grp; w < 4 * grp + 4; ++w)
+          for (int i = 0; i < 8; ++i) acc[i] += (double)h[((size_t)g * 9 + w) * 8 + i];
+      const double tiles = acc[6] > 0 ? acc[6] : 1;
+      printf("{\"phases\": \"%s\", \"waves\": \"%d-%d\", \"cycles_per_tile_wave\": {\"slab_wait\": %.0f, "
+             "\"slab_loop_incl_wait\": %.0f, \"barrier_A\": %.0f, \"write_barrier_B\": %.0f, \"partial_reads\": %.0f, "
+             "\"epilogue\": %.0f}, \"tiles_per_wave\": %.1f}\n", vs[vi].name.c_str(), 4 * grp, 4 * grp + 3,
+             acc[0] / tiles, acc[1] / tiles, acc[2] / tiles, acc[3] / tiles, acc[4] / tiles, acc[5] / tiles,
+             tiles / (grid * 4.0));
+    }
+  }
+#endif
   for (auto& v : vs) {
     std::vector<double> m = v.ms;
     std::sort(m.begin(), m.end());
