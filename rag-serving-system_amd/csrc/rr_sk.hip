@@ -70,7 +70,15 @@ __device__ unsigned long long probe[4096 * 8];
   do {                                                                \
     if (threadIdx.x == 0) probe[blockIdx.x * 8 + (i)] = wall_clock64(); \
   } while (0)
+__device__ unsigned long long probe2[4096 * 8];   // verify list-merge sub-phases
+#define SK_PROBE2(i)                                                   \
+  do {                                                                 \
+    if (threadIdx.x == 0) probe2[blockIdx.x * 8 + (i)] = wall_clock64(); \
+  } while (0)
 #else
+#define SK_PROBE2(i) \
+  do {               \
+  } while (0)
 #define SK_PROBE(i) \
   do {              \
   } while (0)
@@ -261,8 +269,6 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
   uint64_t* cand = scratch + kThreads;
   uint64_t* hs = cand + KT * KT;
   int* cnt = (int*)(hs + 1);
-  unsigned long long* fmax = (unsigned long long*)(hs + 2);
-  unsigned long long* tmax = (unsigned long long*)(hs + 3);
   constexpr int LS = KT + 1;   // list stride: KT keys + the workgroup's floor
   TopK<KT> tk;
   uint64_t fl = 0, tl = 0;     // floors; and every list's own bound, max(its KT-th key, its floor) (wide verify)
@@ -285,28 +291,65 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
       tk.insert(key);
     }
   }
+  SK_PROBE2(0);   // lists loaded (this thread's)
   const int nl = nlists < kThreads ? nlists : kThreads;
+  const int nlp = (nl + 7) & ~7;   // heads padded with empty keys to whole 8-key groups
+  const int lane = tid & 63, wv = tid >> 6;
+  uint64_t* fw = hs + 4;             // [kWaves] per-wave floor maxima, then [kWaves] list-bound maxima
+  uint64_t* tw = fw + kWaves;
   if (tid == 0) {
     hs[0] = 0;
     cnt[0] = 0;
-    *fmax = 0;
-    *tmax = 0;
   }
-  if (tid < nl) heads[tid] = tk.v[0];
+  if (tid < nlp) heads[tid] = tk.v[0];   // (threads past the lists hold empty lists)
+  // the floors' and the list bounds' maxima: a wave-wide max, one LDS word per wave (not one LDS atomic per list on a
+  // single address: 2 x 256 of those serialised to ~7 us)
+  const uint64_t fwv = wave_max_u64(fl), twv = wave_max_u64(tl);
+  if (lane == 0) {
+    fw[wv] = fwv;
+    tw[wv] = twv;
+  }
   __syncthreads();
-  if (fl != 0) __hip_atomic_fetch_max(fmax, (unsigned long long)fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (tl != 0) __hip_atomic_fetch_max(tmax, (unsigned long long)tl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (tid < nl && tk.v[0] != 0) {
-    const uint64_t me = tk.v[0];
+  SK_PROBE2(1);   // heads in LDS
+  // each head's rank among the heads: 8 heads per step from broadcast 16-byte LDS reads; with <= 256 lists two threads
+  // per head, each scanning half of them (every wave busy), their counts added through LDS
+  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+  const u64x2* hv = (const u64x2*)heads;
+  auto count_above = [&](uint64_t me, int j0, int j1) {
     int rank = 0;
-    for (int j = 0; j < nl; ++j) rank += heads[j] > me ? 1 : 0;   // (broadcast LDS reads)
-    if (rank == KT - 1) hs[0] = me;
+    for (int j = j0; j < j1; j += 4) {
+      u64x2 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = hv[j + u];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) rank += (x[u][0] > me ? 1 : 0) + (x[u][1] > me ? 1 : 0);
+    }
+    return rank;
+  };
+  if (nlp <= kThreads / 2) {
+    int* part = (int*)(tw + kWaves);   // [kThreads / 2] the second half's counts
+    const int hh = tid & (kThreads / 2 - 1), half = tid / (kThreads / 2);
+    const uint64_t me = heads[hh];
+    const int g8 = nlp / 16 * 4;       // the first half's end, in 16-byte units (multiple of 4)
+    int rank = 0;
+    if (hh < nl && me != 0) rank = half ? count_above(me, g8, nlp / 2) : count_above(me, 0, g8);
+    if (half) part[hh] = rank;
+    __syncthreads();
+    if (!half && hh < nl && me != 0 && rank + part[hh] == KT - 1) hs[0] = me;
+  } else if (tid < nl && tk.v[0] != 0) {
+    if (count_above(tk.v[0], 0, nlp / 2) == KT - 1) hs[0] = tk.v[0];
   }
   __syncthreads();
   if (tid == 0) {
-    *floor_out = *fmax;
-    *tail_out = *tmax;
+    uint64_t f = 0, t = 0;
+    for (int i = 0; i < kWaves; ++i) {
+      f = umax64(f, fw[i]);
+      t = umax64(t, tw[i]);
+    }
+    *floor_out = f;
+    *tail_out = t;
   }
+  SK_PROBE2(2);   // H known
   const uint64_t th = hs[0];
   if (tid < nl && tk.v[0] != 0 && tk.v[0] >= th) {
     int c = 0;
@@ -318,6 +361,7 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
       if (i < c) cand[pos + i] = tk.v[i];
   }
   __syncthreads();
+  SK_PROBE2(3);   // candidates appended
   const int m = cnt[0];
   if (tid < KT && tid >= m) akeys[tid] = 0;   // fewer than KT keys in all: empty tail
   for (int c = tid; c < m; c += kThreads) {
@@ -724,7 +768,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // ---- MODE 1: this query's candidates (the queries' fragments and scalars above are already built, so
   // their loads overlapped the list loads), then their rows straight into registers ---------------------------
   if constexpr (MODE == 1) {
-    static_assert((size_t)(kThreads + KT * KT + 4) * 8 <= kWideListOff, "verify merge scratch in the slab ring");
+    static_assert((size_t)(kThreads + KT * KT + 4 + 2 * kWaves) * 8 + kThreads / 2 * 4 <= kWideListOff,
+                  "verify merge scratch in the slab ring");
     SK_PROBE(6);
     merge_lists_for_query<KT>(a.vin, a.nlists, QS, vq, (uint64_t*)smem, akeys, vfloor, vtail);
     SK_PROBE(7);

@@ -9,7 +9,7 @@ read DOCS B K DT <<< "$2"
 shift 2
 W="--docs $DOCS --dtype $DT --batch $B --k $K --no-cpu-baseline --variants= --ingest-rows 0 --no-pmc --steps ${STEPS:-40} --warmup ${WARMUP:-10} --latency-steps 5 --steady-steps 60"
 echo "# $DOCS rows, batch $B, k $K, $DT: value kernel_us frac | steady value kernel_us frac" >> "$OUT"
-for rep in 1 2; do
+for rep in $(seq ${REPS:-2}); do
   for arm in "$@"; do
     if [ $arm = new ]; then L=$R/rag-serving-system_amd/librag_retrieval.so; else L=$R/tools/ab/librag_retrieval_$arm.so; fi
     RR_LIBRARY=$L timeout -k 10 200 python3 "$R/bench.py" --gpus 1 $W > /tmp/ab.json 2>/tmp/ab.err || { tail -5 /tmp/ab.err >> "$OUT"; exit 1; }

@@ -77,6 +77,15 @@ int main(int argc, char** argv) {
       std::sort(x.begin(), x.end());
       printf(", \"%s_us\": [%.2f, %.2f]", nm[i], x[x.size() / 2], x.back());
     }
+    std::vector<unsigned long long> h2((size_t)32 * 8);
+    CK(hipMemcpyFromSymbol(h2.data(), HIP_SYMBOL(rr::sk::probe2), h2.size() * 8));
+    const char* nm2[] = {"m_lists_loaded", "m_heads", "m_H", "m_cands"};
+    for (int i = 0; i < 4; ++i) {
+      std::vector<double> x;
+      for (int g = 0; g < 32; ++g) x.push_back((h2[g * 8 + i] - t0) / 100.0);
+      std::sort(x.begin(), x.end());
+      printf(", \"%s_us\": [%.2f, %.2f]", nm2[i], x[x.size() / 2], x.back());
+    }
     printf("}\n");
   }
   return 0;
