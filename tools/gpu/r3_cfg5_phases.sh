@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 rm -f gpurun_out/cfg5_phases.jsonl
-for D in d4 d4stg0; do
+for D in d4; do
   echo "== $D" >> gpurun_out/cfg5_phases.jsonl
   timeout -k 10 120 tools/kbench_cfg5_$D 6250000 5 >> gpurun_out/cfg5_phases.jsonl || exit 1
 done

@@ -151,9 +151,9 @@ int main(int argc, char** argv) {
       const double tiles = acc[6] > 0 ? acc[6] : 1;
       printf("{\"phases\": \"%s\", \"waves\": \"%d-%d\", \"cycles_per_tile_wave\": {\"slab_wait\": %.0f, "
              "\"slab_loop_incl_wait\": %.0f, \"barrier_A\": %.0f, \"write_barrier_B\": %.0f, \"partial_reads\": %.0f, "
-             "\"epilogue\": %.0f}, \"tiles_per_wave\": %.1f}\n", vs[vi].name.c_str(), 4 * grp, 4 * grp + 3,
-             acc[0] / tiles, acc[1] / tiles, acc[2] / tiles, acc[3] / tiles, acc[4] / tiles, acc[5] / tiles,
-             tiles / (grid * 4.0));
+             "\"epilogue\": %.0f}, \"insert_executions_per_tile_wave\": %.3f, \"tiles_per_wave\": %.1f}\n",
+             vs[vi].name.c_str(), 4 * grp, 4 * grp + 3, acc[0] / tiles, acc[1] / tiles, acc[2] / tiles, acc[3] / tiles,
+             acc[4] / tiles, acc[5] / tiles, acc[7] / tiles, tiles / (grid * 4.0));
     }
   }
 #endif
