@@ -534,6 +534,31 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         issue(base, 1, 1);
         pend = 4;
       }
+#ifndef RR_SK_WARM
+#define RR_SK_WARM 0   // A/B only: 3 measured 4-5 % slower at 125k rows (profiles/r03/c/ab_warm_rejected.txt)
+#endif
+      // Start-up warming (A/B): the next RR_SK_WARM tiles of the first chunk touched into L2 (one 4-byte LDS-DMA load
+      // per 128-byte line of this wave's slice, landing in a scratch word block nobody reads) while the query
+      // fragments are built. Waits only grow (the slab waits count these as later ops): results are unchanged.
+      if constexpr (RR_SK_WARM > 0 && LA == 2) {
+        const int tic0 = (int)(C - chunk == 1 ? T - chunk * CT : CT);
+        const unsigned warm_lds = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)((char*)(qexp + QS) + 2048));
+        int nwarm = 0;
+#pragma unroll
+        for (int t = 1; t <= RR_SK_WARM; ++t) {
+          if (t < tic0) {
+            int64_t row = base + 32 * t + (lane & 31);
+            row = row < n ? row : n - 1;
+#pragma unroll
+            for (int j0 = 0; j0 < NS; j0 += 2) {
+              const int j = j0 + (lane >> 5) < NS ? j0 + (lane >> 5) : NS - 1;
+              glds4(wave_src + row * row_bytes + j * kSlabRowBytes, warm_lds);
+              ++nwarm;
+            }
+          }
+        }
+        pend += nwarm;
+      }
     }
   }
   // ---- query side: this wave's K-slice of every query as MFMA B operands, |q| and split exponents.
