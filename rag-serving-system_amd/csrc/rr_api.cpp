@@ -194,6 +194,7 @@ struct rr_handle {
   int dyn_sched = 1;            // split-K kernels: dynamic chunk schedule (rr_set_schedule)
   int streams = 2;              // compute streams for screened blocks (rr_set_compute_streams)
   int screen_grid = 1 << 30;    // screen workgroups at most (A/B: RR_SCREEN_GRID)
+  int verify_cus = 32;           // (kVerifyCUs) CUs an overlapping screen leaves to the other stream's verify (A/B: RR_VERIFY_CUS)
   int xslots = kXSlots;         // pipelined-exchange buffer sets in use (A/B: RR_X_SLOTS, 2..kXSlots)
   int x_delay_us = 0;           // A/B: RR_X_EXCHANGE_DELAY_US, a stand-in for a slower exchange
   int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy)
@@ -852,7 +853,7 @@ bool two_streams(const rr_handle* h, const Shard&) { return h->streams == 2; }
 // completed: a single search, or the first of a burst), so nothing overlaps this one and every CU screens.
 int screen_grid(const rr_handle* h, const Shard& s, bool alone) {
   int g = s.cand_grid;
-  if (two_streams(h, s) && !alone) g = std::max(g / 2, g - kVerifyCUs);
+  if (two_streams(h, s) && !alone) g = std::max(g / 2, g - h->verify_cus);
   return (int)std::max<int64_t>(1, std::min<int64_t>(std::min(g, h->screen_grid), (s.rows() + 31) / 32));
 }
 // Stream index of a screened block of parity p, and a stream by index.
@@ -1395,6 +1396,7 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   }
   if (const char* e = getenv("RR_COMPUTE_STREAMS")) h->streams = atoi(e) == 1 ? 1 : 2;   // (A/B)
   if (const char* e = getenv("RR_SCREEN_GRID")) h->screen_grid = std::max(1, atoi(e));               // (A/B)
+  if (const char* e = getenv("RR_VERIFY_CUS")) h->verify_cus = std::max(0, atoi(e));                 // (A/B)
   if (const char* e = getenv("RR_X_SLOTS")) h->xslots = std::min(kXSlots, std::max(2, atoi(e)));     // (A/B)
   if (const char* e = getenv("RR_X_EXCHANGE_DELAY_US")) h->x_delay_us = std::min(1000, std::max(0, atoi(e)));
   if (const char* e = getenv("RR_DIST_TIMEOUT_MS")) h->timeout_ms = std::max(0, atoi(e));
