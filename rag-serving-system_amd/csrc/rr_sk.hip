@@ -987,9 +987,22 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
             pass[e] = valid && s >= thf;
           }
         }
+        if constexpr (!SCR && KT > 16) {
+          // (32-entry lists: the insert right here — keeping the scores for a later pass spills those kernels)
+          if (pass[e]) {
+            float c = s;
+            if constexpr (COS) {
+              c = c / cos_den(qn, nd);
+              c = fminf(fmaxf(c, -1.0f), 1.0f);
+            }
+            const uint64_t key = make_key(c, idx_base + (uint32_t)row);
+            if ((uint32_t)(key >> 32) >= th) tk.insert(key);
+          }
+          pass[e] = false;
+        }
         anyp = anyp || pass[e];
       }
-      if constexpr (!SCR) {
+      if constexpr (!SCR && KT <= 16) {
         // the few scores that pass: their exact keys (IEEE division for cosine, as the reference's elementwise
         // kernel), inserted when at or above the bar (ties on the score go on to the insert's 64-bit compares)
         if (anyp) {
@@ -1029,7 +1042,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #ifndef RR_SK_STAGGER
 #define RR_SK_STAGGER 2   // 0 off, 1 the 64-slot pass only, 2 every streaming pass
 #endif
-  constexpr bool STG = MODE == 0 && !PIPE && !(QH == 2 && DT == 2) && DT != 6 &&   // (those two spill with it)
+  constexpr bool STG = MODE == 0 && !PIPE && !(QH == 2 && DT == 2) && DT != 6 && KT <= 16 &&   // (measured)
                        (RR_SK_STAGGER == 2 || (RR_SK_STAGGER == 1 && QH == 2));
 #ifndef RR_SK_STAGGER_PAR
 #define RR_SK_STAGGER_PAR 0   // A/B only: defer the odd waves instead of waves 4-7
