@@ -157,6 +157,24 @@ __device__ __forceinline__ void glds16s(const void* sbase, unsigned voff, unsign
       : "memory");
 }
 
+// One whole slab (4 x 8 rows x 128 B) from one scalar base: per-lane offsets v0..v3 (row groups 0, 8, 16, 24), LDS
+// destinations lds, lds + 1 KiB, ... M0 is saved, stepped and restored inside the one statement, with one leading
+// lgkmcnt(0) (this wave's ds_reads of the slot): a third of the scalar instructions of four glds16s calls.
+__device__ __forceinline__ void glds16s_slab(const void* sbase, unsigned v0, unsigned v1, unsigned v2, unsigned v3,
+                                             unsigned lds) {
+  unsigned keep;
+  asm volatile(
+      "s_waitcnt lgkmcnt(0)\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %5 nt\n\t"
+      "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %5 nt\n\t"
+      "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %5 nt\n\t"
+      "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %5 nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(v0), "v"(v1), "v"(v2), "v"(v3), "s"(sbase), "s"(lds)
+      : "memory", "scc");
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
@@ -460,15 +478,24 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 
   // per-lane part of a slab address: row rl of each 8-row group, swizzled 16-byte column (< 8 rows: 32-bit)
   const unsigned lane_off = (unsigned)(rl * row_bytes + ((cl ^ rl) << 4));
+  const unsigned row8 = (unsigned)(8 * row_bytes);   // (row groups 8, 16, 24 of a tile: offsets < 2^32)
   const char* wave_src = corpus + (size_t)w * KS;
   auto issue = [&](int64_t base, int j, int slot) {   // slab j (this wave's K-slice) of the tile at row base
     if (base + 32 <= n) {   // whole tile (workgroup-uniform): scalar addresses
       const int64_t sb = __builtin_amdgcn_readfirstlane((int)(base >> 32)) * 0x100000000ll +
                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)base);
+#ifndef RR_SK_SLAB_ASM
+#define RR_SK_SLAB_ASM 0   // A/B: 1 = one inline-asm statement per slab (not yet measured on the GPU)
+#endif
+      if constexpr (RR_SK_SLAB_ASM) {
+        glds16s_slab(wave_src + sb * row_bytes + j * kSlabRowBytes, lane_off, lane_off + row8, lane_off + 2 * row8,
+                     lane_off + 3 * row8, ring_lds + slot * kSlabBytes);
+      } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        glds16s(wave_src + (sb + 8 * i) * row_bytes + j * kSlabRowBytes, lane_off,
-                ring_lds + slot * kSlabBytes + i * 1024);
+        for (int i = 0; i < 4; ++i)
+          glds16s(wave_src + (sb + 8 * i) * row_bytes + j * kSlabRowBytes, lane_off,
+                  ring_lds + slot * kSlabBytes + i * 1024);
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
