@@ -149,10 +149,11 @@ def timed_steps(ix, k, steps, warmup, dist, cuda_sync, every=1, acct=None):
     owed = int(sum_over_ranks(dist, float(max(0, (f1 - f0) - (r1 - r0)))))
     if owed:
         ix.set_timing(False)
+        prev = ix.kernel
         ix.set_kernel("exact")
         for _ in range(owed):
             ix.search_staged(k)
-        ix.set_kernel("auto")
+        ix.set_kernel(prev)
     ix.synchronize()
     cuda_sync()
     barrier(dist)
@@ -202,6 +203,9 @@ def main() -> None:
     ap.add_argument("--steady-steps", type=int, default=300,
                     help="back-to-back steps timed again after the latency loop (steady-state rate, reported "
                          "beside value)")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "exact", "fused"],
+                    help="similarity kernel of the timed loops (rr_set_kernel; A/B and counter passes: `exact` = the "
+                         "one-pass exact fp32 kernel without the screen)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--exchange-1rank", action="store_true",
                     help="N=1: run the multi-GPU data path anyway (a 1-rank RCCL communicator: per-block all-gather "
@@ -226,12 +230,8 @@ def main() -> None:
         sys.exit(spawn_ranks(args.gpus))
     from rag_service_amd.dist import env_rank_world
     rank, world, _ = env_rank_world()
-    if world > 1:
-        # Before the HIP runtime starts (it reads this once): one hardware queue per stream. With the default 4, the
-        # RCCL communicators' internal streams share queues with the compute streams (profiles/r03/trace: the second
-        # lane's communicator landed on the second compute stream's queue), and an all-gather waiting for its peers
-        # at the head of a shared, in-order queue would hold the screens queued behind it.
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+    # (No GPU_MAX_HW_QUEUES override: the library's streams take the runtime's high-priority queue pool, which RCCL's
+    # internal streams never share at any queue count; DESIGN §5 "Hardware queues", profiles/r04/queues/.)
     stage = {"stage": "start"}
     try:
         run(args, stage)
@@ -290,8 +290,12 @@ def run(args, stage: dict) -> None:
         rccl_ranks = ix.dist_info()[0]
     if world > 1:   # the library's waits on RCCL work: a third of the control-plane deadline, at most 120 s
         ix.set_timeout(int(min(120.0, args.dist_timeout_s / 3) * 1000))
+    # the hardware queues the handle's four streams dispatch to (distinct = none shares an in-order queue)
+    queues = ix.stream_queues(0)
     stage["stage"] = "corpus fill"
     ix.fill_synthetic(_lib.RR_SYNTH_UNIT_NORM, 1234, args.docs, args.dim)
+    if args.kernel != "auto":
+        ix.set_kernel(args.kernel)
     sb, se = ix.shard_range(0)
     rng = np.random.default_rng(5678)
     q = rng.standard_normal((args.batch, args.dim)).astype(np.float32)
@@ -391,7 +395,7 @@ def run(args, stage: dict) -> None:
         del host
 
     variants = {}
-    if world == 1 and args.dtype == "fp32" and args.variant_steps > 0:
+    if world == 1 and args.dtype == "fp32" and args.variant_steps > 0 and args.kernel == "auto":
         # the one-pass exact fp32 kernel (RR_KERNEL_EXACT, DT 3) on the same handle: it streams the fp32 rows the
         # reference streams (retriever.py:600), and it is what a flagged block's re-run and any corpus the screen
         # cannot prune cost
@@ -468,6 +472,7 @@ def run(args, stage: dict) -> None:
             "exchange": ("rccl ncclAllGather of per-shard top-k keys, device merge on every rank"
                          if world > 1 or rccl_ranks else "none (one shard)"),
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default (4)"),
+            "stream_queues_distinct": len(set(queues)),
             "rccl_ranks": rccl_ranks,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -552,7 +557,7 @@ def pmc_counters(args, kernel_s):
            sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "3", "--warmup", "1",
            "--latency-steps", "1", "--no-cpu-baseline", "--docs", str(args.docs), "--dim", str(args.dim),
            "--batch", str(args.batch), "--k", str(args.k), "--dtype", args.dtype, "--metric", args.metric,
-           "--variants", ""]
+           "--variants", "", "--kernel", args.kernel]
     try:
         subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
         vals = {}

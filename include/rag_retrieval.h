@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 5
+#define RR_ABI_VERSION 6
 
 /* error codes */
 #define RR_OK             0
@@ -50,9 +50,9 @@ extern "C" {
 #define RR_E_STATE       -4   /* call out of order (search before load, ...) */
 #define RR_E_UNSUPPORTED -5   /* valid request outside what this build implements */
 #define RR_E_OOM         -6   /* device allocation failed */
-#define RR_E_TIMEOUT     -7   /* multi-process mode: device work (an RCCL all-gather waiting for its peers) did not
-                                 complete within the handle's deadline (rr_set_timeout). The handle is then FAILED:
-                                 every later call returns RR_E_STATE; rr_destroy aborts its communicators and
+#define RR_E_TIMEOUT     -7   /* device work (an RCCL all-gather waiting for its peers; a stream that never drains)
+                                 did not complete within the handle's deadline (rr_set_timeout). The handle is then
+                                 FAILED: every later call returns RR_E_STATE; rr_destroy aborts its communicators and
                                  releases nothing else (the process is expected to exit) */
 
 /* corpus storage dtype in HBM (4 bytes per element for both fp32 forms, 2 for bf16) */
@@ -136,6 +136,13 @@ int rr_info(const rr_handle* h, int64_t* n_total, int32_t* d, int32_t* n_local_s
 
 /* Range [begin, end) of global rows held by local shard `i`. */
 int rr_shard_range(const rr_handle* h, int i, int64_t* begin, int64_t* end);
+
+/* Overwrite existing corpus rows in place: host_rows (n_rows x d fp32) replace the rows at the given global indices
+ * (each in [0, n_total); a repeated index keeps its last row). Rows outside the local shards are skipped, so every
+ * rank of a world may pass the same list. Converted and indexed exactly like loaded rows (storage dtype, per-row
+ * norms, the screening copy). Settles and synchronises the handle first. (The reference has no update path: its
+ * corpus is replaced by reloading, retriever.py:576-582; rr_load stays that path.) */
+int rr_update_rows(rr_handle* h, const float* host_rows, const int64_t* row_idx, int64_t n_rows, int32_t d);
 
 /* Copy rows [row_begin, row_begin + n_rows) of the device-resident corpus back to host as fp32
  * (bf16 corpora are widened). The rows must lie in local shards. Test/diagnostic use. */
@@ -226,20 +233,28 @@ int rr_screen_stats(rr_handle* h, int64_t* blocks, int64_t* fallbacks);
  * settles the last search. Any pointer may be null. */
 int rr_screen_counts(rr_handle* h, int64_t* blocks, int64_t* flagged, int64_t* reruns, int64_t* wide_slots);
 
-/* The screen's adaptive state (fp32 storage): *full_lists = 1 once flagged blocks made the handle switch the screen's
+/* The screen's adaptive state (fp32 storage): *full_lists = 1 once re-run blocks made the handle switch the screen's
  * per-lane lists from 4 keys (+ a floor) to the full list width; *pause_left = search blocks still to run with the
- * one-pass exact kernel because the screen could not prune this corpus (one process per world only); *pauses = how
- * often that happened. Reset at every load. Any pointer may be null. */
+ * one-pass exact kernel because the screen could not prune this corpus; *pauses = how often that happened. Decided
+ * from the searches whose results were collected (rr_fetch_results, rr_synchronize, rr_search, rr_wait), whose
+ * completeness flag is exchanged between shards: every rank of a world decides identically. Reset at every load.
+ * Any pointer may be null. */
 int rr_screen_state(rr_handle* h, int32_t* full_lists, int64_t* pause_left, int64_t* pauses);
 
-/* ---- multi-process deadline -------------------------------------------------------------------------- */
+/* ---- deadline ---------------------------------------------------------------------------------------- */
 
-/* Deadline (milliseconds, 0 = none) of every host wait on this handle's device work in multi-process mode
- * (rr_init_dist): synchronisation, result fetches, rr_wait, query staging and the load-time agreement between
- * ranks. Device work that does not complete in time — an all-gather whose peers never arrive — makes the call
- * return RR_E_TIMEOUT naming the rank and the search block, and fails the handle. Default 120000; the
- * environment variable RR_DIST_TIMEOUT_MS overrides it at rr_create. Ignored without rr_init_dist. */
+/* Deadline (milliseconds, 0 = the runtime's unbounded blocking waits) of every host wait on this handle's device
+ * work, in both modes: synchronisation, result fetches, rr_wait, query staging, corpus upload / fill and the
+ * load-time agreement between ranks. Device work that does not complete in time — an all-gather whose peers never
+ * arrive, a stream that never drains — makes the call return RR_E_TIMEOUT naming the rank (multi-process) or the
+ * local shard, its device, the stream and the newest search block, and fails the handle. Default 120000; the
+ * environment variable RR_TIMEOUT_MS (or its round-3 name RR_DIST_TIMEOUT_MS) overrides it at rr_create. */
 int rr_set_timeout(rr_handle* h, int32_t ms);
+
+/* Diagnostic: the hardware (AQL) queue each of local shard `i`'s four streams dispatches to — out[0] compute
+ * stream 0, out[1] compute stream 1, out[2] exchange lane 0, out[3] exchange lane 1 — as queue addresses (equal
+ * addresses = one shared in-order queue). Shards on one device share one set of streams. Synchronises the handle. */
+int rr_stream_queues(rr_handle* h, int i, uint64_t* out);
 
 /* ---- timing (benchmarks) ----------------------------------------------------------------------- */
 

@@ -57,6 +57,11 @@ constexpr int kXSlots = 4;   // pipelined-exchange buffer sets (Shard::px_keys)
 struct Shard {
   int dev = 0;
   int cus = 256;
+  // Streams (stream, cstream2, xstream, xstream2): one set per DEVICE. Shards on the same device (a test layout of
+  // the single-process exchange) share the first one's set (own_streams false): their work serialises on the
+  // device anyway, and no stream ever waits on another stream's event across shards of one device (DESIGN §5,
+  // "Hardware queues").
+  bool own_streams = true;
   hipStream_t stream = nullptr;
   int64_t row_begin = 0, row_end = 0;   // global rows held
   void* corpus = nullptr;                // [rows][d] fp32 or bf16
@@ -65,7 +70,6 @@ struct Shard {
   float* rscale = nullptr;               // [same] split-f16 row scale 2^-e (pad = 1)
   float* qbuf[2] = {nullptr, nullptr};   // staged queries, double-buffered ([q_cap][d] fp32 each): a new
                                          // batch is copied into one while verifies may still read the other
-  hipEvent_t ev_scr[2] = {nullptr, nullptr};     // compute stream: a block's verify done ([0]: the flag-count copy)
   // Two compute streams (rr_set_compute_streams): screened blocks of parity 1 run on cstream2 (stream index 1),
   // so block i + 1's screen starts while block i's screen drains its last chunks and its verify runs. Other work
   // runs on `stream` (index 0). Ordering between the two, by events:
@@ -90,7 +94,7 @@ struct Shard {
   int* scount = nullptr;                 // screened search: [0] blocks this shard flagged for the exact pass,
                                          // [1] blocks its verify completed
   int* wcount = nullptr;                 // ... query slots its verify proved in the wide phase
-  int* pin_scount = nullptr;             // pinned host copy of scount[0..1], refreshed every 8th block (no sync)
+  int* pin_scount = nullptr;             // pinned staging of scount / wcount reads (rr_screen_counts)
   uint32_t* ctr = nullptr;               // split-K chunk counters (dynamic schedule), 0 between launches: one per
                                          // compute stream, kCtrStride words apart
   uint64_t* shard_keys = nullptr;        // [32][k_cap] this shard's top-k (all-gather send buffer)
@@ -113,6 +117,10 @@ struct Shard {
   hipEvent_t ev_keys[kXSlots] = {};    // compute stream: px_keys[x] written
   hipEvent_t ev_xdone[kXSlots] = {};   // xstream: exchange of slot x finished (buffers free)
   hipEvent_t ev_cdone = nullptr;                // compute stream: a serial (k > KMAX) exchange finished
+  // rr_search_async's D2H of the results (local shard 0, on the stream that wrote them last): the next writer of the
+  // result rows on another stream — an exchange merge on the other lane, a serial exchange on `stream` — waits for it
+  hipEvent_t ev_rcopy = nullptr;
+  bool rcopy_pending = false;
   char* out_base = nullptr;              // one allocation: flag word at 0, scores at kOutHead, indices at out_off
   float* out_scores = nullptr;           // [q_cap][k_cap]
   int64_t* out_idx = nullptr;            // [q_cap][k_cap]
@@ -150,6 +158,8 @@ struct AsyncSlot {
   bool pending = false;
   bool screened = false;   // the search ran screened blocks, the first with sequence number seq0
   bool narrow = false;     // ... with 16-entry lists where 2k + 2 wanted 32
+  bool full = false, wide = false;   // ... full per-lane lists / the handle's screen_wide at the time
+  int blocks = 0;          // ... screened blocks
   int seq0 = 0;
 };
 constexpr int kAsyncSlots = 4;
@@ -198,21 +208,24 @@ struct rr_handle {
   int xslots = kXSlots;         // pipelined-exchange buffer sets in use (A/B: RR_X_SLOTS, 2..kXSlots)
   int x_delay_us = 0;           // A/B: RR_X_EXCHANGE_DELAY_US, a stand-in for a slower exchange
   int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy)
-  int64_t narrow_blocks = 0;    // screened blocks run with 16-entry lists where 2k + 2 wanted 32 (screen_kt)
-  int64_t narrow_reruns = 0;    // ... and re-runs of such searches
+  int64_t narrow_settled = 0;   // settled screened blocks run with 16-entry lists where 2k + 2 wanted 32 (screen_kt)
+  int64_t narrow_reruns = 0;    // ... of them re-run exactly
   bool screen_wide = false;     // narrow lists re-ran too often on this corpus: use the wide ones
   bool last_narrow = false;     // the last search ran narrow lists
+  bool last_full = false;       // ... full per-lane lists
+  bool last_wide = false;       // ... (screen_wide at the time)
+  int last_blocks = 0;          // ... this many screened blocks
   bool last_scr_block = false;  // the last block enqueued was a screened one
-  // multi-process deadline (rr_set_timeout): host waits on device work poll against it; a miss fails the handle
+  // deadline (rr_set_timeout): every host wait on device work polls against it; a miss fails the handle
   int timeout_ms = 120000;
+  bool stream_prio = true;      // streams at the runtime's greatest priority (A/B: RR_STREAM_PRIORITY=0)
   bool failed = false;
   int wide_verify = 1;          // the verify's wide phase (A/B: RR_WIDE_VERIFY=0)
-  // adaptive screen (adapt_screen): the screen's per-lane lists grow from 4 keys to KT once blocks flag, and (one
-  // process per handle's world) screening pauses when even that leaves most blocks to the exact pass
+  // adaptive screen (observe_settled): the screen's per-lane lists grow from 4 keys to KT once blocks flag, and
+  // screening pauses when even that leaves most blocks to the exact pass — decided from settled searches only
   bool full_lists = false;
   bool full_lists_env = false;              // (A/B: RR_SCREEN_FULL_LISTS=1, full lists from every load)
-  int64_t win_blocks0 = 0, win_flag0 = 0;   // completed / flagged screened blocks when the current window began
-  bool win_wide = false;                    // screen_wide when it began (a switch starts a fresh window)
+  int64_t win_nb = 0, win_nf = 0;           // settled screened blocks of the current window, and re-run ones
   int64_t screen_pause = 0;                 // search blocks still to run without the screen
   int64_t pauses = 0;                       // statistics: pauses so far (since the load)
 };
@@ -220,28 +233,35 @@ struct rr_handle {
 namespace {
 
 // ---- host waits on device work ---------------------------------------------------------------------------------
-// Without a communicator: the runtime's blocking waits. One process per GPU (rr_init_dist): a polled wait against
-// the handle's deadline, because an all-gather whose peers never arrive would block the caller forever — a miss
-// returns RR_E_TIMEOUT naming this rank and the newest search block, and fails the handle (rr_destroy then aborts
-// the communicators instead of waiting for streams that may never drain).
-template <class Q>
-int poll_until(rr_handle* h, Q&& done, const char* what, int scale = 1) {
+// Every host wait on the handle's device work is a polled wait against the handle's deadline (rr_set_timeout,
+// default 120 s; 0 = the runtime's blocking waits): one process per GPU, an all-gather whose peers never arrive
+// would block the caller forever; within one process, a stream that never drains (round 3's one hung run,
+// DESIGN §5 "Hardware queues") did. A miss returns RR_E_TIMEOUT naming the rank or shard, the device, the stream
+// and the newest search block, and fails the handle (rr_destroy then aborts the communicators and frees nothing
+// that queued work may still reference).
+template <class Q, class L>
+int poll_until(rr_handle* h, Q&& done, L&& label, int scale = 1) {
   const auto t0 = std::chrono::steady_clock::now();
   const int64_t limit_ms = (int64_t)h->timeout_ms * scale;
   for (int i = 0;; ++i) {
     const hipError_t e = done();
     if (e == hipSuccess) return RR_OK;
-    if (e != hipErrorNotReady) return fail(RR_E_HIP, "%s failed: %s", what, hipGetErrorString(e));
+    if (e != hipErrorNotReady) return fail(RR_E_HIP, "%s failed: %s", label().c_str(), hipGetErrorString(e));
     if ((i & 63) == 63) {   // a short spin first (the common case completes within microseconds), then the clock
       const int64_t ms =
           std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
       if (ms >= limit_ms) {
         (void)hipGetLastError();
         h->failed = true;
-        return fail(RR_E_TIMEOUT,
-                    "rank %d of %d: %s did not complete within %lld ms (newest search block %d); an all-gather is "
-                    "probably waiting for a peer rank that never joined",
-                    h->shard_base, h->world, what, (long long)limit_ms, h->screen_seq);
+        const std::string l = label();
+        const char* what = l.c_str();
+        if (h->dist)
+          return fail(RR_E_TIMEOUT,
+                      "rank %d of %d: %s did not complete within %lld ms (newest search block %d); an all-gather is "
+                      "probably waiting for a peer rank that never joined",
+                      h->shard_base, h->world, what, (long long)limit_ms, h->screen_seq);
+        return fail(RR_E_TIMEOUT, "%s did not complete within %lld ms (newest search block %d)", what,
+                    (long long)limit_ms, h->screen_seq);
       }
       if (ms >= 2) std::this_thread::sleep_for(std::chrono::microseconds(20));
       else std::this_thread::yield();
@@ -251,20 +271,36 @@ int poll_until(rr_handle* h, Q&& done, const char* what, int scale = 1) {
 int failed_handle() {
   return fail(RR_E_STATE, "the handle failed earlier (device work missed its deadline, RR_E_TIMEOUT): destroy it");
 }
-bool deadline_on(const rr_handle* h) { return h->dist && h->timeout_ms > 0; }
-int wait_stream(rr_handle* h, hipStream_t st, const char* what = "device stream", int scale = 1) {
+bool deadline_on(const rr_handle* h) { return h->timeout_ms > 0; }
+const char* stream_role(const Shard& s, hipStream_t st) {
+  if (st == s.stream) return "compute stream 0";
+  if (st == s.cstream2) return "compute stream 1";
+  if (st == s.xstream) return "exchange lane 0";
+  if (st == s.xstream2) return "exchange lane 1";
+  return "a work stream";
+}
+// "shard i (device d), <stream>: <what>" (the rank instead of the shard index in multi-process mode)
+std::string wait_label(const rr_handle* h, const Shard& s, const char* stream, const char* what) {
+  char buf[256];
+  const int i = (int)(&s - h->shards.data());
+  snprintf(buf, sizeof buf, "%s %d (device %d), %s: %s", h->dist ? "rank" : "shard", h->dist ? h->shard_base : i,
+           s.dev, stream, what);
+  return buf;
+}
+int wait_stream(rr_handle* h, const Shard& s, hipStream_t st, const char* what = "device work", int scale = 1) {
   if (!deadline_on(h)) {
     HIP_TRY(hipStreamSynchronize(st));
     return RR_OK;
   }
-  return poll_until(h, [&] { return hipStreamQuery(st); }, what, scale);
+  return poll_until(h, [&] { return hipStreamQuery(st); }, [&] { return wait_label(h, s, stream_role(s, st), what); },
+                    scale);
 }
-int wait_event(rr_handle* h, hipEvent_t ev, const char* what = "device event") {
+int wait_event(rr_handle* h, const Shard& s, hipEvent_t ev, const char* what = "device event") {
   if (!deadline_on(h)) {
     HIP_TRY(hipEventSynchronize(ev));
     return RR_OK;
   }
-  return poll_until(h, [&] { return hipEventQuery(ev); }, what);
+  return poll_until(h, [&] { return hipEventQuery(ev); }, [&] { return wait_label(h, s, "event", what); });
 }
 
 int sync_streams(rr_handle* h);   // every local shard's streams idle (defined with the C-ABI's waits)
@@ -332,17 +368,15 @@ int free_shard(Shard& s) {
   if (s.keys_ready) hipEventDestroy(s.keys_ready);
   if (s.pin_q_free) hipEventDestroy(s.pin_q_free);
   if (s.copies_done) hipEventDestroy(s.copies_done);
-  for (hipEvent_t e : {s.ev_cdone, s.ev_scr[0],
-                       s.ev_scr[1]})
-    if (e) hipEventDestroy(e);
+  if (s.ev_cdone) hipEventDestroy(s.ev_cdone);
+  if (s.ev_rcopy) hipEventDestroy(s.ev_rcopy);
   for (hipEvent_t e : {s.ev_fork, s.ev_join, s.ev_stage, s.ev_q[0][0], s.ev_q[0][1], s.ev_q[1][0], s.ev_q[1][1]})
     if (e) hipEventDestroy(e);
-  if (s.xstream) hipStreamDestroy(s.xstream);
-  if (s.xstream2) hipStreamDestroy(s.xstream2);
   if (s.comm2) ncclCommDestroy(s.comm2);
-  if (s.cstream2) hipStreamDestroy(s.cstream2);
   if (s.comm) ncclCommDestroy(s.comm);
-  if (s.stream) hipStreamDestroy(s.stream);
+  if (s.own_streams)
+    for (hipStream_t st : {s.xstream, s.xstream2, s.cstream2, s.stream})
+      if (st) hipStreamDestroy(st);
   s = Shard();
   return RR_OK;
 }
@@ -391,13 +425,15 @@ int finish_corpus(rr_handle* h, Shard& s, bool* screen_ok) {
     if (e == hipSuccess && s.rows() > 0) e = rr::launch_absmax((const float*)s.corpus, s.rows() * h->d, dmax, s.stream);
     float m = 0.f;
     if (e == hipSuccess) e = hipMemcpyAsync(&m, dmax, sizeof(float), hipMemcpyDeviceToHost, s.stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
+    if (e != hipSuccess) {
+      hipFree(dmax);
+      return fail(RR_E_HIP, "corpus range check failed: %s", hipGetErrorString(e));
+    }
+    if (int rc = wait_stream(h, s, s.stream, "the corpus range check")) return rc;
     hipFree(dmax);
-    if (e != hipSuccess) return fail(RR_E_HIP, "corpus range check failed: %s", hipGetErrorString(e));
     *screen_ok = m < 32768.0f;   // also false for NaN
   }
-  HIP_TRY(hipStreamSynchronize(s.stream));
-  return RR_OK;
+  return wait_stream(h, s, s.stream, "the corpus norms");
 }
 
 // Finish every local shard; the screened search is allowed only when every shard's range allows it — in a
@@ -423,7 +459,7 @@ int finish_all(rr_handle* h) {
       if (r != ncclSuccess) rc = fail(RR_E_RCCL, "screen-range agreement failed: %s", ncclGetErrorString(r));
     }
     // ranks finish loading at different times: a generous multiple of the deadline
-    if (e == hipSuccess && rc == RR_OK) rc = wait_stream(h, s.stream, "the ranks' screen-range agreement", 10);
+    if (e == hipSuccess && rc == RR_OK) rc = wait_stream(h, s, s.stream, "the ranks' screen-range agreement", 10);
     if (e == hipSuccess && rc == RR_OK) e = hipMemcpy(&all, dv, sizeof(int), hipMemcpyDeviceToHost);
     if (!h->failed) hipFree(dv);
     if (rc) return rc;
@@ -490,15 +526,15 @@ int upload_rows(rr_handle* h, Shard& s, const float* src, int64_t dst_row, int64
   for (int64_t c = 0, r0 = 0; e == hipSuccess && r0 < nrows; ++c, r0 += chunk_rows) {
     const int i = (int)(c & 1);
     const int64_t nr = std::min(chunk_rows, nrows - r0);
-    if (c >= 2) e = hipEventSynchronize(done[i]);   // chunk c - 2 has left pin[i] / tmp[i]
-    if (e != hipSuccess) break;
+    if (c >= 2) {   // chunk c - 2 has left pin[i] / tmp[i]
+      if (int rc = wait_event(h, s, done[i], "a corpus upload chunk")) return rc;   // (a timeout fails the handle)
+    }
     par_memcpy(pin[i], src + r0 * d, (size_t)nr * d * 4);
     e = hipMemcpyAsync(tmp[i], pin[i], (size_t)nr * d * 4, hipMemcpyHostToDevice, s.stream);
     if (e == hipSuccess) e = store_rows(h, s, tmp[i], dst_row + r0, nr);
     if (e == hipSuccess) e = hipEventRecord(done[i], s.stream);
   }
-  const hipError_t es = hipStreamSynchronize(s.stream);
-  if (e == hipSuccess) e = es;
+  if (int rc = wait_stream(h, s, s.stream, "the corpus upload")) return rc;   // (a timeout fails the handle)
   for (int i = 0; i < 2; ++i) {
     if (pin[i]) hipHostFree(pin[i]);
     if (tmp[i]) hipFree(tmp[i]);
@@ -526,8 +562,8 @@ int drop_work_buffers(rr_handle* h) {
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
     for (hipStream_t st : {s.stream, s.xstream, s.xstream2, s.cstream2})
-      if (int rc = wait_stream(h, st)) return rc;
-    s.c2_busy = s.fork_pending = s.stage_pending = false;
+      if (int rc = wait_stream(h, s, st)) return rc;
+    s.c2_busy = s.fork_pending = s.stage_pending = s.rcopy_pending = false;
     s.last_x = -1;
     s.q_rd[0][0] = s.q_rd[0][1] = s.q_rd[1][0] = s.q_rd[1][1] = false;
     s.last_vsi = -1;
@@ -556,11 +592,10 @@ int drop_work_buffers(rr_handle* h) {
   h->xslot = 0;
   h->screen_blocks = 0;   // the flagged-block counters (scount) were freed above
   h->screen_reruns = 0;
-  h->narrow_blocks = h->narrow_reruns = 0;
+  h->narrow_settled = h->narrow_reruns = 0;
   h->screen_wide = false;
   h->full_lists = h->full_lists_env;
-  h->win_wide = false;
-  h->win_blocks0 = h->win_flag0 = 0;
+  h->win_nb = h->win_nf = 0;
   h->screen_pause = h->pauses = 0;
   h->last_screened = false;
   h->last_settled = true;
@@ -615,7 +650,7 @@ int ensure_buffers(rr_handle* h, int b, int k) {
       if (old && cnt) {
         HIP_TRY(hipMemcpyAsync(s.out_base, old, kOutHead + cnt * 4, hipMemcpyDeviceToDevice, s.stream));
         HIP_TRY(hipMemcpyAsync(s.out_base + s.out_off, old + old_off, cnt * 8, hipMemcpyDeviceToDevice, s.stream));
-        if (int rc = wait_stream(h, s.stream)) return rc;
+        if (int rc = wait_stream(h, s, s.stream)) return rc;
       } else {
         HIP_TRY(hipMemset(s.out_base, 0, kOutHead));   // the screened-search flag word starts at 0
       }
@@ -668,8 +703,8 @@ int ensure_full_sort(rr_handle* h, Shard& s, int k) {
                 (long long)s.rows());
   const size_t need = (size_t)rr::kQSlots * std::max<int64_t>(s.rows(), (int64_t)h->world * k);
   if (need > s.full_cap) {
-    if (int rc = wait_stream(h, s.stream)) return rc;   // the old buffers may still be in use
-    if (int rc = wait_stream(h, s.cstream2)) return rc;
+    if (int rc = wait_stream(h, s, s.stream)) return rc;   // the old buffers may still be in use
+    if (int rc = wait_stream(h, s, s.cstream2)) return rc;
     s.c2_busy = false;
     if (int rc = dmalloc(&s.full_keys, need * 8)) return rc;
     if (int rc = dmalloc(&s.sorted, need * 8)) return rc;
@@ -712,22 +747,7 @@ int screen_kt(const rr_handle* h, int k) {
   return k + 3 <= RR_FUSED_KMAX ? RR_FUSED_KMAX : 0;
 }
 bool narrow_lists(const rr_handle* h, int k) { return std::max(2 * k + 2, k + 3) > 16 && screen_kt(h, k) == 16; }
-void note_rerun(rr_handle* h, bool narrow) {
-  if (!narrow) return;
-  ++h->narrow_reruns;
-  if (h->narrow_blocks >= 64 && h->narrow_reruns * 32 > h->narrow_blocks) h->screen_wide = true;
-}
-// The same rule on the device's flagged-block counts (staged searches whose results nobody fetches are never
-// re-run, but flag just the same): blocks flagged since the load, as the pinned copies last showed them.
-// (One process per GPU: ranks must agree on the list width — it sizes the all-gather — so there only the re-run
-// rule applies: every rank sees the same exchanged flag and re-runs the same searches.)
-void check_narrow(rr_handle* h) {
-  if (h->screen_wide || h->narrow_blocks < 64 || h->dist) return;
-  int64_t flagged = 0;
-  for (const Shard& s : h->shards)
-    if (s.pin_scount) flagged += *(volatile const int*)s.pin_scount;
-  if (flagged * 32 > h->narrow_blocks) h->screen_wide = true;
-}
+// (note the list-width switch: observe_settled)
 
 // Error bound of the screen (rr_sk.hip, DT 6 and DT 7 alike: the same f16 values of x, <= 16 MFMAs per wave partial):
 // eps = kScreenEpsA |x||q| + kScreenEpsB (sqrt(d) |x| + sum|q|).
@@ -751,55 +771,54 @@ bool screened(const rr_handle* h, int k, int slots) {
          (h->screen_pause == 0 || h->kernel == RR_KERNEL_SCREEN_FALLBACK);
 }
 
-// Adaptive screen, at the start of every search, from the flagged-block counts the pinned copies last showed (a block
-// or two late; rr_api.cpp check_narrow reads the same). Windows of >= 32 screened blocks:
-//   * short per-lane lists (4 keys + the workgroup's floor, rr_sk.hip KL) -> full lists (KT keys) when more than 1
-//     in 32 blocks of the window flagged (each costs an exact pass, twice a screen: 3 % flagged cost more than the
-//     full lists do): crowded near-duplicates (a few lanes holding many of them) raise the floors
-//     above what the verify can prove; full lists have no floors. Rank-local (it changes no exchange);
-//   * full lists, and still more than 1 in 2 blocks flagged: the screen cannot prune this corpus (near-duplicate
-//     clusters stored together fill a few workgroups' lists), and each flagged block pays the screen AND the exact
-//     pass — pause screening for 1024 blocks (the one-pass exact kernel alone), then probe again. One process only:
-//     it changes the exchanged list width, which the ranks of a world must agree on. Not while this k still screens
-//     with the narrow 16-entry lists (screen_kt): check_narrow tries the 32-entry ones first.
-// Reset at every load.
-// Windows count blocks the device has COMPLETED (the verify's own count, copied with the flags): a burst of staged
-// searches is enqueued long before the counts of its first blocks reach the host.
-void device_counts(const rr_handle* h, int64_t* flagged, int64_t* done) {
-  *flagged = *done = 0;
-  for (const Shard& s : h->shards)
-    if (s.pin_scount) {
-      *flagged += ((volatile const int*)s.pin_scount)[0];
-      *done += ((volatile const int*)s.pin_scount)[1];
+// Adaptive screen (r4): decided from SETTLED searches only — a search whose completeness the host checked when it
+// collected the results (settle_screen: rr_fetch_results, rr_synchronize, rr_search; rr_wait). The flag word read
+// there is, after an exchange, the largest over every rank's shards, so every rank of a world observes the same
+// outcomes in the same order and takes the same decisions at the same search (the list width and the pause change
+// the exchanged list width and which collectives run: ranks must agree). Round 3 read the device's flagged-block
+// counts asynchronously instead ("a block or two late", rank-dependent) and therefore disabled the pause and the
+// narrow -> wide switch under rr_init_dist. A staged search nobody collects is not observed (its outcome is never
+// read; the bench pays its re-run itself).
+//   * narrow (16-entry) lists -> 32-entry ones when more than 1 in 32 settled narrow blocks re-ran (over >= 64);
+//   * windows of >= 32 settled screened blocks of the current configuration (list width, per-lane list form):
+//     short per-lane lists (4 keys + the workgroup's floor, rr_sk.hip KL) -> full lists (KT keys) when more than
+//     1 in 32 re-ran (each costs an exact pass, twice a screen: 3 % re-run cost more than the full lists do):
+//     crowded near-duplicates (a few lanes holding many of them) raise the floors above what the verify can prove;
+//   * full lists, and still more than 1 in 2 re-ran: the screen cannot prune this corpus (near-duplicate clusters
+//     stored together fill a few workgroups' lists) and each such block pays the screen AND the exact pass — pause
+//     screening for 1024 blocks (the one-pass exact kernel alone), then probe again. Not while this k screens with
+//     the narrow lists (the 32-entry ones are tried first).
+// A block counts as re-run when its search was (a flagged search re-runs all its blocks). Reset at every load.
+void observe_settled(rr_handle* h, int blocks, bool narrow, bool full, bool wide, bool rerun) {
+  if (blocks <= 0) return;
+  const int nre = rerun ? blocks : 0;
+  if (narrow && !h->screen_wide) {
+    h->narrow_settled += blocks;
+    h->narrow_reruns += nre;
+    if (h->narrow_settled >= 64 && h->narrow_reruns * 32 > h->narrow_settled) {
+      h->screen_wide = true;   // the wide lists are judged afresh
+      h->win_nb = h->win_nf = 0;
+      return;
     }
-}
-void adapt_screen(rr_handle* h, int k) {
-  if (h->screen_pause > 0) return;
-  int64_t flagged = 0, done = 0;
-  device_counts(h, &flagged, &done);
-  const int64_t nb = done - h->win_blocks0, nf = flagged - h->win_flag0;
-  if (h->win_wide != h->screen_wide) {   // the list width just changed (check_narrow): judge the new one afresh
-    h->win_wide = h->screen_wide;
-    h->win_blocks0 = done;
-    h->win_flag0 = flagged;
-    return;
   }
-  if (nb < 32) return;
+  // a search enqueued under another configuration than the current one (before a switch or a pause) tells nothing
+  if (h->screen_pause > 0 || full != h->full_lists || (narrow && h->screen_wide) || wide != h->screen_wide) return;
+  h->win_nb += blocks;
+  h->win_nf += nre;
+  if (h->win_nb < 32) return;
   if (!h->full_lists) {
-    if (nf * 32 > nb) h->full_lists = true;
-  } else if (!h->dist && nf * 2 > nb && !narrow_lists(h, k)) {
+    if (h->win_nf * 32 > h->win_nb) h->full_lists = true;
+  } else if (h->win_nf * 2 > h->win_nb && !narrow) {
     h->screen_pause = 1024;
     ++h->pauses;
   }
-  h->win_blocks0 = done;
-  h->win_flag0 = flagged;
+  h->win_nb = h->win_nf = 0;
 }
-// After a search of `blocks` blocks: count down a pause; when it ends, the next window starts from here (a window
-// opened while blocks before the pause are still being counted only sees them late: harmless, it flags anyway).
+// After a search of `blocks` blocks run during a pause: count the pause down (a fresh window follows it).
 void pause_tick(rr_handle* h, int blocks) {
   if (h->screen_pause <= 0) return;
   h->screen_pause = std::max<int64_t>(0, h->screen_pause - blocks);
-  if (h->screen_pause == 0) device_counts(h, &h->win_flag0, &h->win_blocks0);
+  if (h->screen_pause == 0) h->win_nb = h->win_nf = 0;
 }
 
 // Large k (32 < k <= kWideMax): split-K kernel with wide per-workgroup lists, radix select, completeness check
@@ -964,6 +983,10 @@ int enqueue_exchange_px(rr_handle* h, int p, int x, int q0, int bb, int k, int k
     }
     if (h->x_delay_us > 0) HIP_TRY(rr::launch_delay(h->x_delay_us, xs));   // (A/B: a slower exchange)
     if (dst.last_x >= 0 && (dst.last_x & 1) != lane) HIP_TRY(hipStreamWaitEvent(xs, dst.ev_xdone[dst.last_x], 0));
+    if (dst.rcopy_pending) {   // an asynchronous search's result copy still reads these rows (later merges follow this one)
+      HIP_TRY(hipStreamWaitEvent(xs, dst.ev_rcopy, 0));
+      dst.rcopy_pending = false;
+    }
     HIP_TRY(rr::launch_merge(kt, dst.px_gathered[x], h->world, kt, bb, k, nullptr, dst.out_scores + (size_t)q0 * k,
                              dst.out_idx + (size_t)q0 * k, xs, slots, (int64_t)slot, (uint64_t*)dst.out_base));
     HIP_TRY(hipEventRecord(dst.ev_xdone[x], xs));
@@ -1008,7 +1031,6 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
   if (scr || wk) {
     ++h->screen_seq;
     ++h->screen_blocks;
-    if (scr && narrow_lists(h, k)) ++h->narrow_blocks;
   }
   const int seq = h->screen_seq;
   for (size_t si = 0; si < h->shards.size(); ++si) {
@@ -1110,14 +1132,6 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         s.q_rd[t][bsi] = true;
         s.last_vsi = bsi;
         s.last_vq = t;
-      }
-      // the flagged-block count reaches the host without a sync (read a block or two late by check_narrow), every
-      // 8th block, on the exchange stream so that the copy gates nothing on the compute stream. (No event is
-      // recorded on the other blocks: each record between two kernels widened the dispatch gap.)
-      if (s.rows() > 0 && (h->screen_blocks & 7) == 0) {
-        HIP_TRY(hipEventRecord(s.ev_scr[0], vs));
-        HIP_TRY(hipStreamWaitEvent(s.xstream, s.ev_scr[0], 0));
-        HIP_TRY(hipMemcpyAsync(s.pin_scount, s.scount, 2 * sizeof(int), hipMemcpyDeviceToHost, s.xstream));
       }
     } else if (kt) {
       int grid = fused_grid(s);
@@ -1267,6 +1281,10 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
     HIP_TRY(hipSetDevice(s.dev));
     float* osc = s.out_scores + (size_t)q0 * k;
     int64_t* oix = s.out_idx + (size_t)q0 * k;
+    if (s.rcopy_pending) {   // an asynchronous search's result copy (on an exchange lane) still reads these rows
+      HIP_TRY(hipStreamWaitEvent(s.stream, s.ev_rcopy, 0));
+      s.rcopy_pending = false;
+    }
     if (wk) {   // the world lists' union -> top-k (radix select), and the largest of their flag words
       rr::SelArgs sa{};
       sa.in = s.gathered;
@@ -1359,17 +1377,43 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   h->metric = metric;
   h->world = n_dev;
   h->shards.resize(n_dev);
+  if (const char* e = getenv("RR_STREAM_PRIORITY")) h->stream_prio = atoi(e) != 0;   // (A/B)
   for (int i = 0; i < n_dev; ++i) {
     Shard& s = h->shards[i];
     if (devices[i] < 0 || devices[i] >= ndev_avail) {
+      for (int j = i; j < n_dev; ++j) h->shards[j].own_streams = false;   // nothing created for them yet
       rr_destroy(h);
       return fail(RR_E_INVALID, "device %d not available (%d devices)", devices[i], ndev_avail);
     }
     s.dev = devices[i];
     hipError_t e = hipSetDevice(s.dev);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&s.cus, hipDeviceAttributeMultiprocessorCount, s.dev);
+    // Streams: one set of four per device, shared by every shard on it (Shard::own_streams), created at the
+    // runtime's greatest priority: HIP keeps a separate pool of GPU_MAX_HW_QUEUES hardware queues per priority, so
+    // none of ours shares an in-order hardware queue with a normal-priority stream of the process — RCCL's internal
+    // streams (whose barrier packets wait for all-gathers), the null stream, torch's (DESIGN §5 "Hardware queues").
+    const Shard* owner = nullptr;
+    for (int j = 0; j < i; ++j)
+      if (h->shards[j].dev == s.dev) {
+        owner = &h->shards[j];
+        break;
+      }
+    if (owner) {
+      s.own_streams = false;
+      s.stream = owner->stream;
+      s.cstream2 = owner->cstream2;
+      s.xstream = owner->xstream;
+      s.xstream2 = owner->xstream2;
+    } else {
+      int least = 0, greatest = 0;
+      if (e == hipSuccess && h->stream_prio) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+      const int prio = h->stream_prio ? greatest : least;
+      // creation order = the order the hardware queues are handed out in (least used first)
+      for (hipStream_t* st : {&s.stream, &s.xstream, &s.xstream2, &s.cstream2})
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio);
+    }
     if (e != hipSuccess) {
+      for (int j = i + 1; j < n_dev; ++j) h->shards[j].own_streams = false;
       rr_destroy(h);
       return fail(RR_E_HIP, "device %d setup failed: %s", devices[i], hipGetErrorString(e));
     }
@@ -1378,15 +1422,11 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
     hipError_t e = hipSetDevice(s.dev);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.keys_ready, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.copies_done, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.xstream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.xstream2, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.cstream2, hipStreamNonBlocking);
     for (int x = 0; x < kXSlots && e == hipSuccess; ++x) {
       e = hipEventCreateWithFlags(&s.ev_keys[x], hipEventDisableTiming);
       if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev_xdone[x], hipEventDisableTiming);
     }
-    for (hipEvent_t* ev : {&s.ev_cdone, &s.ev_scr[0],
-                           &s.ev_scr[1], &s.ev_fork, &s.ev_join, &s.ev_stage, &s.ev_q[0][0], &s.ev_q[0][1],
+    for (hipEvent_t* ev : {&s.ev_cdone, &s.ev_rcopy, &s.ev_fork, &s.ev_join, &s.ev_stage, &s.ev_q[0][0], &s.ev_q[0][1],
                            &s.ev_q[1][0], &s.ev_q[1][1]})
       if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -1399,7 +1439,8 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   if (const char* e = getenv("RR_VERIFY_CUS")) h->verify_cus = std::max(0, atoi(e));                 // (A/B)
   if (const char* e = getenv("RR_X_SLOTS")) h->xslots = std::min(kXSlots, std::max(2, atoi(e)));     // (A/B)
   if (const char* e = getenv("RR_X_EXCHANGE_DELAY_US")) h->x_delay_us = std::min(1000, std::max(0, atoi(e)));
-  if (const char* e = getenv("RR_DIST_TIMEOUT_MS")) h->timeout_ms = std::max(0, atoi(e));
+  if (const char* e = getenv("RR_DIST_TIMEOUT_MS")) h->timeout_ms = std::max(0, atoi(e));   // (the round-3 name)
+  if (const char* e = getenv("RR_TIMEOUT_MS")) h->timeout_ms = std::max(0, atoi(e));
   if (const char* e = getenv("RR_WIDE_VERIFY")) h->wide_verify = atoi(e) ? 1 : 0;   // (A/B)
   if (const char* e = getenv("RR_SCREEN_FULL_LISTS")) h->full_lists_env = atoi(e) != 0;   // (A/B: start with full lists)
   *out = h;
@@ -1518,11 +1559,11 @@ int rr_fill_synthetic(rr_handle* h, int kind, uint64_t seed, int64_t n_total, in
         const int64_t nr = std::min(chunk_rows, rows - r0);
         hipError_t e = rr::launch_synth(kind, seed, s.row_begin + r0, nr, d, tmp, s.stream);
         if (e == hipSuccess) e = store_rows(h, s, tmp, r0, nr);
-        if (e == hipSuccess) e = hipStreamSynchronize(s.stream);
         if (e != hipSuccess) {
           hipFree(tmp);
           return fail(RR_E_HIP, "synthetic fill failed: %s", hipGetErrorString(e));
         }
+        if (int rc = wait_stream(h, s, s.stream, "the synthetic fill")) return rc;   // (a timeout fails the handle)
       }
       hipFree(tmp);
     }
@@ -1545,6 +1586,55 @@ int rr_shard_range(const rr_handle* h, int i, int64_t* begin, int64_t* end) {
   if (!h || i < 0 || i >= (int)h->shards.size()) return fail(RR_E_INVALID, "bad shard %d", i);
   if (begin) *begin = h->shards[i].row_begin;
   if (end) *end = h->shards[i].row_end;
+  return RR_OK;
+}
+
+int rr_update_rows(rr_handle* h, const float* host_rows, const int64_t* row_idx, int64_t n_rows, int32_t d) {
+  if (!h || ((!host_rows || !row_idx) && n_rows > 0)) return fail(RR_E_INVALID, "null argument");
+  if (h->failed) return failed_handle();
+  if (!h->loaded) return fail(RR_E_STATE, "no corpus loaded");
+  if (d != h->d) return fail(RR_E_INVALID, "row dim %d != corpus dim %d", d, h->d);
+  if (n_rows < 0) return fail(RR_E_INVALID, "n_rows=%lld", (long long)n_rows);
+  for (int64_t i = 0; i < n_rows; ++i)
+    if (row_idx[i] < 0 || row_idx[i] >= h->n_total)
+      return fail(RR_E_INVALID, "row index %lld outside [0, %lld)", (long long)row_idx[i], (long long)h->n_total);
+  // the screen reads fp32 rows as f16 (|x| < 2^15): decided over every given row, on the host — every rank of a world
+  // passes the same rows, so the ranks agree without a collective
+  bool in_range = true;
+  for (int64_t e = 0; e < n_rows * (int64_t)d && in_range; ++e) in_range = fabsf(host_rows[e]) < 32768.0f;   // NaN: no
+  // the last search may still be re-run from the rows about to change: settle it, and let every stream drain
+  if (int rc = rr_synchronize(h)) return rc;
+  const size_t eb = elem_bytes(h->dtype);
+  const bool norms = (h->metric == RR_METRIC_COSINE || kdt_of(h->dtype) == rr::KDT_F32_MFMA) &&
+                     kdt_of(h->dtype) != rr::KDT_F32_SPLIT;   // (the split computes its own)
+  for (Shard& s : h->shards) {
+    std::vector<int64_t> mine;
+    for (int64_t i = 0; i < n_rows; ++i)
+      if (row_idx[i] >= s.row_begin && row_idx[i] < s.row_end) mine.push_back(i);
+    if (mine.empty()) continue;
+    HIP_TRY(hipSetDevice(s.dev));
+    std::vector<float> packed(mine.size() * (size_t)d);
+    for (size_t j = 0; j < mine.size(); ++j)
+      memcpy(packed.data() + j * d, host_rows + mine[j] * (int64_t)d, (size_t)d * 4);
+    float* tmp = nullptr;
+    HIP_TRY(hipMalloc((void**)&tmp, packed.size() * 4));
+    hipError_t e = hipMemcpyAsync(tmp, packed.data(), packed.size() * 4, hipMemcpyHostToDevice, s.stream);
+    // in the given order: a repeated index keeps its last row
+    for (size_t j = 0; j < mine.size() && e == hipSuccess; ++j) {
+      const int64_t lr = row_idx[mine[j]] - s.row_begin;
+      e = store_rows(h, s, tmp + j * d, lr, 1);
+      if (e == hipSuccess && norms)
+        e = rr::launch_row_norms(h->dtype == RR_DTYPE_BF16 ? 1 : 0, (const char*)s.corpus + lr * d * eb, 1, d,
+                                 s.norms + lr, s.stream);
+    }
+    if (e != hipSuccess) {
+      hipFree(tmp);
+      return fail(RR_E_HIP, "row update failed: %s", hipGetErrorString(e));
+    }
+    if (int rc = wait_stream(h, s, s.stream, "the row update")) return rc;
+    hipFree(tmp);
+  }
+  if (!in_range) h->screen_ok = false;
   return RR_OK;
 }
 
@@ -1596,7 +1686,7 @@ int rr_set_queries(rr_handle* h, const float* host_q, int32_t b, int32_t d) {
   for (Shard& s : h->shards) {   // every shard's copy out of pin_q has landed before it is rewritten
     HIP_TRY(hipSetDevice(s.dev));
     if (s.pin_q_free) {
-      if (int rc = wait_event(h, s.pin_q_free, "the previous batch's query copy")) return rc;
+      if (int rc = wait_event(h, s, s.pin_q_free, "the previous batch's query copy")) return rc;
     } else {
       HIP_TRY(hipEventCreateWithFlags(&s.pin_q_free, hipEventDisableTiming));
     }
@@ -1641,10 +1731,11 @@ int rr_search_staged(rr_handle* h, int32_t k) {
   const int b = h->cur_b;
   if (int rc = ensure_buffers(h, b, k)) return rc;
   const int slots = block_slots(h, b, k);
-  check_narrow(h);
-  adapt_screen(h, k);
   h->last_screened = checked(h, k, slots);
   h->last_narrow = screened(h, k, slots) && narrow_lists(h, k);
+  h->last_full = h->full_lists;
+  h->last_wide = h->screen_wide;
+  h->last_blocks = screened(h, k, slots) ? (b + slots - 1) / slots : 0;
   h->last_seq0 = h->screen_seq + 1;
   h->last_settled = !h->last_screened;
   h->last_qpar = h->qpar;
@@ -1680,19 +1771,20 @@ int sync_streams(rr_handle* h) {
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
     for (hipStream_t st : {s.stream, s.xstream, s.xstream2, s.cstream2})
-      if (int rc = wait_stream(h, st)) return rc;
+      if (int rc = wait_stream(h, s, st)) return rc;
     s.c2_busy = false;
+    s.rcopy_pending = false;
   }
   return collect_timing(h);
 }
 
-// D2H of device bytes on local shard 0's `stream` (never the null stream: it would take a hardware queue of its
-// own, and GPU_MAX_HW_QUEUES = 4 are already spoken for by the compute and exchange streams). The streams are idle.
+// D2H of device bytes on local shard 0's `stream` (never the null stream: it sits in the normal-priority queue pool
+// with RCCL's internal streams, whose barrier packets may wait for an all-gather). The streams are idle.
 int copy_out(rr_handle* h, void* dst, const void* src, size_t bytes) {
   Shard& s = h->shards[0];
   HIP_TRY(hipSetDevice(s.dev));
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s.stream));
-  return wait_stream(h, s.stream, "result copy");
+  return wait_stream(h, s, s.stream, "result copy");
 }
 
 // Screened search, last step: `flag` is the last search's flag word (shard 0's result head, which after an
@@ -1702,10 +1794,11 @@ int settle_screen(rr_handle* h, uint64_t flag, bool* rerun) {
   *rerun = false;
   if (!h->last_screened || h->last_settled) return RR_OK;
   h->last_settled = true;
-  if (flag < (uint64_t)h->last_seq0) return RR_OK;
+  const bool flagged = flag >= (uint64_t)h->last_seq0;
+  observe_settled(h, h->last_blocks, h->last_narrow, h->last_full, h->last_wide, flagged);
+  if (!flagged) return RR_OK;
   // the search's own queries (begin_stage keeps its buffer intact until it is settled); a batch staged
   // since stays staged
-  const bool was_narrow = h->last_narrow;
   const int saved_kernel = h->kernel, saved_qpar = h->qpar, saved_b = h->cur_b;
   h->kernel = RR_KERNEL_EXACT;
   h->qpar = h->last_qpar;
@@ -1716,7 +1809,6 @@ int settle_screen(rr_handle* h, uint64_t flag, bool* rerun) {
   h->cur_b = saved_b;
   if (rc) return rc;
   ++h->screen_reruns;
-  note_rerun(h, was_narrow);
   *rerun = true;
   return sync_streams(h);
 }
@@ -1830,12 +1922,25 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
   HIP_TRY(hipMemcpyAsync(a.pin + res_off + kOutHead, s0.out_scores, cnt * 4, hipMemcpyDeviceToHost, rs));
   HIP_TRY(hipMemcpyAsync(a.pin + idx_off, s0.out_idx, cnt * 8, hipMemcpyDeviceToHost, rs));
   HIP_TRY(hipEventRecord(a.done, rs));
+  // the next writer of these result rows on another stream must wait for the copy: the next screened verify on the
+  // other compute stream (ev_q), a cstream2 block after a search on `stream` (ev_fork), an exchange merge on the other
+  // lane or a serial exchange on `stream` (ev_rcopy)
   if (on_v) HIP_TRY(hipEventRecord(s0.ev_q[s0.last_vq][s0.last_vsi], rs));
+  if (!xchg && !on_v) {
+    if (int rc = fork_point(s0)) return rc;
+  }
+  if (xchg) {
+    HIP_TRY(hipEventRecord(s0.ev_rcopy, rs));
+    s0.rcopy_pending = true;
+  }
   a.b = b;
   a.k = k;
   a.ticket = t;
   a.screened = h->last_screened;
   a.narrow = h->last_narrow;
+  a.full = h->last_full;
+  a.wide = h->last_wide;
+  a.blocks = h->last_blocks;
   a.seq0 = h->last_seq0;
   a.pending = true;
   h->next_ticket = t + 1 < 0x40000000 ? t + 1 : 0;
@@ -1849,13 +1954,14 @@ int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx) {
   if (ticket < 0) return fail(RR_E_INVALID, "bad ticket %d", ticket);
   AsyncSlot& a = h->aslots[ticket % kAsyncSlots];
   if (!a.pending || a.ticket != ticket) return fail(RR_E_STATE, "ticket %d is not in flight", ticket);
-  if (int rc = wait_event(h, a.done, "an asynchronous search")) return rc;
+  if (int rc = wait_event(h, h->shards[0], a.done, "an asynchronous search")) return rc;
   a.pending = false;
   const size_t qbytes = (size_t)a.b * h->d * 4, cnt = (size_t)a.b * a.k;
   const size_t res_off = (qbytes + 255) & ~(size_t)255;
   const size_t idx_off = res_off + ((kOutHead + cnt * 4 + 255) & ~(size_t)255);
   uint64_t flag = 0;
   memcpy(&flag, a.pin + res_off, sizeof flag);
+  if (a.screened) observe_settled(h, a.blocks, a.narrow, a.full, a.wide, flag >= (uint64_t)a.seq0);
   if (a.screened && flag >= (uint64_t)a.seq0) {
     // a block needed the exact pass: this batch again, exactly (every rank of an exchange sees the same
     // flag here, so all re-run it together). A batch staged with rr_set_queries before this wait stays the
@@ -1873,7 +1979,6 @@ int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx) {
     h->kernel = saved;
     if (rc == RR_OK) {
       ++h->screen_reruns;
-      note_rerun(h, a.narrow);
       rc = rr_fetch_results(h, out_scores, out_idx);
     }
     h->qpar = saved_qpar;
@@ -1895,15 +2000,12 @@ int rr_screen_counts(rr_handle* h, int64_t* blocks, int64_t* flagged, int64_t* r
     HIP_TRY(hipSetDevice(s.dev));
     int wv = 0;
     HIP_TRY(hipMemcpyAsync(s.pin_scount, s.scount, sizeof(int), hipMemcpyDeviceToHost, s.stream));
-    if (int rc = wait_stream(h, s.stream, "the flagged-block count")) return rc;
+    if (int rc = wait_stream(h, s, s.stream, "the flagged-block count")) return rc;
     fb += *(volatile int*)s.pin_scount;
     HIP_TRY(hipMemcpyAsync(s.pin_scount, s.wcount, sizeof(int), hipMemcpyDeviceToHost, s.stream));
-    if (int rc = wait_stream(h, s.stream, "the wide-verify count")) return rc;
+    if (int rc = wait_stream(h, s, s.stream, "the wide-verify count")) return rc;
     wv = *(volatile int*)s.pin_scount;
     ws += wv;
-    // pin_scount is the counts' host copy (check_narrow, adapt_screen read it): restore it
-    HIP_TRY(hipMemcpyAsync(s.pin_scount, s.scount, 2 * sizeof(int), hipMemcpyDeviceToHost, s.stream));
-    if (int rc = wait_stream(h, s.stream, "the flagged-block count")) return rc;
   }
   if (blocks) *blocks = h->screen_blocks * (int64_t)h->shards.size();
   if (flagged) *flagged = fb;
@@ -1920,6 +2022,27 @@ int rr_set_timeout(rr_handle* h, int32_t ms) {
   if (!h) return fail(RR_E_INVALID, "null handle");
   if (ms < 0) return fail(RR_E_INVALID, "timeout %d ms", ms);
   h->timeout_ms = ms;
+  return RR_OK;
+}
+
+int rr_stream_queues(rr_handle* h, int i, uint64_t* out) {
+  if (!h || !out) return fail(RR_E_INVALID, "null argument");
+  if (i < 0 || i >= (int)h->shards.size()) return fail(RR_E_INVALID, "bad shard %d", i);
+  if (h->failed) return failed_handle();
+  if (int rc = sync_streams(h)) return rc;
+  Shard& s = h->shards[i];
+  HIP_TRY(hipSetDevice(s.dev));
+  uint64_t* dq = nullptr;
+  HIP_TRY(hipMalloc((void**)&dq, 4 * sizeof(uint64_t)));
+  const hipStream_t st[4] = {s.stream, s.cstream2, s.xstream, s.xstream2};
+  hipError_t e = hipSuccess;
+  for (int j = 0; j < 4 && e == hipSuccess; ++j) e = rr::launch_queue_probe(dq + j, st[j]);
+  int rc = RR_OK;
+  if (e == hipSuccess) rc = sync_streams(h);
+  if (e == hipSuccess && rc == RR_OK) e = hipMemcpy(out, dq, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost);
+  if (!h->failed) hipFree(dq);
+  if (rc) return rc;
+  if (e != hipSuccess) return fail(RR_E_HIP, "queue probe failed: %s", hipGetErrorString(e));
   return RR_OK;
 }
 

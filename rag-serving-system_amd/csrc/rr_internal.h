@@ -133,6 +133,8 @@ hipError_t launch_select(const SelArgs& a, hipStream_t s);
 
 // A/B only: a one-workgroup kernel that holds a CU for `us` microseconds (a stand-in for a slower exchange).
 hipError_t launch_delay(int us, hipStream_t s);
+// Diagnostic: *out = the address of the hardware queue a launch on stream s is dispatched from.
+hipError_t launch_queue_probe(uint64_t* out, hipStream_t s);
 
 // Largest |x| of n values (non-negative float bits compared as ints) into *out (device, pre-zeroed).
 hipError_t launch_absmax(const float* x, int64_t n, float* out, hipStream_t s);

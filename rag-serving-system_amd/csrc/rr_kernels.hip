@@ -1115,6 +1115,16 @@ hipError_t launch_delay(int us, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Diagnostic: the address of the hardware (AQL) queue this launch was dispatched from, into *out (rr_stream_queues).
+__global__ void queue_probe_kernel(uint64_t* out) {
+  if (threadIdx.x == 0) *out = (uint64_t)(uintptr_t)__builtin_amdgcn_queue_ptr();
+}
+
+hipError_t launch_queue_probe(uint64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(queue_probe_kernel, dim3(1), dim3(64), 0, s, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_synth(int kind, uint64_t seed, int64_t row_begin, int64_t n_rows, int d, float* out,
                         hipStream_t s) {
   const int64_t count = n_rows * (int64_t)d;

@@ -423,7 +423,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // (no key missing from its list is above max(the list's KT-th key, the floor)); the verify adds the floors to its
   // completeness bound. The branch-free insert, the epilogue's largest VALU item, then costs KL compare-selects.
   // (FL = 1: full lists, KL = KT — the handle switches to them when the short lists' floors stop the verify's
-  // proofs, e.g. near-duplicate clusters whose copies crowd a few lanes; rr_api.cpp adapt_screen)
+  // proofs, e.g. near-duplicate clusters whose copies crowd a few lanes; rr_api.cpp observe_settled)
   constexpr int KL = SCR && KT > 4 && !FL ? 4 : KT;
   constexpr int EB = DT == 1 || DT == 7 ? 2 : 4;                // storage bytes per element
   const int row_bytes = d * EB;
@@ -485,7 +485,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       const int64_t sb = __builtin_amdgcn_readfirstlane((int)(base >> 32)) * 0x100000000ll +
                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)base);
 #ifndef RR_SK_SLAB_ASM
-#define RR_SK_SLAB_ASM 0   // A/B: 1 = one inline-asm statement per slab (not yet measured on the GPU)
+#define RR_SK_SLAB_ASM 1   // one inline-asm statement per slab; A/B (r4, profiles/r04/ab_slab.txt): window +1.5 %, steady +0.8 %
 #endif
       if constexpr (RR_SK_SLAB_ASM) {
         glds16s_slab(wave_src + sb * row_bytes + j * kSlabRowBytes, lane_off, lane_off + row8, lane_off + 2 * row8,

@@ -42,7 +42,7 @@ RR_KERNEL_AUTO = 0
 RR_KERNEL_FUSED = 1
 RR_KERNEL_EXACT = 2
 RR_KERNEL_SCREEN_FALLBACK = 3
-RR_ABI_VERSION = 5
+RR_ABI_VERSION = 6
 
 DTYPES = {"fp32": RR_DTYPE_F32, "float32": RR_DTYPE_F32, "f32": RR_DTYPE_F32,
           "bf16": RR_DTYPE_BF16, "bfloat16": RR_DTYPE_BF16, "fp32-split": RR_DTYPE_F32_SPLIT}
@@ -83,6 +83,8 @@ SIGNATURES = {
     "rr_dist_info": (_c_int, [_vp, _ip, _ip]),
     "rr_screen_counts": (_c_int, [_vp, _i64p, _i64p, _i64p, _i64p]),
     "rr_set_timeout": (_c_int, [_vp, _c_i32]),
+    "rr_stream_queues": (_c_int, [_vp, _c_int, ctypes.POINTER(ctypes.c_uint64)]),
+    "rr_update_rows": (_c_int, [_vp, _fp, _i64p, _c_i64, _c_i32]),
     "rr_screen_state": (_c_int, [_vp, ctypes.POINTER(_c_i32), _i64p, _i64p]),
 }
 
@@ -185,6 +187,7 @@ class Index:
         self._h = h
         self.n = 0
         self.d = 0
+        self.kernel = "auto"
         self._tickets = {}
 
     # -- lifecycle ---------------------------------------------------------------------------------
@@ -234,6 +237,14 @@ class Index:
         b, e = _c_i64(), _c_i64()
         _check(self._lib.rr_shard_range(self._h, i, ctypes.byref(b), ctypes.byref(e)))
         return b.value, e.value
+
+    def update_rows(self, rows: np.ndarray, row_idx) -> None:
+        """Overwrite the corpus rows at the given global indices in place (rr_update_rows)."""
+        r = np.ascontiguousarray(rows, dtype=np.float32)
+        ix = np.ascontiguousarray(row_idx, dtype=np.int64)
+        if r.ndim != 2 or ix.ndim != 1 or r.shape[0] != ix.shape[0]:
+            raise ValueError("rows must be (n, d) with one index per row")
+        _check(self._lib.rr_update_rows(self._h, _fptr(r), _i64ptr(ix), r.shape[0], r.shape[1]))
 
     def read_rows(self, row_begin: int, n_rows: int) -> np.ndarray:
         out = np.empty((n_rows, self.d), dtype=np.float32)
@@ -307,6 +318,7 @@ class Index:
         'exact' (split-K, fp32 scored exactly in one pass), 'fused' (register-streaming kernel) or
         'screen-fallback' (test hook: the screened search's exact fallback pass always runs)."""
         _check(self._lib.rr_set_kernel(self._h, self.KERNELS[kernel]))
+        self.kernel = kernel
 
     def set_schedule(self, dynamic: bool) -> None:
         """Split-K work schedule: dynamic chunk counter (default) or static round-robin chunks."""
@@ -352,9 +364,17 @@ class Index:
         return bool(f.value), p.value, n.value
 
     def set_timeout(self, ms: int) -> None:
-        """Multi-process deadline of every host wait on device work (0 = none); a miss raises
-        HipRetrievalError with code RR_E_TIMEOUT and fails the handle."""
+        """Deadline of every host wait on device work, both modes (0 = unbounded); a miss raises
+        HipRetrievalError with code RR_E_TIMEOUT (naming the rank or shard, device and stream) and fails
+        the handle."""
         _check(self._lib.rr_set_timeout(self._h, int(ms)))
+
+    def stream_queues(self, shard: int = 0) -> list:
+        """Hardware-queue addresses of local shard `shard`'s four streams (compute 0, compute 1, exchange
+        lanes 0 and 1); equal addresses share one in-order queue (diagnostic)."""
+        out = (ctypes.c_uint64 * 4)()
+        _check(self._lib.rr_stream_queues(self._h, int(shard), out))
+        return list(out)
 
     def set_timing(self, enable: bool) -> None:
         _check(self._lib.rr_set_timing(self._h, 1 if enable else 0))

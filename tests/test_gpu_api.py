@@ -106,3 +106,52 @@ def test_async_pipeline_matches_sync(lib, shards):
         lib._lib._check(ix._lib.rr_wait(ix._h, tickets[0], gs.ctypes.data_as(lib._lib._fp),
                                         gi.ctypes.data_as(lib._lib._i64p)))
     ix.close()
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16", "fp32-split"])
+def test_update_rows_equals_reload(lib, dtype, devices):
+    """rr_update_rows overwrites rows in place — storage conversion, per-row norms, the screening copy — so a handle
+    updated in place answers bit-identically to one loaded with the modified corpus, for both metrics and every k
+    path (screened k <= 29 for fp32, k > 32), across shard boundaries and with a repeated index (the last row wins).
+    A row beyond the f16 range turns the screened search off (the exact kernel's results, still identical)."""
+    rng = np.random.default_rng(11)
+    n, d = 6007, 512
+    corpus = rng.standard_normal((n, d)).astype(np.float32)
+    q = rng.standard_normal((40, d)).astype(np.float32)
+    idx = np.array([0, 17, 2002, 2003, 4005, n - 1, 17], dtype=np.int64)
+    new = rng.standard_normal((len(idx), d)).astype(np.float32)
+    new[1] = q[3] * 2.0                              # overwritten again by the repeated index below
+    new[-1] = q[5] * 0.5                             # row 17 becomes a near-copy of query 5
+    changed = corpus.copy()
+    for r, row in zip(idx, new):
+        changed[r] = row
+    for metric in ("cosine", "dot"):
+        up = lib.Index(devices=devices, dtype=dtype, metric=metric)
+        up.load(corpus)
+        up.search(q, 5)
+        up.update_rows(new, idx)
+        fresh = lib.Index(devices=devices, dtype=dtype, metric=metric)
+        fresh.load(changed)
+        for k in (5, 12, 40):
+            want = fresh.search(q, k)
+            got = up.search(q, k)
+            assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), (metric, k)
+        assert up.read_rows(17, 1).tobytes() == fresh.read_rows(17, 1).tobytes()
+        if dtype == "fp32":                          # |x| >= 2^15: the screen's f16 reading cannot hold it
+            big = np.zeros((1, d), np.float32)
+            big[0, 0] = 40000.0
+            up.update_rows(big, np.array([9], np.int64))
+            changed2 = changed.copy()
+            changed2[9] = big[0]
+            ex = lib.Index(devices=devices, dtype=dtype, metric=metric)
+            ex.load(changed2)
+            ex.set_kernel("exact")
+            want = ex.search(q, 5)
+            blocks0 = up.screen_stats()[0]
+            got = up.search(q, 5)
+            assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), metric
+            assert up.screen_stats()[0] == blocks0   # no screened block ran
+            ex.close()
+        up.close()
+        fresh.close()

@@ -132,33 +132,65 @@ def test_config5_bf16_b64_through_rccl(Index, golden_configs, config5):
 N5 = 50_000_000
 
 
+def planted_top10(q: np.ndarray, metric: str):
+    """Per query, 10 rows with known, strictly descending exact scores above every random F2 row's: the query itself
+    with its first 16 j elements zeroed (j = 0..9; a block whose squares sum to 0 is skipped, so every step lowers
+    the score). dot: |q|^2 - (the zeroed squares) ~ 340 .. 290, exact in fp32 (integers x 2^-14 < 2^24 x 2^-14);
+    cosine: sqrt(1 - zeroed/|q|^2) ~ 1 .. 0.93. A random F2 row x scores a sum of 1024 independent bounded terms of
+    mean 0: by Hoeffding P(x.q >= 200) <= exp(-200^2 / (2 |q|^2)) < 1e-25 (cosine 0.6: the same bound), so over 50M
+    rows and 64 queries the planted rows are the top-10 with probability > 1 - 1e-15."""
+    rows, scores = [], []
+    for qi in q.astype(np.float64):
+        sq = qi * qi
+        cut, rr, ss = 0, [], []
+        for j in range(10):
+            x = qi.copy()
+            x[:cut] = 0
+            rr.append(x)
+            ss.append(sq[cut:].sum() if metric == "dot" else np.sqrt(sq[cut:].sum()) / np.sqrt(sq.sum()))
+            cut += 16
+            while sq[cut - 16:cut].sum() == 0:
+                cut += 16
+        rows.append(np.array(rr, np.float32))
+        scores.append(np.array(ss))
+    return np.stack(rows), np.stack(scores)
+
+
 @pytest.mark.parametrize("metric", ["dot", "cosine"])
 def test_config5_50m_full_size(Index, metric):
-    """BASELINE config 5 at its defining size on one MI355X: 50M x 1024 bf16 rows (102 GB; F2
-    exact-integer rows generated on the device, exact in bf16), B = 64, k = 10, through the 64-slot bf16 kernel.
-    The 64 queries are corpus rows planted at spread-out indices, so each query's top-1 is its own row (its self
-    dot |x|^2 ~ 340 against ~ +-11 for the others, and cosine 1). Every returned score equals the fp64 metric at
-    the returned index — exactly for dot (integer products, |sum| < 2^24: exact in fp32 in any order), within 1e-6
-    for cosine — and one shard and 8 in-process shards (the 8-GPU exchange and merge) give bit-identical results.
-    Property checks in place of a host-side golden: the reference cannot run 50M rows here."""
-    planted = np.arange(64, dtype=np.int64) * 781_249 + 12_345
+    """BASELINE config 5 at its defining size on one MI355X: 50M x 1024 bf16 rows (102 GB; F2 exact-integer rows
+    generated on the device, exact in bf16), B = 64, k = 10, through the 64-slot bf16 kernel. Per query, 10 rows with
+    known, strictly descending exact scores above every random row's (planted_top10) are written into the corpus at
+    spread-out indices (rr_update_rows), so the whole expected top-10 — indices and scores — is known on the host:
+    every list must equal it exactly (dot: bit-identical integers; cosine: within 1e-6 of fp64), and the
+    register-streaming kernel (rr_set_kernel fused: another arithmetic and tiling) and 8 in-process shards (the
+    8-GPU exchange and merge) give the same lists. A dropped, duplicated or mis-merged row at any rank 1-10 — a
+    chunk-schedule or exchange bug that only shows at full size — fails it. Contract: retriever.py:750-769."""
     seed = 5
-    q = np.stack([synth.exact_int_rows(seed, int(r), 1, D)[0] for r in planted])
+    q = synth.exact_int_queries(77, 64, D)
+    rows, want_s = planted_top10(q, metric)                    # [64][10][D], [64][10]
+    where = (np.arange(64, dtype=np.int64)[:, None] * 781_249 + np.arange(10, dtype=np.int64)[None, :] * 70_001
+             + 12_345)                                         # spread over the 50M rows and all 8 shards
+    assert where.max() < N5 and len(np.unique(where)) == 640
+    order = np.argsort(-want_s, axis=1, kind="stable")
+    want_i = np.take_along_axis(where, order, axis=1)
+    want_s = np.take_along_axis(want_s, order, axis=1)
+    results = {}
     one = Index(dtype="bf16", metric=metric)
     one.fill_synthetic(0, seed, N5, D)
-    s1, i1 = one.search(q, K)
-    one.close()                                          # free the 102 GB before the 8-shard handle
-    assert np.array_equal(i1[:, 0], planted)
-    for i in range(q.shape[0]):
-        rows = np.stack([synth.exact_int_rows(seed, int(r), 1, D)[0] for r in i1[i]])
-        want = exact_scores(rows, q[i:i + 1], metric)[0]
-        if metric == "dot":
-            assert np.array_equal(s1[i].astype(np.float64), want), i
-        else:
-            assert np.max(np.abs(s1[i] - want)) <= 1e-6, i
-        assert np.all(np.diff(s1[i]) <= 0), i            # sorted
+    one.update_rows(rows.reshape(640, D), where.reshape(640))
+    results["split-K, 1 shard"] = one.search(q, K)
+    one.set_kernel("fused")
+    results["register-streaming, 1 shard"] = one.search(q, K)
+    one.close()                                                # free the 102 GB before the 8-shard handle
     many = Index(devices=[0] * 8, dtype="bf16", metric=metric)
     many.fill_synthetic(0, seed, N5, D)
-    s8, i8 = many.search(q, K)
+    many.update_rows(rows.reshape(640, D), where.reshape(640))
+    results["split-K, 8 shards"] = many.search(q, K)
     many.close()
-    assert np.array_equal(i8, i1) and np.array_equal(s8, s1)
+    for name, (s1, i1) in results.items():
+        assert np.array_equal(i1, want_i), name
+        if metric == "dot":
+            assert np.array_equal(s1.astype(np.float64), want_s), name
+        else:
+            assert np.max(np.abs(s1 - want_s)) <= 1e-6, name

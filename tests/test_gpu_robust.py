@@ -29,6 +29,36 @@ def _same(got, want):
     return np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
 
 
+def test_stream_queues_distinct_and_shared_per_device(Index):
+    """Hardware-queue placement (rr_stream_queues: each stream's AQL queue address, read by a probe kernel). A handle's
+    four streams dispatch to four distinct hardware queues at the box's own GPU_MAX_HW_QUEUES (they take the
+    high-priority pool, which nothing else of the process uses), also with a 1-rank RCCL communicator whose internal
+    streams are created after them; shards on one device share one set of streams (no cross-shard stream waits)."""
+    import gc
+    from rag_service_amd import get_unique_id
+    gc.collect()                                               # handles of earlier tests released
+    corpus = synth.unit_norm_gaussian(75, 4000, 512)
+    one = Index(dtype="fp32", metric="cosine")
+    one.load(corpus)
+    qs = one.stream_queues(0)
+    assert len(set(qs)) == 4 and all(qs), [hex(v) for v in qs]
+    one.close()
+    many = Index(devices=[0, 0, 0], dtype="fp32", metric="cosine")
+    many.load(corpus)
+    q0 = many.stream_queues(0)
+    assert len(set(q0)) == 4, [hex(v) for v in q0]
+    assert many.stream_queues(1) == q0 and many.stream_queues(2) == q0
+    many.close()
+    rx = Index(dtype="fp32", metric="cosine")
+    rx.init_dist(1, 0, get_unique_id())
+    rx.load(corpus)
+    q = synth.unit_norm_gaussian(76, 32, 512)
+    rx.search(q, 5)                                            # the communicators' streams are in use
+    qr = rx.stream_queues(0)
+    assert len(set(qr)) == 4, [hex(v) for v in qr]
+    rx.close()
+
+
 def test_exchange_flag_word_cleared_between_list_widths(Index):
     """Through the RCCL exchange (1-rank communicator): k = 20 screens with 32-entry lists, so its exchanged keys
     reach past where k = 3's flag word sits (after 32 x 8 keys). Every buffer set is written at k = 20, then read
@@ -159,3 +189,36 @@ def test_dist_deadline_fails_loudly(Index, monkeypatch):
     ok.load(corpus)
     ok.search(q, 5)
     ok.close()
+
+
+def test_single_process_deadline_names_shard_and_stream(Index, monkeypatch):
+    """Round 3's one hang (a stream that never drained, rr_search never returned) becomes a loud error: within one
+    process too, every host wait polls against the handle's deadline (rr_set_timeout). Two shards on one device
+    exchange by peer copies; a stand-in kernel holds the exchange lanes 1 ms per search block (RR_X_EXCHANGE_DELAY_US)
+    under a 2 ms deadline over 24 blocks: the wait returns RR_E_TIMEOUT naming the shard, its device and the stream,
+    and the handle is failed (later calls: RR_E_STATE)."""
+    from rag_service_amd._lib import HipRetrievalError, RR_E_STATE, RR_E_TIMEOUT
+    corpus = synth.unit_norm_gaussian(73, 8000, 512)
+    q = synth.unit_norm_gaussian(74, 32, 512)
+    monkeypatch.setenv("RR_X_EXCHANGE_DELAY_US", "1000")
+    ix = Index(devices=[0, 0], dtype="fp32", metric="cosine")
+    monkeypatch.delenv("RR_X_EXCHANGE_DELAY_US")
+    ix.load(corpus)
+    ix.search(q, 5)                                            # warm, default 120 s deadline
+    ix.set_timeout(2)
+    ix.set_queries(q)
+    for _ in range(24):
+        ix.search_staged(5)
+    t0 = time.perf_counter()
+    with pytest.raises(HipRetrievalError) as e:
+        ix.synchronize()
+    msg = str(e.value)
+    assert e.value.code == RR_E_TIMEOUT and "shard 0 (device 0)" in msg, msg
+    assert ("compute stream" in msg or "exchange lane" in msg) and "did not complete within 2 ms" in msg, msg
+    assert time.perf_counter() - t0 < 1.0
+    with pytest.raises(HipRetrievalError) as e2:
+        ix.search_staged(5)
+    assert e2.value.code == RR_E_STATE
+    time.sleep(1.0)                                            # 24 ms of stand-in delay: the queues drain
+    ix.close()
+

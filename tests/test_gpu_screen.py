@@ -269,36 +269,63 @@ def test_wide_verify_on_clustered_embeddings(Index, metric, layout):
     ex.close()
 
 
+def _plain_and_dist(Index, corpus):
+    """The same corpus in a plain handle and in one with a 1-rank RCCL communicator (rr_init_dist: every search takes
+    the multi-process data path — all-gather of the candidates with the flag words, device merge). Both on the static
+    chunk schedule: the dynamic one hands rows to workgroups by a race, so which blocks a clustered corpus flags
+    varies from run to run (the results never do); static, the screen's lists and so the flags are reproducible, and
+    the two handles must then switch at the same searches."""
+    from rag_service_amd import get_unique_id
+    plain = Index(dtype="fp32", metric="cosine")
+    plain.load(corpus)
+    dist = Index(dtype="fp32", metric="cosine")
+    dist.init_dist(1, 0, get_unique_id())
+    dist.load(corpus)
+    for ix in (plain, dist):
+        ix.set_schedule(False)
+    return plain, dist
+
+
 @pytest.mark.parametrize("layout", ["interleaved", "contiguous"])
 def test_screen_adapts_to_clustered_corpora(Index, layout):
-    """The adaptive screen (rr_api.cpp adapt_screen) on 1000 noisy copies of each of 100 SQuAD rows (sigma 0.01):
+    """The adaptive screen (rr_api.cpp observe_settled) on 1000 noisy copies of each of 100 SQuAD rows (sigma 0.01):
     interleaved, every cluster's copies fall on a few lanes of each workgroup (a stride of 100 rows), overflow the
-    short per-lane lists and their floors stop every proof — after one window of flagged blocks the handle switches
-    to full lists, and from then on the wide phase proves every block (no flags). Contiguous, a cluster fills a
-    few workgroups' lists even then: after a second window the handle pauses screening (the exact kernel alone)
-    for 1024 blocks. Results bit-identical to the exact kernel at every step."""
+    short per-lane lists and their floors stop every proof — after one window of 32 re-run blocks the handle
+    switches to full lists, and from then on the wide phase proves every block (no flags). Contiguous, a cluster
+    fills a few workgroups' lists even then: after a second window the handle pauses screening (the exact kernel
+    alone) for 1024 blocks. Decided from settled searches only, so a handle in multi-process mode (1-rank RCCL
+    communicator) switches at exactly the same searches as a plain one. Results bit-identical to the exact kernel
+    at every step."""
     corpus, q = _clustered(100000, 0.01, layout, clusters=100)
     ex = Index(dtype="fp32", metric="cosine")
     ex.load(corpus)
     ex.set_kernel("exact")
     want = ex.search(q, 5)
-    ix = Index(dtype="fp32", metric="cosine")
-    ix.load(corpus)
-    assert ix.screen_state() == (False, 0, 0)
-    hist = []
-    for step in range(140):
-        got = ix.search(q, 5)
-        assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), step
-        hist.append(ix.screen_counts_all() + ix.screen_state())
+    handles = _plain_and_dist(Index, corpus)
+    hists = []
+    for ix in handles:
+        assert ix.screen_state() == (False, 0, 0)
+        hist = []
+        for step in range(140):
+            got = ix.search(q, 5)
+            assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), step
+            hist.append(ix.screen_counts_all() + ix.screen_state())
+        hists.append(hist)
+        ix.close()
+    hist, hist_dist = hists
+    assert [h[4:] for h in hist] == [h[4:] for h in hist_dist]          # the same switch points, step by step
+    assert [h[:3] for h in hist] == [h[:3] for h in hist_dist]          # the same blocks, flags and re-runs
     blocks, flagged, reruns, wide_slots, full, pause_left, pauses = hist[-1]
     print(layout, hist[40], hist[-1])
-    assert full
+    full_at = next(i for i, h in enumerate(hist) if h[4])
+    assert full_at % 32 == 31                                           # decided at the end of a 32-block window
     if layout == "interleaved":
         assert pauses == 0 and blocks == 140
-        assert hist[-1][1] == hist[80][1] and wide_slots >= 32 * 50     # no flags once the lists are full
+        assert hist[-1][1] == hist[full_at][1] and wide_slots >= 32 * 50    # no flags once the lists are full
     else:
-        assert pauses == 1 and pause_left > 0 and blocks < 140          # screening paused: exact kernel alone
-    ix.close()
+        pause_at = next(i for i, h in enumerate(hist) if h[6])
+        assert pause_at % 32 == 31 and pauses == 1 and blocks == pause_at + 1   # then the exact kernel alone
+        assert pause_left == 1024 - (139 - pause_at)
     ex.close()
 
 
@@ -419,28 +446,32 @@ def test_screen_copy_equals_fp32_screen_and_exact(Index, metric):
 
 def test_narrow_lists_switch_to_wide(Index):
     """k = 10 screens with 16-entry lists (k + 3 spare). Twenty near-copies of each query make the 16th upper
-    bound exceed the exact 10th score: every block is re-run exactly — until, after 64 narrow blocks, the
-    handle switches to 32-entry lists, which prove these blocks complete. Results are exact throughout."""
+    bound exceed the exact 10th score: every block is re-run exactly — until, after 64 settled narrow blocks, the
+    handle switches to 32-entry lists, which prove these blocks complete. The same switch, at the same search, in
+    multi-process mode (1-rank RCCL communicator: the decision comes from the exchanged flag words). Results are
+    exact throughout."""
     rng = np.random.default_rng(5)
     corpus = synth.unit_norm_gaussian(91, 65536, 1024)
     q = synth.unit_norm_gaussian(92, 32, 1024)
     for i in range(32):
         near = q[i] + 1e-6 * rng.standard_normal((20, 1024)).astype(np.float32)
         corpus[1000 + 40 * i:1020 + 40 * i] = near / np.linalg.norm(near, axis=1, keepdims=True)
-    ix = Index(dtype="fp32", metric="cosine")
-    ix.load(corpus)
     ex = Index(dtype="fp32", metric="cosine")
     ex.load(corpus)
     ex.set_kernel("exact")
     want = ex.search(q, 10)
-    for step in range(80):
-        got = ix.search(q, 10)
-        assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), step
-        if step == 69:
-            flagged70 = ix.screen_stats()[1]
-    blocks, flagged = ix.screen_stats()
-    assert blocks == 80 and 64 <= flagged <= 70 and flagged == flagged70     # none after the switch
-    ix.close()
+    per_mode = []
+    for ix in _plain_and_dist(Index, corpus):
+        flags = []
+        for step in range(80):
+            got = ix.search(q, 10)
+            assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), step
+            flags.append(ix.screen_stats()[1])
+        blocks, flagged = ix.screen_stats()
+        assert blocks == 80 and flagged == 64 and flags[63] == 64 and flags[62] == 63   # none after the switch
+        per_mode.append(flags)
+        ix.close()
+    assert per_mode[0] == per_mode[1]
     ex.close()
 
 

@@ -7,7 +7,7 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/$1
 read DOCS B K DT <<< "$2"
 shift 2
-W="--docs $DOCS --dtype $DT --batch $B --k $K --no-cpu-baseline --variants= --ingest-rows 0 --no-pmc --steps ${STEPS:-40} --warmup ${WARMUP:-10} --latency-steps 5 --steady-steps 60"
+W="--docs $DOCS --dtype $DT --batch $B --k $K --no-cpu-baseline --variants= --ingest-rows 0 --no-pmc --steps ${STEPS:-40} --warmup ${WARMUP:-10} --latency-steps 5 --steady-steps 60 $EXTRA"
 echo "# $DOCS rows, batch $B, k $K, $DT: value kernel_us frac | steady value kernel_us frac" >> "$OUT"
 for rep in $(seq ${REPS:-2}); do
   for arm in "$@"; do

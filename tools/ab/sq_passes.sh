@@ -8,6 +8,7 @@ read DOCS B K DT <<< "$2"
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 W="--docs $DOCS --dtype $DT --batch $B --k $K --no-cpu-baseline --variants= --ingest-rows 0 --no-pmc --steps 3 --warmup 1"
+[ -n "$EXACT" ] && W="$W --kernel exact"
 P1="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY"
 P2="SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_BRANCH SQ_ACTIVE_INST_MISC SQ_VALU_MFMA_BUSY_CYCLES"
 i=0
