@@ -133,7 +133,6 @@ struct Shard {
   uint64_t* wsel = nullptr;              // [32][kSelParts][kWideMax] stage-1 selections
   // full-sort path (k > kWideMax, unsupported shapes, and the exact re-run of an unproven large-k search)
   uint64_t* full_keys = nullptr;         // [32][max(rows, world*k)]
-  uint64_t* sorted = nullptr;
   size_t full_cap = 0;                   // elements
   void* sort_temp = nullptr;
   size_t sort_temp_bytes = 0;
@@ -353,7 +352,7 @@ int dmalloc(T** p, size_t bytes) {
 int free_shard(Shard& s) {
   hipSetDevice(s.dev);
   void* ptrs[] = {s.corpus, s.scr16, s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.wcount, s.ctr, s.shard_keys, s.gathered, s.out_base,
-                  s.full_keys, s.sorted, s.sort_temp, s.wcand, s.wfloor, s.wsel};
+                  s.full_keys, s.sort_temp, s.wcand, s.wfloor, s.wsel};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (int x = 0; x < kXSlots; ++x) {
@@ -568,7 +567,7 @@ int drop_work_buffers(rr_handle* h) {
     s.q_rd[0][0] = s.q_rd[0][1] = s.q_rd[1][0] = s.q_rd[1][1] = false;
     s.last_vsi = -1;
     void** ptrs[] = {(void**)&s.qbuf[0], (void**)&s.qbuf[1], (void**)&s.cand, (void**)&s.scount, (void**)&s.wcount, (void**)&s.ctr, (void**)&s.shard_keys, (void**)&s.gathered,
-                     (void**)&s.out_base, (void**)&s.full_keys, (void**)&s.sorted, &s.sort_temp,
+                     (void**)&s.out_base, (void**)&s.full_keys, &s.sort_temp,
                      (void**)&s.wcand, (void**)&s.wfloor, (void**)&s.wsel};
     for (void** p : ptrs) {
       if (*p) HIP_TRY(hipFree(*p));
@@ -695,23 +694,18 @@ int ensure_buffers(rr_handle* h, int b, int k) {
   return RR_OK;
 }
 
-// Buffers of the full-sort path (every key of the shard, segmented radix sort), allocated on first use.
+// Buffers of the full-key path (every key of the shard, then its top-k sorted: rr_topk.hip), allocated on first use.
 int ensure_full_sort(rr_handle* h, Shard& s, int k) {
-  // hipcub's segmented sort takes an int item count
-  if ((int64_t)rr::kQSlots * std::max<int64_t>(s.rows(), (int64_t)h->world * k) > INT32_MAX)
-    return fail(RR_E_UNSUPPORTED, "k=%d on a shard of %lld rows exceeds the full-sort path's size limit", k,
-                (long long)s.rows());
   const size_t need = (size_t)rr::kQSlots * std::max<int64_t>(s.rows(), (int64_t)h->world * k);
-  if (need > s.full_cap) {
+  const size_t tb = rr::topk_scratch_bytes(rr::kQSlots, k);
+  if (need > s.full_cap || tb > s.sort_temp_bytes) {
     if (int rc = wait_stream(h, s, s.stream)) return rc;   // the old buffers may still be in use
     if (int rc = wait_stream(h, s, s.cstream2)) return rc;
     s.c2_busy = false;
-    if (int rc = dmalloc(&s.full_keys, need * 8)) return rc;
-    if (int rc = dmalloc(&s.sorted, need * 8)) return rc;
-    s.full_cap = need;
-    size_t tb = 0;
-    HIP_TRY(rr::segmented_sort_desc(nullptr, &tb, s.full_keys, s.sorted, rr::kQSlots,
-                                    (int64_t)(need / rr::kQSlots), s.stream));
+    if (need > s.full_cap) {
+      if (int rc = dmalloc(&s.full_keys, need * 8)) return rc;
+      s.full_cap = need;
+    }
     if (tb > s.sort_temp_bytes) {
       if (int rc = dmalloc(&s.sort_temp, tb)) return rc;
       s.sort_temp_bytes = tb;
@@ -1247,9 +1241,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
                                        bb, base, s.full_keys, s.stream));
         }
         if (timed) HIP_TRY(hipEventRecord(e1, s.stream));
-        size_t tb = s.sort_temp_bytes;
-        HIP_TRY(rr::segmented_sort_desc(s.sort_temp, &tb, s.full_keys, s.sorted, bb, rows, s.stream));
-        HIP_TRY(rr::launch_take_prefix(s.sorted, bb, rows, k, s.shard_keys, s.stream));
+        HIP_TRY(rr::launch_topk_sorted(s.full_keys, bb, rows, k, s.shard_keys, s.sort_temp, s.stream));
       } else if (timed) {
         HIP_TRY(hipEventRecord(e1, s.stream));
       }
@@ -1304,9 +1296,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
     } else {
       const int64_t seg = (int64_t)h->world * k;
       HIP_TRY(rr::launch_regroup(s.gathered, h->world, k, bb, s.full_keys, s.stream));
-      size_t tb = s.sort_temp_bytes;
-      HIP_TRY(rr::segmented_sort_desc(s.sort_temp, &tb, s.full_keys, s.sorted, bb, seg, s.stream));
-      HIP_TRY(rr::launch_take_prefix(s.sorted, bb, seg, k, s.shard_keys, s.stream));
+      HIP_TRY(rr::launch_topk_sorted(s.full_keys, bb, seg, k, s.shard_keys, s.sort_temp, s.stream));
       HIP_TRY(rr::launch_decode(s.shard_keys, bb, k, osc, oix, s.stream));
     }
     // later pipelined exchanges write the results after this one

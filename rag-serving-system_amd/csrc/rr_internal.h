@@ -144,12 +144,10 @@ hipError_t launch_full_keys(int kdt, int metric, int grid, const void* corpus, c
                             const float* rscale, const float* queries, int64_t n, int d, int b,
                             uint32_t idx_base, uint64_t* keys, hipStream_t s);
 
-// Segmented descending sort of b segments of `seg` keys each (in -> out); temp from hipcub.
-hipError_t segmented_sort_desc(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out,
-                               int b, int64_t seg, hipStream_t s);
-
-// Gather first k of each sorted segment: out_keys [b][k] (row stride k) from sorted [b][seg].
-hipError_t launch_take_prefix(const uint64_t* sorted, int b, int64_t seg, int k, uint64_t* out_keys,
+// Top-k of b segments of `seg` keys each, sorted descending (rr_topk.hip: radix select, compaction, bitonic tiles,
+// rank merges): out [b][k] (row stride k), 0-padded past a segment's non-zero keys. scratch: topk_scratch_bytes(b, k).
+size_t topk_scratch_bytes(int b, int64_t k);
+hipError_t launch_topk_sorted(const uint64_t* in, int b, int64_t seg, int64_t k, uint64_t* out, void* scratch,
                               hipStream_t s);
 
 // gathered [world][32][k] -> per-query segments [b][world*k].

@@ -16,7 +16,6 @@
 // deterministic tie rule of this implementation (the reference's tie order is implementation
 // defined: numpy introselect / CUB). Key 0 = empty slot.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include <stdint.h>
 #include <type_traits>
 #include "rr_internal.h"
@@ -543,14 +542,6 @@ __global__ void decode_kernel(const uint64_t* __restrict__ keys, int64_t count, 
 }
 
 // sorted [b][seg] -> out [32 slots][k] (rows >= b untouched)
-__global__ void take_prefix_kernel(const uint64_t* __restrict__ sorted, int64_t seg, int k,
-                                   uint64_t* __restrict__ out) {
-  const int q = blockIdx.y;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gridDim.x * blockDim.x)
-    out[(size_t)q * k + i] = i < seg ? sorted[(size_t)q * seg + i] : 0;
-}
-
-// gathered [world][32][k] -> per-query segments [b][world*k] (k > RR_FUSED_KMAX cross-shard merge)
 __global__ void regroup_kernel(const uint64_t* __restrict__ in, int world, int k, uint64_t* __restrict__ out) {
   const int q = blockIdx.y;
   const int total = world * k;
@@ -992,25 +983,6 @@ hipError_t launch_merge(int kt, const uint64_t* in, int nlists, int in_kt, int b
     case 32: hipLaunchKernelGGL(merge_kernel<32>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out, clear_word); break;
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
-}
-
-hipError_t segmented_sort_desc(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, int b,
-                               int64_t seg, hipStream_t s) {
-  hipcub::CountingInputIterator<int64_t> it0(0);
-  struct Mul {
-    int64_t seg;
-    __host__ __device__ int64_t operator()(int64_t i) const { return i * seg; }
-  };
-  hipcub::TransformInputIterator<int64_t, Mul, hipcub::CountingInputIterator<int64_t>> offs(it0, Mul{seg});
-  return hipcub::DeviceSegmentedRadixSort::SortKeysDescending(temp, *temp_bytes, in, out, (int64_t)b * seg, b,
-                                                              offs, offs + 1, 0, 64, s);
-}
-
-hipError_t launch_take_prefix(const uint64_t* sorted, int b, int64_t seg, int k, uint64_t* out_keys,
-                              hipStream_t s) {
-  const int gx = (k + 255) / 256;
-  hipLaunchKernelGGL(take_prefix_kernel, dim3(gx, b), dim3(256), 0, s, sorted, seg, k, out_keys);
   return hipGetLastError();
 }
 

@@ -59,11 +59,18 @@ def test_version_and_error_string_without_gpu(lib):
     assert isinstance(lib.rr_last_error(), bytes)
 
 
-def test_code_object_targets_gfx950():
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", _lib.LIB_PATH, "-d", "--section=none"],
-                         capture_output=True, text=True)
-    blob = open(_lib.LIB_PATH, "rb").read()
-    assert b"gfx950" in blob
+def test_code_object_targets_gfx950(tmp_path):
+    """The library's device code objects are gfx950 ones (llvm-objdump --offloading extracts the bundles next to its
+    input: it runs on a copy in tmp_path, so nothing lands in the package directory)."""
+    import shutil
+    lib_copy = tmp_path / "librag_retrieval.so"
+    shutil.copy(_lib.LIB_PATH, lib_copy)
+    subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib_copy)], capture_output=True,
+                   text=True, cwd=tmp_path)
+    bundles = [f.name for f in tmp_path.iterdir() if f.name != lib_copy.name]
+    assert any("gfx950" in b for b in bundles), bundles
+    assert not any(("gfx9" in b and "gfx950" not in b) for b in bundles), bundles
+    assert b"gfx950" in open(_lib.LIB_PATH, "rb").read()
 
 
 def test_product_path_has_no_oracle_or_fallback():

@@ -142,3 +142,40 @@ def test_large_k_async_and_staged(Index):
     _same(ix.fetch(), ref.search(qs[0], 64))
     ix.close()
     ref.close()
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+@pytest.mark.parametrize("dtype,metric", [("fp32", "cosine"), ("fp32", "dot"), ("bf16", "cosine")])
+def test_full_key_path_k_above_256(Index, dtype, metric, devices):
+    """k > 256: every key of the shard, then its top-k sorted by the hand-written select + sort (rr_topk.hip: radix
+    select of the k-th key, compaction, bitonic 2048-key tiles, rank merges) — one tile, several tiles and merge
+    passes, k = n (no select), k > n (zero padding -> -inf / -1) — and, with three shards, the serial exchange's
+    merge of world x k candidates by the same routine. Against the oracle's canonical top-k (retriever.py:750-769),
+    and bit-identical across shard counts. The largest k is the reference's own clamp k -> n (retriever.py:730)."""
+    rng = np.random.default_rng(len(devices) * 7 + len(dtype) + len(metric))
+    n, d, b = 20011, 256, 40
+    corpus = rng.standard_normal((n, d)).astype(np.float32)
+    if dtype == "bf16":
+        corpus = synth.bf16_round(corpus)
+    q = rng.standard_normal((b, d)).astype(np.float32)
+    ix = Index(devices=devices, dtype=dtype, metric=metric)
+    ix.load(corpus)
+    one = Index(dtype=dtype, metric=metric) if len(devices) > 1 else None
+    if one:
+        one.load(corpus)
+    ex = exact_scores(corpus, q, metric)
+    for k in (257, 2048, 2049, 7000, n, n + 9):
+        scores, idx = ix.search(q, k)
+        kk = min(k, n)
+        _, cidx = canonical_topk(ex, kk)
+        tol = 1e-3 * (np.sqrt(d) if metric == "dot" else 1.0)
+        check_topk(idx[:, :kk], scores[:, :kk], cidx, corpus, q, metric, near_tie=1e-5 * np.sqrt(d), score_tol=tol)
+        assert np.all(np.diff(scores[:, :kk], axis=1) <= 0), k
+        if k > n:
+            assert np.all(idx[:, n:] == -1) and np.all(np.isneginf(scores[:, n:])), k
+        assert np.array_equal(np.sort(idx[:, :kk], axis=1), np.tile(np.arange(n), (b, 1))) if kk == n else True
+        if one:
+            _same(one.search(q, k), (scores, idx), k)
+    ix.close()
+    if one:
+        one.close()

@@ -15,6 +15,7 @@ F="-O3 -std=c++17 -Wno-unused-value -Wno-unused-result -fPIC -I$T/include -I$T/r
 P=$T/rag-serving-system_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 $F -c $P/rr_kernels.hip -o $B/rr_kernels.o &
 /opt/rocm/bin/hipcc --offload-arch=gfx950 $F -c $P/rr_sk.hip -o $B/rr_sk.o &
+[ -f $P/rr_topk.hip ] && /opt/rocm/bin/hipcc --offload-arch=gfx950 $F -c $P/rr_topk.hip -o $B/rr_topk.o &
 /opt/rocm/bin/hipcc $F -pthread -c $P/rr_api.cpp -o $B/rr_api.o &
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $B/*.o -L/opt/rocm/lib -lrccl -pthread -Wl,-rpath,/opt/rocm/lib \

@@ -4,6 +4,7 @@
 #   bash tools/gpu/run.sh tests smoke bench trace_x125k sq_fp32 ...
 # Steps:
 #   tests          the full GPU suite at the box's own GPU_MAX_HW_QUEUES (pytest -m gpu, per-test timeout)
+#   tests:<file>   one test file (e.g. tests:test_gpu_screen.py)
 #   smoke          __graft_entry__.smoke()
 #   bench          the driver's bench command (PMC child pass, CPU baseline)
 #   prof           bench + rocprofv3 --kernel-trace --stats of the same command (tools/prof_round.sh)
@@ -22,12 +23,15 @@ step() {
   case "$1" in
     tests) timeout -k 10 1000 python -u -m pytest -x -v --timeout 150 --timeout-method thread -m gpu "$R/tests" \
              > "$O/gpu_tests.log" 2>&1 ;;
+    tests:*) f=${1#tests:}; timeout -k 10 900 python -u -m pytest -x -v --timeout 150 --timeout-method thread -m gpu \
+             "$R/tests/$f" > "$O/gpu_tests_${f%%.py*}.log" 2>&1 ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
     bench) (cd /tmp && timeout -k 10 420 python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 > "$O/bench.json" \
              2> "$O/bench.err") ;;
     prof) bash "$R/tools/prof_round.sh" "gpurun_out/${OUT:-r4}/prof" ;;
     trace_x125k)
       Q=${QUEUES:-4}
+      mkdir -p "$O/trace_q$Q"
       (cd /tmp && GPU_MAX_HW_QUEUES=$Q timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
         -d "$O/trace_q$Q" -o x125k -- python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 --exchange-1rank \
         --docs 125000 --variants "" --no-cpu-baseline --no-pmc --ingest-rows 0 --latency-steps 20 --steady-steps 40 \
