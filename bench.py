@@ -145,6 +145,7 @@ def timed_steps(ix, k, steps, warmup, dist, cuda_sync, every=1, acct=None):
         if every > 1:
             ix.set_timing(i % every == 0)
         ix.search_staged(k)
+    t_enq = time.perf_counter() - t0           # host time to enqueue the K steps (the device may still be running)
     b1, f1, r1, w1 = ix.screen_counts_all()    # synchronises (and settles the last search)
     owed = int(sum_over_ranks(dist, float(max(0, (f1 - f0) - (r1 - r0)))))
     if owed:
@@ -162,7 +163,7 @@ def timed_steps(ix, k, steps, warmup, dist, cuda_sync, every=1, acct=None):
     ix.set_timing(False)
     if acct is not None:
         acct.update({"blocks": b1 - b0, "flagged": f1 - f0, "reruns_library": r1 - r0, "reruns_paid": owed,
-                     "wide_slots": w1 - w0})
+                     "wide_slots": w1 - w0, "host_enqueue_ms_per_step": round(t_enq / max(steps, 1) * 1e3, 4)})
     return elapsed, kern_ms, launches
 
 
@@ -462,6 +463,10 @@ def run(args, stage: dict) -> None:
                                "batches": args.latency_steps, "in_flight": 2,
                                "note": "host numpy queries in, host results out: rr_search_async (pinned H2D + "
                                        "search + D2H enqueued) / rr_wait, two batches in flight"},
+            "host_enqueue_ms_per_step": {"window": acct.get("host_enqueue_ms_per_step"),
+                                         "steady": st_acct.get("host_enqueue_ms_per_step"),
+                                         "note": "host time to enqueue one search step (rr_search_staged) in the timed "
+                                                 "loops: below ms_per_step, the device and not the host sets the rate"},
             "steady_state": {"value": round(args.batch * args.steady_steps / st_el, 2), "unit": "queries/s",
                              "steps": args.steady_steps,
                              "ms_per_step": round(st_el / args.steady_steps * 1e3, 4),

@@ -54,6 +54,17 @@ int fail(int code, const char* fmt, ...) {
 
 constexpr int kXSlots = 4;   // pipelined-exchange buffer sets (Shard::px_keys)
 
+// Host-side cost of enqueueing (diagnostics: RR_HOST_PROF=1 prints per-call averages at rr_destroy): [0] whole
+// rr_search_staged, [1] the pipelined exchange's enqueue, [2] the ncclAllGather call alone, [3] the screened block's
+// screen + verify launches; nanoseconds and calls.
+struct HostProf {
+  int64_t ns[4] = {0, 0, 0, 0}, n[4] = {0, 0, 0, 0};
+};
+inline int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
 struct Shard {
   int dev = 0;
   int cus = 256;
@@ -220,6 +231,10 @@ struct rr_handle {
   bool stream_prio = true;      // streams at the runtime's greatest priority (A/B: RR_STREAM_PRIORITY=0)
   bool failed = false;
   int wide_verify = 1;          // the verify's wide phase (A/B: RR_WIDE_VERIFY=0)
+  bool host_prof = false;       // RR_HOST_PROF=1 (diagnostics)
+  HostProf hp;
+  bool ab_no_verify = false;    // A/B only (RR_AB_NO_VERIFY=1): skip the screened search's verify launch — results
+                                // invalid; measures what the verify's launch costs the step
   // adaptive screen (observe_settled): the screen's per-lane lists grow from 4 keys to KT once blocks flag, and
   // screening pauses when even that leaves most blocks to the exact pass — decided from settled searches only
   bool full_lists = false;
@@ -967,7 +982,12 @@ int enqueue_exchange_px(rr_handle* h, int p, int x, int q0, int bb, int k, int k
     const hipStream_t xs = lane ? dst.xstream2 : dst.xstream;
     if (h->dist) {
       HIP_TRY(hipStreamWaitEvent(xs, dst.ev_keys[x], 0));
+      const int64_t ta = h->host_prof ? now_ns() : 0;
       NCCL_TRY(ncclAllGather(dst.px_keys[x], dst.px_gathered[x], slot, ncclUint64, lane ? dst.comm2 : dst.comm, xs));
+      if (h->host_prof) {
+        h->hp.ns[2] += now_ns() - ta;
+        ++h->hp.n[2];
+      }
     } else {
       for (size_t i = 0; i < h->shards.size(); ++i) {
         const Shard& src = h->shards[i];
@@ -1081,6 +1101,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       const bool alone = !two || s.last_vsi < 0 || s.last_vsi == bsi ||
                          hipEventQuery(s.ev_q[s.last_vq][s.last_vsi]) == hipSuccess;
       const int sgrid = screen_grid(h, s, alone);
+      const int64_t tl = h->host_prof ? now_ns() : 0;
       if (timed) HIP_TRY(hipEventRecord(e0, cs));
       if (s.rows() > 0) {
         rr::SkArgs a = sk_base(h, s, qb, bb);
@@ -1102,7 +1123,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       // stream (the same rows of the result buffer)
       if (two && !multi && s.last_vsi >= 0 && s.last_vsi != bsi)
         HIP_TRY(hipStreamWaitEvent(vs, s.ev_q[s.last_vq][s.last_vsi], 0));
-      if (s.rows() > 0) {
+      if (s.rows() > 0 && !h->ab_no_verify) {
         rr::SkArgs v = sk_base(h, s, qb, bb);
         v.vin = candp;
         v.nlists = sgrid;
@@ -1118,8 +1139,12 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         v.wide_verify = h->wide_verify;
         v.wide_count = s.wcount;
         HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 1, rr::kQSlots, rr::kQSlots, v, vs));
-      } else {   // a shard without rows contributes empty lists and no flag
+      } else if (!h->ab_no_verify) {   // a shard without rows contributes empty lists and no flag
         HIP_TRY(hipMemsetAsync(s.px_keys[x], 0, ((size_t)slots * kt + 1) * 8, vs));
+      }
+      if (h->host_prof) {
+        h->hp.ns[3] += now_ns() - tl;
+        ++h->hp.n[3];
       }
       if (two) {   // this verify (the last reader of query buffer t on this stream)
         HIP_TRY(hipEventRecord(s.ev_q[t][bsi], vs));
@@ -1253,7 +1278,12 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
     return RR_OK;
   }
   if (kt) {
+    const int64_t tx = h->host_prof ? now_ns() : 0;
     if (int rc = enqueue_exchange_px(h, p, x, q0, bb, k, kt, slots, scr)) return rc;
+    if (h->host_prof) {
+      h->hp.ns[1] += now_ns() - tx;
+      ++h->hp.n[1];
+    }
     h->parity ^= 1;
     h->xslot = (x + 1) % h->xslots;
     return RR_OK;
@@ -1432,6 +1462,8 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   if (const char* e = getenv("RR_DIST_TIMEOUT_MS")) h->timeout_ms = std::max(0, atoi(e));   // (the round-3 name)
   if (const char* e = getenv("RR_TIMEOUT_MS")) h->timeout_ms = std::max(0, atoi(e));
   if (const char* e = getenv("RR_WIDE_VERIFY")) h->wide_verify = atoi(e) ? 1 : 0;   // (A/B)
+  if (const char* e = getenv("RR_AB_NO_VERIFY")) h->ab_no_verify = atoi(e) != 0;    // (A/B only: invalid results)
+  if (const char* e = getenv("RR_HOST_PROF")) h->host_prof = atoi(e) != 0;
   if (const char* e = getenv("RR_SCREEN_FULL_LISTS")) h->full_lists_env = atoi(e) != 0;   // (A/B: start with full lists)
   *out = h;
   return RR_OK;
@@ -1439,6 +1471,13 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
 
 void rr_destroy(rr_handle* h) {
   if (!h) return;
+  if (h->host_prof) {
+    static const char* what[4] = {"rr_search_staged", "exchange enqueue", "ncclAllGather call", "screen+verify launches"};
+    for (int i = 0; i < 4; ++i)
+      if (h->hp.n[i])
+        fprintf(stderr, "[rr host prof] %s: %.2f us x %lld\n", what[i], h->hp.ns[i] / 1e3 / h->hp.n[i],
+                (long long)h->hp.n[i]);
+  }
   if (h->failed) {
     // device work missed its deadline: an all-gather may still be waiting for a peer. Abort the communicators
     // (their kernels observe the abort and exit) and release nothing else — freeing buffers or destroying streams
@@ -1713,7 +1752,16 @@ int rr_set_queries_device(rr_handle* h, const float* dev_q, int32_t b, int32_t d
   return RR_OK;
 }
 
+static int search_staged_body(rr_handle* h, int32_t k);
 int rr_search_staged(rr_handle* h, int32_t k) {
+  if (!h || !h->host_prof) return search_staged_body(h, k);
+  const int64_t t0 = now_ns();
+  const int rc = search_staged_body(h, k);
+  h->hp.ns[0] += now_ns() - t0;
+  ++h->hp.n[0];
+  return rc;
+}
+static int search_staged_body(rr_handle* h, int32_t k) {
   if (!h) return fail(RR_E_INVALID, "null handle");
   if (h->failed) return failed_handle();
   if (!h->loaded || h->cur_b < 1) return fail(RR_E_STATE, "no queries staged");

@@ -7,6 +7,7 @@
 #   tests:<file>   one test file (e.g. tests:test_gpu_screen.py)
 #   smoke          __graft_entry__.smoke()
 #   bench          the driver's bench command (PMC child pass, CPU baseline)
+#   bench:<name>:<args>   a short bench.py run (no CPU baseline, variants, ingest or PMC pass) with extra args
 #   prof           bench + rocprofv3 --kernel-trace --stats of the same command (tools/prof_round.sh)
 #   trace_x125k    rocprofv3 kernel + memory-copy trace of the 1-rank RCCL exchange path at the 8-GPU shard size
 #                  (Queue_Id / Stream_Id per kernel), QUEUES=4 default
@@ -28,6 +29,9 @@ step() {
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
     bench) (cd /tmp && timeout -k 10 420 python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 > "$O/bench.json" \
              2> "$O/bench.err") ;;
+    bench:*) IFS=: read -r _ name bargs <<< "$1"
+             (cd /tmp && timeout -k 10 300 python3 "$R/bench.py" --gpus 1 --no-cpu-baseline --variants= --ingest-rows 0 \
+               --no-pmc $bargs > "$O/bench_$name.json" 2> "$O/bench_$name.err") ;;
     prof) bash "$R/tools/prof_round.sh" "gpurun_out/${OUT:-r4}/prof" ;;
     trace_x125k)
       Q=${QUEUES:-4}
