@@ -107,7 +107,9 @@ struct Shard {
   int* wcount = nullptr;                 // ... query slots its verify proved in the wide phase
   int* pin_scount = nullptr;             // pinned staging of scount / wcount reads (rr_screen_counts)
   uint32_t* ctr = nullptr;               // split-K chunk counters (dynamic schedule), 0 between launches: one per
-                                         // compute stream, kCtrStride words apart
+                                         // compute stream, kCtrStride words apart; then (words 2 and 3 x kCtrStride)
+                                         // each compute stream's 64-bit count of fused-verify screen workgroups
+  uint64_t vbase[2] = {0, 0};            // ... that count when the stream's next fused launch begins
   uint64_t* shard_keys = nullptr;        // [32][k_cap] this shard's top-k (all-gather send buffer)
   uint64_t* gathered = nullptr;          // [world][32][k_cap] (all-gather receive buffer)
   // pipelined exchange (k <= RR_FUSED_KMAX, world > 1): the exchange of search i (all-gather + final
@@ -233,6 +235,7 @@ struct rr_handle {
   int wide_verify = 1;          // the verify's wide phase (A/B: RR_WIDE_VERIFY=0)
   bool host_prof = false;       // RR_HOST_PROF=1 (diagnostics)
   HostProf hp;
+  bool fuse_verify = false;     // the exchange path's screens verify their own lists (RR_FUSED_VERIFY=1; slower)
   bool ab_no_verify = false;    // A/B only (RR_AB_NO_VERIFY=1): skip the screened search's verify launch — results
                                 // invalid; measures what the verify's launch costs the step
   // adaptive screen (observe_settled): the screen's per-lane lists grow from 4 keys to KT once blocks flag, and
@@ -688,8 +691,9 @@ int ensure_buffers(rr_handle* h, int b, int k) {
       HIP_TRY(hipMemset(s.wcount, 0, sizeof(int)));
       if (!s.pin_scount) HIP_TRY(hipHostMalloc((void**)&s.pin_scount, 2 * sizeof(int), hipHostMallocDefault));
       ((volatile int*)s.pin_scount)[0] = ((volatile int*)s.pin_scount)[1] = 0;
-      if (int rc = dmalloc(&s.ctr, 2 * kCtrStride * sizeof(uint32_t))) return rc;
-      HIP_TRY(hipMemset(s.ctr, 0, 2 * kCtrStride * sizeof(uint32_t)));
+      if (int rc = dmalloc(&s.ctr, 4 * kCtrStride * sizeof(uint32_t))) return rc;
+      HIP_TRY(hipMemset(s.ctr, 0, 4 * kCtrStride * sizeof(uint32_t)));
+      s.vbase[0] = s.vbase[1] = 0;
     }
     if ((h->world > 1 || h->dist) && !s.px_keys[0]) {
       for (int p = 0; p < kXSlots; ++p) {
@@ -970,24 +974,18 @@ int local_gather(rr_handle* h, size_t per) {
 // process per GPU, peer copies within one process) into px_gathered[x] and merges it into the results,
 // while the compute stream goes on with the next block. px_keys[x] is rewritten kXSlots blocks later and only
 // after ev_xdone[x] of every shard that read it (enqueue_block).
-int enqueue_exchange_px(rr_handle* h, int p, int x, int q0, int bb, int k, int kt, int slots, bool scr) {
+// The stream operations of one exchange, after its ev_keys were recorded.
+int issue_exchange(rr_handle* h, int x, int q0, int bb, int k, int kt, int slots, int64_t* ns_gather) {
   const size_t slot = (size_t)slots * kt + kXTail;   // keys + the shard's flag word
-  for (Shard& s : h->shards) {   // px_keys[x] is written on the block's compute stream (a screened block: its parity's)
-    HIP_TRY(hipSetDevice(s.dev));
-    HIP_TRY(hipEventRecord(s.ev_keys[x], scr ? cstream(h, s, p) : s.stream));
-  }
   const int lane = x & 1;
   for (Shard& dst : h->shards) {
     HIP_TRY(hipSetDevice(dst.dev));
     const hipStream_t xs = lane ? dst.xstream2 : dst.xstream;
     if (h->dist) {
       HIP_TRY(hipStreamWaitEvent(xs, dst.ev_keys[x], 0));
-      const int64_t ta = h->host_prof ? now_ns() : 0;
+      const int64_t ta = ns_gather ? now_ns() : 0;
       NCCL_TRY(ncclAllGather(dst.px_keys[x], dst.px_gathered[x], slot, ncclUint64, lane ? dst.comm2 : dst.comm, xs));
-      if (h->host_prof) {
-        h->hp.ns[2] += now_ns() - ta;
-        ++h->hp.n[2];
-      }
+      if (ns_gather) *ns_gather += now_ns() - ta;
     } else {
       for (size_t i = 0; i < h->shards.size(); ++i) {
         const Shard& src = h->shards[i];
@@ -1007,6 +1005,22 @@ int enqueue_exchange_px(rr_handle* h, int p, int x, int q0, int bb, int k, int k
     dst.last_x = x;
   }
   return RR_OK;
+}
+
+// Pipelined exchange of the block just scored into px_keys[x] (k <= RR_FUSED_KMAX, an exchange step): ev_keys[x] on the
+// block's compute stream, then the exchange's stream operations.
+int enqueue_exchange_px(rr_handle* h, int p, int x, int q0, int bb, int k, int kt, int slots, bool scr) {
+  for (Shard& s : h->shards) {   // px_keys[x] is written on the block's compute stream (a screened block: its parity's)
+    HIP_TRY(hipSetDevice(s.dev));
+    HIP_TRY(hipEventRecord(s.ev_keys[x], scr ? cstream(h, s, p) : s.stream));
+  }
+  int64_t ng = 0;
+  const int rc = issue_exchange(h, x, q0, bb, k, kt, slots, h->host_prof ? &ng : nullptr);
+  if (ng) {
+    h->hp.ns[2] += ng;
+    ++h->hp.n[2];
+  }
+  return rc;
 }
 
 // Query slots of one corpus pass for a search of b queries at k.
@@ -1098,9 +1112,20 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       }
       if (multi) HIP_TRY(wait_px(x, cs));
       uint64_t* candp = s.cand + (size_t)p * cand_half(s);
+      // the f16 copy holds exactly the values the fp32-reading screen rounds to: half the bytes
+      const bool s16 = s.scr16 && h->screen_copy && rr::sk_slabs(rr::KDT_SCREEN16, d);
+      // Fused verify (rr_sk.hip fused_verify): with an exchange step the verify writes keys, not result rows, so the
+      // screen's last 32 workgroups can verify in the same launch; the screen then always takes every CU.
+      const int full_grid = screen_grid(h, s, true);
+      const bool fuse = multi && h->fuse_verify && !h->ab_no_verify && s.rows() > 0 && s16 && h->dyn_sched && kt <= 16 &&
+                        2 * rr::sk_slabs(rr::KDT_SCREEN16, d) <= 4 && full_grid >= 2 * rr::kQSlots;
       const bool alone = !two || s.last_vsi < 0 || s.last_vsi == bsi ||
                          hipEventQuery(s.ev_q[s.last_vq][s.last_vsi]) == hipSuccess;
-      const int sgrid = screen_grid(h, s, alone);
+      // A fused launch must have its whole grid resident (its verifiers wait for every workgroup's lists): alone it
+      // takes every CU; beside the other stream's fused launch each takes half, so the two always fit together (a
+      // workgroup left waiting for a CU the other launch holds would hold back this block's verify by a whole screen).
+      const int sgrid = fuse ? (alone ? full_grid : std::max(2 * rr::kQSlots, std::min(full_grid, s.cus / 2)))
+                             : screen_grid(h, s, alone);
       const int64_t tl = h->host_prof ? now_ns() : 0;
       if (timed) HIP_TRY(hipEventRecord(e0, cs));
       if (s.rows() > 0) {
@@ -1109,12 +1134,27 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         a.clear_word = multi ? s.px_keys[x] + (size_t)slots * kt : nullptr;   // the verify below may raise it
         a.ctr = s.ctr + (cs == s.stream ? 0 : kCtrStride);
         a.sqrt_d = sqrtf((float)d) * (1.0f + 0x1p-20f);
-        // the f16 copy holds exactly the values the fp32-reading screen rounds to: half the bytes
-        const bool s16 = s.scr16 && h->screen_copy && rr::sk_slabs(rr::KDT_SCREEN16, d);
         a.full_lists = h->full_lists ? 1 : 0;
         a.eps_a = s16 ? kScreen16EpsA : kScreenEpsA;
         a.eps_b = s16 ? kScreen16EpsB : kScreenEpsB;
         if (s16) a.corpus = (const char*)s.scr16;
+        if (fuse) {   // the verify's arguments (below) on the screen's launch
+          a.fuse = 1;
+          a.vcorpus = (const char*)s.corpus;
+          a.vsync = (uint64_t*)(s.ctr + (2 + bsi) * kCtrStride);
+          a.vbase = s.vbase[bsi];
+          s.vbase[bsi] += (uint64_t)sgrid;
+          a.vin = candp;
+          a.nlists = sgrid;
+          a.k_out = k;
+          a.out_keys = s.px_keys[x];
+          a.flag = s.px_keys[x] + (size_t)slots * kt;
+          a.count = s.scount;
+          a.seq = seq;
+          a.force_incomplete = h->kernel == RR_KERNEL_SCREEN_FALLBACK;
+          a.wide_verify = h->wide_verify;
+          a.wide_count = s.wcount;
+        }
         HIP_TRY(rr::launch_sk_args(s16 ? rr::KDT_SCREEN16 : rr::KDT_SCREEN, h->metric, kt, 0, sgrid, rr::kQSlots, a,
                                    cs));
       }
@@ -1123,7 +1163,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       // stream (the same rows of the result buffer)
       if (two && !multi && s.last_vsi >= 0 && s.last_vsi != bsi)
         HIP_TRY(hipStreamWaitEvent(vs, s.ev_q[s.last_vq][s.last_vsi], 0));
-      if (s.rows() > 0 && !h->ab_no_verify) {
+      if (s.rows() > 0 && !h->ab_no_verify && !fuse) {
         rr::SkArgs v = sk_base(h, s, qb, bb);
         v.vin = candp;
         v.nlists = sgrid;
@@ -1139,7 +1179,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         v.wide_verify = h->wide_verify;
         v.wide_count = s.wcount;
         HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 1, rr::kQSlots, rr::kQSlots, v, vs));
-      } else if (!h->ab_no_verify) {   // a shard without rows contributes empty lists and no flag
+      } else if (!h->ab_no_verify && !fuse) {   // a shard without rows contributes empty lists and no flag
         HIP_TRY(hipMemsetAsync(s.px_keys[x], 0, ((size_t)slots * kt + 1) * 8, vs));
       }
       if (h->host_prof) {
@@ -1243,7 +1283,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         HIP_TRY(hipStreamWaitEvent(s.xstream2, s.ev_cdone, 0));
       }
     } else {
-      // k > RR_FUSED_KMAX: all keys of this shard, segmented radix sort, keep the first k. The exchange
+      // k > RR_FUSED_KMAX: all keys of this shard, their top-k sorted (rr_topk.hip). The exchange
       // is serial on the compute stream, after every pipelined exchange still writing results.
       const int64_t rows = s.rows();
       if (int rc = ensure_full_sort(h, s, k)) return rc;
@@ -1464,6 +1504,7 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   if (const char* e = getenv("RR_WIDE_VERIFY")) h->wide_verify = atoi(e) ? 1 : 0;   // (A/B)
   if (const char* e = getenv("RR_AB_NO_VERIFY")) h->ab_no_verify = atoi(e) != 0;    // (A/B only: invalid results)
   if (const char* e = getenv("RR_HOST_PROF")) h->host_prof = atoi(e) != 0;
+  if (const char* e = getenv("RR_FUSED_VERIFY")) h->fuse_verify = atoi(e) != 0;   // (A/B)
   if (const char* e = getenv("RR_SCREEN_FULL_LISTS")) h->full_lists_env = atoi(e) != 0;   // (A/B: start with full lists)
   *out = h;
   return RR_OK;

@@ -81,6 +81,14 @@ struct SkArgs {
   uint64_t* floors;
   // MODE 0, KT 32, 32 slots: every key instead of lists, all_keys[q * n + row] for q < b (full-sort path)
   uint64_t* all_keys;
+  // Fused verify (MODE 0, the f16-copy screen on the dynamic schedule, KT <= 16): the screen's last 32 workgroups to
+  // finish verify one query slot each (the MODE 1 fields above: vin = out, nlists = grid, k_out, out_keys, flag,
+  // count, seq, force_incomplete, wide_verify, wide_count) over the fp32 rows vcorpus. vsync: the compute stream's
+  // count of screen workgroups that finished (never reset); vbase: its value when this launch began.
+  int fuse;
+  const char* vcorpus;
+  uint64_t* vsync;
+  uint64_t vbase;
 };
 
 // Split-K streaming kernel (rr_sk.hip): same output contract as launch_fused. sdt = KDT_* (0..3).

@@ -391,6 +391,225 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
   __syncthreads();
 }
 
+// ---- Fused verify ---------------------------------------------------------------------------------------------
+// The f16-copy screen on the dynamic schedule (DT 7, SCHED 1, KT <= 16) can verify its own lists (SkArgs::fuse): the
+// last 32 workgroups to finish the screen wait until every workgroup has published its lists, then each verifies one
+// query slot — exactly the MODE 1 verify (same candidates, same exact DT 3 arithmetic: K split over the 8 waves,
+// MFMA order, wave order of the partial sums, the cosine quotient and clip; the same completeness proof and wide
+// phase), so results are bit-identical. No kernel boundary between the screen and its verify, and no CUs held back
+// for a separate verify launch. Registers: the 9-wave screen's budget (168 VGPRs), so the verify here keeps no
+// per-lane lists: a tile's 32 exact keys go through LDS and the top-KT is kept by rank selection.
+// LDS (all free after the screen): [0, 16 KiB) the list merge's scratch, [16, 20 KiB) the query, [20 KiB, ring end)
+// the wide phase's rows; the partial block of the screen (red) for the K-partials; the MODE 1 scalars block.
+constexpr int kFvQueryOff = 16384;
+constexpr int kFvWideOff = 20480;
+constexpr int kFvWideCap = (int)((ring_bytes(2) - kFvWideOff) / 4);
+
+template <int NSV, int KT, bool COS>
+__device__ __forceinline__ void fused_verify(const SkArgs& a, const int vq, char* smem, float* red, float* qinfo,
+                                             uint64_t* akeys, int* grow, float* gnorm, int* gvalid, uint64_t* xk,
+                                             uint64_t* vfloor, uint64_t* vtail, int* vstate, uint64_t* tkeys,
+                                             const bool lists_ok) {
+  constexpr int QS = 32;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int d = a.d;
+  const uint32_t idx_base = a.idx_base;
+  const char* __restrict__ vcorpus = a.vcorpus;
+  const int row_bytes = d * 4;
+  constexpr int KSV = NSV * kSlabRowBytes;   // bytes of a row per wave (fp32 rows)
+  const int p0 = w * (KSV / 16);
+  float* qv = (float*)(smem + kFvQueryOff);
+  int* wl = (int*)(smem + kFvWideOff);
+  if (vq >= a.b) {   // padding slot: keep the exchange buffer uniform
+    if (a.out_keys && tid < KT) a.out_keys[(size_t)vq * KT + tid] = 0;
+    return;
+  }
+  // the query into LDS; |q| and max |q| by wave 0 exactly as the exact pass computes them
+  for (int e = 4 * tid; e < d; e += 4 * kThreads) *(f32x4*)(qv + e) = *(const f32x4*)(a.queries + (size_t)vq * d + e);
+  if (w == 0) {
+    const int nc = d >> 2;
+    f32x4 v[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int cc = lane + 64 * c;
+      v[c] = zero_unless(((const f32x4*)a.queries)[(size_t)vq * nc + (cc < nc ? cc : 0)], opaque_mask(cc < nc));
+    }
+    float ss = 0.f, m = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (lane + 64 * c < nc) {
+        const f32x4 x = v[c];
+        ss = fmaf(x.x, x.x, ss); ss = fmaf(x.y, x.y, ss); ss = fmaf(x.z, x.z, ss); ss = fmaf(x.w, x.w, ss);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+      }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      ss += __shfl_xor(ss, off, 64);
+      m = fmaxf(m, __shfl_xor(m, off, 64));
+    }
+    if (lane == 0) {
+      qinfo[vq] = sqrtf(ss);
+      qinfo[QS + vq] = m;
+    }
+  }
+  __syncthreads();
+  const float qn = qinfo[vq];
+  merge_lists_for_query<KT>(a.vin, a.nlists, QS, vq, (uint64_t*)smem, akeys, vfloor, vtail);
+  if (tid < 32) {
+    const uint64_t k0 = akeys[0];
+    const uint64_t key = tid < KT ? akeys[tid] : 0;
+    const int64_t first = k0 ? (int64_t)(0xFFFFFFFFu - (uint32_t)k0) - idx_base : 0;
+    const int64_t row = key ? (int64_t)(0xFFFFFFFFu - (uint32_t)key) - idx_base : first;
+    grow[tid] = (int)row;
+    gvalid[tid] = key != 0;
+    gnorm[tid] = COS ? a.norms[row] : 0.f;
+  }
+  if (tid < KT) xk[tid] = 0;
+  __syncthreads();
+
+  // exact keys of the 32 rows grow[] (gvalid: 0 -> key 0) into tkeys[]: the DT 3 tile of the full pass with query vq
+  auto score_tile = [&]() {
+    const char* src = vcorpus + (int64_t)grow[r] * row_bytes + (size_t)w * KSV;
+    f32x4 vr[NSV][4];
+#pragma unroll
+    for (int j = 0; j < NSV; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        vr[j][i] = *(const f32x4*)(src + j * kSlabRowBytes + ((4 * (i >> 1) + 2 * h + (i & 1)) << 4));
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NSV; ++j)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const float x[8] = {vr[j][2 * t].x, vr[j][2 * t].y, vr[j][2 * t].z, vr[j][2 * t].w,
+                            vr[j][2 * t + 1].x, vr[j][2 * t + 1].y, vr[j][2 * t + 1].z, vr[j][2 * t + 1].w};
+        bf16x8 b0, b1, b2, c0, c1, c2;
+        split3(x, b0, b1, b2);
+        const f32x4 qa = *(const f32x4*)(qv + 4 * inv_pair(p0 + 8 * j + 4 * t + 2 * h));
+        const f32x4 qb = *(const f32x4*)(qv + 4 * inv_pair(p0 + 8 * j + 4 * t + 2 * h + 1));
+        const float qx[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+        split3(qx, c0, c1, c2);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c0, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c1, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c0, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c1, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c2, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, c0, acc, 0, 0, 0);
+      }
+    // every column holds query vq: column 0's partials (lanes 0 and 32: docs 8a + 4h + i), summed in wave order
+    if (r == 0) {
+#pragma unroll
+      for (int a4 = 0; a4 < 4; ++a4)
+        *(f32x4*)(red + w * 32 + 8 * a4 + 4 * h) = (f32x4){acc[4 * a4], acc[4 * a4 + 1], acc[4 * a4 + 2], acc[4 * a4 + 3]};
+    }
+    __syncthreads();
+    if (tid < 32) {
+      float sv = red[tid];
+#pragma unroll
+      for (int ww = 1; ww < kWaves; ++ww) sv = sv + red[ww * 32 + tid];
+      uint64_t key = 0;
+      if (gvalid[tid]) {
+        float c = sv;
+        if constexpr (COS) {
+          c = c / cos_den(qn, gnorm[tid]);   // IEEE division then clip, as every exact path (retriever.py:605-609)
+          c = fminf(fmaxf(c, -1.0f), 1.0f);
+        }
+        key = make_key(c, idx_base + (uint32_t)grow[tid]);
+      }
+      tkeys[tid] = key;
+    }
+    __syncthreads();
+  };
+  // the running top-KT (xk, descending) and the tile's keys -> the new top-KT, by rank (keys are unique but for 0)
+  auto merge_tile = [&]() {
+    uint64_t me = 0;
+    if (tid < KT + 32) me = tid < KT ? xk[tid] : tkeys[tid - KT];
+    int rank = 0;
+    if (me != 0) {
+      for (int i = 0; i < KT; ++i) rank += xk[i] > me ? 1 : 0;
+      for (int i = 0; i < 32; ++i) rank += tkeys[i] > me ? 1 : 0;
+    }
+    __syncthreads();
+    if (tid < KT) xk[tid] = 0;
+    __syncthreads();
+    if (me != 0 && rank < KT) xk[rank] = me;
+    __syncthreads();
+  };
+  auto finish = [&](bool complete) {   // (thread 0)
+    complete = complete && lists_ok && qinfo[QS + vq] < 32768.0f && !a.force_incomplete;
+    if (!complete)
+      if (__hip_atomic_fetch_max(a.flag, (uint64_t)a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint64_t)a.seq)
+        __hip_atomic_fetch_add(a.count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (vq == 0) __hip_atomic_fetch_add(a.count + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.out_keys)
+      for (int i = 0; i < KT; ++i) a.out_keys[(size_t)vq * KT + i] = xk[i];
+    if (a.out_scores)
+      for (int i = 0; i < a.k_out; ++i) {
+        const uint64_t key = xk[i];
+        a.out_scores[(size_t)vq * a.k_out + i] = key ? float_of_ord((uint32_t)(key >> 32)) : -INFINITY;
+        a.out_idx[(size_t)vq * a.k_out + i] = key ? (int64_t)(0xFFFFFFFFu - (uint32_t)key) : -1;
+      }
+  };
+
+  score_tile();
+  merge_tile();
+  if (tid == 0) {
+    const uint64_t ukt = umax64(akeys[KT - 1], *vfloor);
+    const uint64_t ek = xk[a.k_out - 1];
+    const bool complete = ukt == 0 || (ek != 0 && (uint32_t)(ek >> 32) > (uint32_t)(ukt >> 32));
+    const uint64_t tb = *vtail;
+    const bool wide = !complete && lists_ok && a.wide_verify && !a.force_incomplete && qinfo[QS + vq] < 32768.0f &&
+                      (uint32_t)(akeys[a.k_out - 1] >> 32) > (uint32_t)(tb >> 32);
+    vstate[0] = wide ? 1 : 0;
+    vstate[1] = 0;
+    if (!wide) finish(complete);
+  }
+  __syncthreads();
+  if (vstate[0] != 1) return;
+
+  // wide phase (MODE 1's): every list entry whose bound is above the largest single-list bound, rescored exactly
+  const uint32_t tb_ord = (uint32_t)(*vtail >> 32);
+  for (int l = tid; l < a.nlists; l += kThreads) {
+    const uint64_t* src = a.vin + ((size_t)vq * a.nlists + l) * (KT + 1);
+    int c = 0;
+    while (c < KT && (uint32_t)(src[c] >> 32) > tb_ord) ++c;   // a prefix of the sorted list
+    if (c) {
+      const int pos = atomicAdd(&vstate[1], c);
+      for (int i = 0; i < c; ++i)
+        if (pos + i < kFvWideCap) wl[pos + i] = (int)((int64_t)(0xFFFFFFFFu - (uint32_t)src[i]) - idx_base);
+    }
+  }
+  __syncthreads();
+  const int nr = vstate[1];
+  if (nr > kFvWideCap) {
+    if (tid == 0) finish(false);
+    return;
+  }
+  if (tid < KT) xk[tid] = 0;
+  __syncthreads();
+  for (int t = 0; t < (nr + 31) / 32; ++t) {
+    if (tid < 32) {
+      const int i = 32 * t + tid;
+      const int row = wl[i < nr ? i : 0];
+      grow[tid] = row;
+      gvalid[tid] = i < nr;
+      gnorm[tid] = COS ? a.norms[row] : 0.f;
+    }
+    __syncthreads();
+    score_tile();
+    merge_tile();
+  }
+  if (tid == 0) {
+    const uint64_t ek = xk[a.k_out - 1];
+    const bool complete = tb_ord == 0 || (ek != 0 && (uint32_t)(ek >> 32) > tb_ord);
+    if (complete && a.wide_count) __hip_atomic_fetch_add(a.wide_count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    finish(complete);
+  }
+}
+
 // QH = query halves: 32 * QH query slots per pass (64 for the batch-64 configs: one corpus pass serves
 // them all; each A fragment then feeds the MFMAs of both halves).
 // MODE 0: top-KT per query over this workgroup's rows (DT 6: by upper bound).
@@ -1433,6 +1652,37 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       const uint64_t m = group_max_u64<LPQ>(tk.v[0]);
       if (m != 0 && tk.v[0] == m) tk.pop();
       if (lane % LPQ == 0) dst[rnd] = m;
+    }
+    if constexpr (DT == 7 && SCHED == 1 && QH == 1 && KT <= 16) {
+      if (a.fuse) {   // fused verify (see fused_verify): the last 32 workgroups verify one query slot each
+        // The stream's 64-bit counter of finished screen workgroups is never reset: this launch's workgroups are the
+        // ones counted from vbase (the host adds each fused launch's grid), so even a verifier that gave up waiting
+        // cannot leave the next launch miscounted.
+        int* fv = vstate;   // [2] this workgroup's finishing rank, [3] every list published in time
+        __threadfence();    // this workgroup's lists: visible to every XCD before it counts itself done
+        __syncthreads();
+        if (tid == 0)
+          fv[2] = (int)(__hip_atomic_fetch_add(a.vsync, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) -
+                        a.vbase);
+        __syncthreads();
+        const int tkt = fv[2];
+        if (tkt < (int)G - QS) return;
+        if (tid == 0) {   // wait for the other workgroups' lists; bounded (a miss flags the block: exact re-run)
+          bool ok = false;
+          for (int it = 0; it < (1 << 21); ++it) {
+            if (__hip_atomic_load(a.vsync, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= a.vbase + (uint64_t)G) {
+              ok = true;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+          }
+          fv[3] = ok ? 1 : 0;
+        }
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        fused_verify<2 * NS, KT, COS>(a, tkt - ((int)G - QS), smem, red, qinfo, akeys, grow, gnorm, gvalid, xk, vfloor,
+                                      vtail, vstate, vW, fv[3] != 0);
+      }
     }
   } else if constexpr (MODE == 1) {
     // The wave that owns query slot vq (QH 1: queries 4w..4w+3) merges its lanes' lists into xk; its leader lane

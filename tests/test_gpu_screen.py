@@ -522,3 +522,47 @@ def test_two_compute_streams_match_one(Index, devices):
 
     for (s1, i1), (s2, i2) in zip(run(1), run(2)):
         assert np.array_equal(i1, i2) and np.array_equal(s1, s2)
+
+
+@pytest.mark.parametrize("layout", ["interleaved", "contiguous"])
+def test_fused_verify_matches_separate_verify(Index, layout, monkeypatch):
+    """With an exchange step (here a 1-rank RCCL communicator) the screen's last 32 workgroups verify their own lists
+    in the same launch (rr_sk.hip fused_verify) instead of a separate verify launch. On near-duplicate clusters —
+    interleaved: the wide phase proves every query slot; contiguous: blocks flag and re-run exactly — the fused
+    handle's results, flags, re-runs and wide-phase proofs equal the separate-verify handle's (RR_FUSED_VERIFY=0),
+    and both equal the exact kernel, for k = 5 and 10, over back-to-back staged searches too."""
+    from rag_service_amd import get_unique_id
+    corpus, q = _clustered(60000, 0.01, layout)
+    ex = Index(dtype="fp32", metric="cosine")
+    ex.load(corpus)
+    ex.set_kernel("exact")
+    handles = {}
+    for fused in (True, False):
+        monkeypatch.setenv("RR_FUSED_VERIFY", "1" if fused else "0")
+        ix = Index(dtype="fp32", metric="cosine")
+        monkeypatch.delenv("RR_FUSED_VERIFY")
+        ix.init_dist(1, 0, get_unique_id())
+        ix.load(corpus)
+        ix.set_schedule(True)
+        handles[fused] = ix
+    counts = {}
+    for fused, ix in handles.items():
+        for k in (5, 10):
+            want = ex.search(q, k)
+            got = ix.search(q, k)
+            assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), (fused, k)
+            ix.set_queries(q)
+            for _ in range(6):
+                ix.search_staged(k)
+            got = ix.fetch()
+            assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), (fused, k, "staged")
+        counts[fused] = ix.screen_counts_all()
+        ix.close()
+    print(layout, counts)
+    blocks, flagged, reruns, wide = counts[True]
+    assert blocks == counts[False][0] == 14
+    if layout == "interleaved":     # the fused verify's wide phase proves what the separate one proves
+        assert flagged == 0 and wide >= 32 and counts[False][1] == 0 and counts[False][3] >= 32
+    else:
+        assert flagged >= 1 and reruns >= 1
+    ex.close()
