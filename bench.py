@@ -35,9 +35,9 @@ sys.path.insert(0, os.path.join(REPO, "rag-serving-system_amd"))
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "retrieval queries/sec + p99 latency, batch=32, 1M docs d=1024, 1/2/4/8 GPU"
 SCORE_KERNEL_DOC = ("the corpus-streaming kernel: sk_score_kernel MODE 0 (split-K, LDS-DMA; for fp32 storage the "
-                    "screened search's screen — DT 7 over the f16 screening copy of the rows when the handle keeps "
-                    "one, else DT 6 over the fp32 rows — whose exact fp32 verify of the candidates runs overlapped "
-                    "on the exchange stream), else fused_score_kernel")
+                    "screened search's screen — DT 8 over the int8 screening copy (d a multiple of 512 up to 1024), "
+                    "DT 7 over the f16 copy, else DT 6 over the fp32 rows — whose exact fp32 verify of the candidates "
+                    "runs on the other compute stream), else fused_score_kernel")
 
 
 def is_score_kernel(name: str) -> bool:
@@ -106,10 +106,14 @@ def cpu_baseline(n_docs: int, d: int, batch: int, k: int, budget_s: float) -> di
                                       "argpartition/argsort (a stronger CPU point)"}}
 
 
-def algorithmic_bytes(rows: int, d: int, batch: int, dtype: str, metric: str, screen16: bool = False) -> int:
+def algorithmic_bytes(rows: int, d: int, batch: int, dtype: str, metric: str, screen16: bool = False,
+                      screen8: bool = False) -> int:
     """HBM bytes one corpus-streaming launch must move: the rows once (4 B/element fp32 and fp32-split, 2 B bf16,
-    2 B when the fp32 screen streams the f16 screening copy), the per-row factors it reads (norm for cosine,
-    row scale for fp32-split), the fp32 queries once."""
+    2 B when the fp32 screen streams the f16 screening copy, 1 B the int8 copy), the per-row factors it reads (norm
+    for cosine, row scale for fp32-split; the int8 copy's norm, scale and error norm), the queries once (fp32; the
+    int8 screen's two int8 pieces of 32 slots)."""
+    if screen8:
+        return rows * (d + 12) + 2 * 32 * d + 4 * 32 * 4
     elem = 2 if dtype == "bf16" or screen16 else 4
     # per-row factors: the norm (cosine; and the fp32 screen's error bound for either metric), the split scale
     per_row = (4 if metric == "cosine" or dtype == "fp32" else 0) + (4 if dtype == "fp32-split" else 0)
@@ -348,7 +352,8 @@ def run(args, stage: dict) -> None:
     n_local = se - sb
     # the fp32 screened search (k <= 29) streams the f16 screening copy when the handle keeps one
     screen16 = args.dtype == "fp32" and args.k <= 29 and ix.screen_copy()
-    alg_bytes = algorithmic_bytes(n_local, args.dim, args.batch, args.dtype, args.metric, screen16)
+    screen8 = screen16 and ix.screen_int8()   # ... and the int8 copy, unless the adaptive screen gave it up
+    alg_bytes = algorithmic_bytes(n_local, args.dim, args.batch, args.dtype, args.metric, screen16, screen8)
     fp32_floor = n_local * args.dim * 4 + args.batch * args.dim * 4
     avg_kernel_s = (kern_ms / max(launches, 1)) / 1e3
     step_s = elapsed / args.steps
@@ -507,13 +512,15 @@ def run(args, stage: dict) -> None:
                          "frac_vs_fp32_floor": round(fp32_floor / step_s / 1e9 / HBM_PEAK_GBS, 4),
                          "frac_vs_fp32_floor_steady": round(fp32_floor / (st_el / args.steady_steps) / 1e9
                                                             / HBM_PEAK_GBS, 4),
-                         "basis_note": ("frac = the bytes the launch streams (the f16 screening copy + norms) / step "
+                         "basis_note": ("frac = the bytes the launch streams (the int8 or f16 screening copy + per-row "
+                                        "factors) / step "
                                         "time; frac_vs_fp32_floor = the fp32 corpus bytes SURVEY §8(d) prices (4 B per "
                                         "element) / step time — above 1 because the screen proves most fp32 rows "
                                         "need not be read; valid only with every flagged block's exact re-run paid "
                                         "(screen_fallbacks_timed, reruns_paid)" if screen16 else
                                         "frac and frac_vs_fp32_floor on the same rows"),
                          "screen_copy": bool(screen16),
+                         "screen_int8": bool(screen8),
                          "screen_fallbacks_timed": acct.get("flagged"),
                          "reruns_paid": acct.get("reruns_paid"),
                          "reruns_by_library_timed": acct.get("reruns_library"),

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 6
+#define RR_ABI_VERSION 7
 
 /* error codes */
 #define RR_OK             0
@@ -221,6 +221,16 @@ int rr_set_compute_streams(rr_handle* h, int32_t n, int32_t* in_use);
  * and screen from the fp32 rows, -1: leave as is. *present (may be null): the copy is in use on every local
  * shard. */
 int rr_screen_copy(rr_handle* h, int32_t use, int32_t* present);
+
+/* The screened search's int8 copy (fp32 storage, d a multiple of 512 up to 1024, beside the f16 copy): per row a
+ * scale and the rounding error's norm, the rows as int8 — a quarter of the fp32 bytes per screen — against two int8
+ * pieces of each query (v_mfma_i32_32x32x32_i8). Its upper bound (exact integer sums + the error norms, Cauchy-
+ * Schwarz) is ~8x looser than the f16 copy's, so more rows reach the verify; results are bit-identical either way.
+ * Adaptive: when more than 1 in 32 settled blocks of a window re-run, the handle screens the f16 copy instead (reset
+ * at every load). Made at load time when it fits (default; RR_SCREEN_I8=0 at creation: not made). use = 1: screen it
+ * (re-armed; from the next load if none was made), 0: screen the f16 copy, -1: leave as is. *active (may be null):
+ * the next search screens the int8 copy on every local shard. */
+int rr_screen_int8(rr_handle* h, int32_t use, int32_t* active);
 
 /* Screened-search counters since the corpus was (re)loaded: search blocks screened (summed over local
  * shards) and how many of them needed the exact fallback pass. Synchronises the handle's streams. */

@@ -77,6 +77,13 @@ struct Shard {
   int64_t row_begin = 0, row_end = 0;   // global rows held
   void* corpus = nullptr;                // [rows][d] fp32 or bf16
   uint16_t* scr16 = nullptr;             // fp32 storage: f16 copy of the rows for the screened search (or null)
+  // fp32 storage: the int8 screen's copy (rr_sk.hip DT 8; or null): [round_up(rows, 2)][d] int8 rows (a padding row
+  // of zeros), per row its scale and error norm ([rows]); per compute stream the queries' int8 pieces and scalars
+  int8_t* scr8 = nullptr;
+  float* sx8 = nullptr;
+  float* e8 = nullptr;
+  int8_t* q8[2] = {nullptr, nullptr};
+  float* q8s[2] = {nullptr, nullptr};
   float* norms = nullptr;                // [round_up(rows, 32) + 32] |row| (pad = 1)
   float* rscale = nullptr;               // [same] split-f16 row scale 2^-e (pad = 1)
   float* qbuf[2] = {nullptr, nullptr};   // staged queries, double-buffered ([q_cap][d] fp32 each): a new
@@ -170,6 +177,7 @@ struct AsyncSlot {
   bool pending = false;
   bool screened = false;   // the search ran screened blocks, the first with sequence number seq0
   bool narrow = false;     // ... with 16-entry lists where 2k + 2 wanted 32
+  bool i8 = false;         // ... screening the int8 copy
   bool full = false, wide = false;   // ... full per-lane lists / the handle's screen_wide at the time
   int blocks = 0;          // ... screened blocks
   int seq0 = 0;
@@ -220,6 +228,9 @@ struct rr_handle {
   int xslots = kXSlots;         // pipelined-exchange buffer sets in use (A/B: RR_X_SLOTS, 2..kXSlots)
   int x_delay_us = 0;           // A/B: RR_X_EXCHANGE_DELAY_US, a stand-in for a slower exchange
   int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy)
+  int screen_i8 = 1;            // ... and an int8 copy, screened first (rr_screen_int8; RR_SCREEN_I8=0 at creation: off)
+  bool i8_off = false;          // adaptive: the int8 screen re-ran too often on this corpus, the f16 copy screens
+  bool last_i8 = false;         // the last search screened the int8 copy
   int64_t narrow_settled = 0;   // settled screened blocks run with 16-entry lists where 2k + 2 wanted 32 (screen_kt)
   int64_t narrow_reruns = 0;    // ... of them re-run exactly
   bool screen_wide = false;     // narrow lists re-ran too often on this corpus: use the wide ones
@@ -369,7 +380,7 @@ int dmalloc(T** p, size_t bytes) {
 
 int free_shard(Shard& s) {
   hipSetDevice(s.dev);
-  void* ptrs[] = {s.corpus, s.scr16, s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.wcount, s.ctr, s.shard_keys, s.gathered, s.out_base,
+  void* ptrs[] = {s.corpus, s.scr16, s.scr8, s.sx8, s.e8, s.q8[0], s.q8[1], s.q8s[0], s.q8s[1], s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.wcount, s.ctr, s.shard_keys, s.gathered, s.out_base,
                   s.full_keys, s.sort_temp, s.wcand, s.wfloor, s.wsel};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -398,6 +409,17 @@ int free_shard(Shard& s) {
   return RR_OK;
 }
 
+// Release the shard's int8 screen copy and its query buffers (current device = s.dev).
+void free_i8(Shard& s) {
+  for (void* p : {(void*)s.scr8, (void*)s.sx8, (void*)s.e8, (void*)s.q8[0], (void*)s.q8[1], (void*)s.q8s[0],
+                  (void*)s.q8s[1]})
+    if (p) hipFree(p);
+  s.scr8 = nullptr;
+  s.sx8 = s.e8 = nullptr;
+  s.q8[0] = s.q8[1] = nullptr;
+  s.q8s[0] = s.q8s[1] = nullptr;
+}
+
 // Allocate the shard's corpus storage for the current range (and norms when cosine).
 int alloc_corpus(rr_handle* h, Shard& s) {
   HIP_TRY(hipSetDevice(s.dev));
@@ -407,6 +429,7 @@ int alloc_corpus(rr_handle* h, Shard& s) {
   // reads the fp32 rows and rounds them to f16 in registers (the same values)
   if (s.scr16) HIP_TRY(hipFree(s.scr16));
   s.scr16 = nullptr;
+  free_i8(s);
   size_t free_b = 0, total_b = 0;
   const size_t need16 = (size_t)rows * h->d * 2;
   if (h->dtype == RR_DTYPE_F32 && h->screen_copy && rows > 0 && hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
@@ -414,6 +437,29 @@ int alloc_corpus(rr_handle* h, Shard& s) {
     if (hipMalloc((void**)&s.scr16, need16) != hipSuccess) {
       s.scr16 = nullptr;
       (void)hipGetLastError();
+    }
+  }
+  // the int8 copy (a quarter of the fp32 bytes; d a multiple of 512 up to 1024), next to the f16 one it falls back to
+  if (s.scr16 && h->screen_i8 && rr::sk_slabs(rr::KDT_SCREEN8, h->d) && hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+    const int64_t r2 = (rows + 1) / 2 * 2;
+    const size_t need8 = (size_t)r2 * h->d + 2 * (size_t)r2 * 4;
+    if (free_b > need8 + (4ull << 30)) {
+      bool ok = hipMalloc((void**)&s.scr8, (size_t)r2 * h->d) == hipSuccess;
+      ok = ok && hipMalloc((void**)&s.sx8, (size_t)r2 * 4) == hipSuccess;
+      ok = ok && hipMalloc((void**)&s.e8, (size_t)r2 * 4) == hipSuccess;
+      for (int i = 0; i < 2 && ok; ++i) {
+        ok = hipMalloc((void**)&s.q8[i], (size_t)2 * rr::kQSlots * h->d) == hipSuccess;
+        ok = ok && hipMalloc((void**)&s.q8s[i], (size_t)4 * rr::kQSlots * 4) == hipSuccess;
+      }
+      // the padding row (odd row counts) is read as the second half of the last kernel row: zeros, scale 0
+      if (ok && r2 > rows) {
+        ok = hipMemset(s.scr8 + (size_t)rows * h->d, 0, h->d) == hipSuccess;
+        ok = ok && hipMemset(s.sx8 + rows, 0, 4) == hipSuccess && hipMemset(s.e8 + rows, 0, 4) == hipSuccess;
+      }
+      if (!ok) {
+        (void)hipGetLastError();
+        free_i8(s);
+      }
     }
   }
   const int64_t npad = (rows + rr::kTileDocs - 1) / rr::kTileDocs * rr::kTileDocs + rr::kTileDocs;
@@ -499,6 +545,10 @@ hipError_t store_rows(rr_handle* h, Shard& s, const float* tmp, int64_t dst_row,
     default:
       if (s.scr16)
         if (hipError_t e = rr::launch_f32_to_f16(tmp, s.scr16 + dst_row * d, nr, d, s.stream)) return e;
+      if (s.scr8)
+        if (hipError_t e = rr::launch_f32_to_i8(tmp, nr, d, s.scr8 + dst_row * d, s.sx8 + dst_row, s.e8 + dst_row,
+                                                s.stream))
+          return e;
       return rr::launch_permute_f32(tmp, (float*)s.corpus + dst_row * d, nr, d, 0, s.stream);
   }
 }
@@ -612,6 +662,7 @@ int drop_work_buffers(rr_handle* h) {
   h->narrow_settled = h->narrow_reruns = 0;
   h->screen_wide = false;
   h->full_lists = h->full_lists_env;
+  h->i8_off = false;
   h->win_nb = h->win_nf = 0;
   h->screen_pause = h->pauses = 0;
   h->last_screened = false;
@@ -777,6 +828,13 @@ constexpr float kScreenEpsB = 4.0e-8f;
 // the margins; 8 instead of 16 MFMAs per wave partial only shrink the accumulation term).
 constexpr float kScreen16EpsA = 1.1e-3f;
 constexpr float kScreen16EpsB = 7.5e-8f;
+// DT 8 (the int8 copy) bounds its own arithmetic exactly from the per-row error norms and the query residual
+// (rr_sk.hip epilogue): eps_a / eps_b carry only the exact DT 3 score's error (4.9e-5 |x||q| + the subnormal term)
+constexpr float kScreen8EpsA = 6.0e-5f;
+constexpr float kScreen8EpsB = 4.0e-8f;
+
+// The int8 copy screens (shards that hold one) unless turned off or given way to the f16 copy (observe_settled).
+bool i8_active(const rr_handle* h) { return h->screen_i8 && !h->i8_off && h->screen_copy; }
 
 bool screened(const rr_handle* h, int k, int slots) {
   return (h->kernel == RR_KERNEL_AUTO || h->kernel == RR_KERNEL_SCREEN_FALLBACK) && h->dtype == RR_DTYPE_F32 &&
@@ -793,6 +851,8 @@ bool screened(const rr_handle* h, int k, int slots) {
 // narrow -> wide switch under rr_init_dist. A staged search nobody collects is not observed (its outcome is never
 // read; the bench pays its re-run itself).
 //   * narrow (16-entry) lists -> 32-entry ones when more than 1 in 32 settled narrow blocks re-ran (over >= 64);
+//   * the int8 copy's screen -> the f16 copy's when more than 1 in 32 blocks of a window re-ran (its bound is ~8x
+//     looser: corpora whose top scores crowd within it);
 //   * windows of >= 32 settled screened blocks of the current configuration (list width, per-lane list form):
 //     short per-lane lists (4 keys + the workgroup's floor, rr_sk.hip KL) -> full lists (KT keys) when more than
 //     1 in 32 re-ran (each costs an exact pass, twice a screen: 3 % re-run cost more than the full lists do):
@@ -802,7 +862,7 @@ bool screened(const rr_handle* h, int k, int slots) {
 //     screening for 1024 blocks (the one-pass exact kernel alone), then probe again. Not while this k screens with
 //     the narrow lists (the 32-entry ones are tried first).
 // A block counts as re-run when its search was (a flagged search re-runs all its blocks). Reset at every load.
-void observe_settled(rr_handle* h, int blocks, bool narrow, bool full, bool wide, bool rerun) {
+void observe_settled(rr_handle* h, int blocks, bool narrow, bool full, bool wide, bool i8, bool rerun) {
   if (blocks <= 0) return;
   const int nre = rerun ? blocks : 0;
   if (narrow && !h->screen_wide) {
@@ -815,11 +875,15 @@ void observe_settled(rr_handle* h, int blocks, bool narrow, bool full, bool wide
     }
   }
   // a search enqueued under another configuration than the current one (before a switch or a pause) tells nothing
-  if (h->screen_pause > 0 || full != h->full_lists || (narrow && h->screen_wide) || wide != h->screen_wide) return;
+  if (h->screen_pause > 0 || full != h->full_lists || (narrow && h->screen_wide) || wide != h->screen_wide ||
+      i8 != i8_active(h))
+    return;
   h->win_nb += blocks;
   h->win_nf += nre;
   if (h->win_nb < 32) return;
-  if (!h->full_lists) {
+  if (i8) {   // the int8 screen's looser bound first gives way to the f16 copy's
+    if (h->win_nf * 32 > h->win_nb) h->i8_off = true;
+  } else if (!h->full_lists) {
     if (h->win_nf * 32 > h->win_nb) h->full_lists = true;
   } else if (h->win_nf * 2 > h->win_nb && !narrow) {
     h->screen_pause = 1024;
@@ -1114,10 +1178,12 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       uint64_t* candp = s.cand + (size_t)p * cand_half(s);
       // the f16 copy holds exactly the values the fp32-reading screen rounds to: half the bytes
       const bool s16 = s.scr16 && h->screen_copy && rr::sk_slabs(rr::KDT_SCREEN16, d);
+      // the int8 copy: a quarter of the fp32 bytes, a bound ~8x looser (more rows reach the verify's wide phase)
+      const bool s8 = s16 && s.scr8 && i8_active(h);
       // Fused verify (rr_sk.hip fused_verify): with an exchange step the verify writes keys, not result rows, so the
       // screen's last 32 workgroups can verify in the same launch; the screen then always takes every CU.
       const int full_grid = screen_grid(h, s, true);
-      const bool fuse = multi && h->fuse_verify && !h->ab_no_verify && s.rows() > 0 && s16 && h->dyn_sched && kt <= 16 &&
+      const bool fuse = multi && h->fuse_verify && !h->ab_no_verify && s.rows() > 0 && s16 && !s8 && h->dyn_sched && kt <= 16 &&
                         2 * rr::sk_slabs(rr::KDT_SCREEN16, d) <= 4 && full_grid >= 2 * rr::kQSlots;
       const bool alone = !two || s.last_vsi < 0 || s.last_vsi == bsi ||
                          hipEventQuery(s.ev_q[s.last_vq][s.last_vsi]) == hipSuccess;
@@ -1138,6 +1204,18 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         a.eps_a = s16 ? kScreen16EpsA : kScreenEpsA;
         a.eps_b = s16 ? kScreen16EpsB : kScreenEpsB;
         if (s16) a.corpus = (const char*)s.scr16;
+        if (s8) {   // the queries' int8 pieces on this stream first (the previous block's screen here is done with them)
+          HIP_TRY(rr::launch_q8_prep(qb, bb, d, s.q8[bsi], s.q8s[bsi], cs));
+          a.corpus = (const char*)s.scr8;
+          a.n = (s.rows() + 1) / 2;
+          a.rows8 = s.rows();
+          a.q8 = s.q8[bsi];
+          a.q8s = s.q8s[bsi];
+          a.sx8 = s.sx8;
+          a.e8 = s.e8;
+          a.eps_a = kScreen8EpsA;
+          a.eps_b = kScreen8EpsB;
+        }
         if (fuse) {   // the verify's arguments (below) on the screen's launch
           a.fuse = 1;
           a.vcorpus = (const char*)s.corpus;
@@ -1155,8 +1233,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
           a.wide_verify = h->wide_verify;
           a.wide_count = s.wcount;
         }
-        HIP_TRY(rr::launch_sk_args(s16 ? rr::KDT_SCREEN16 : rr::KDT_SCREEN, h->metric, kt, 0, sgrid, rr::kQSlots, a,
-                                   cs));
+        HIP_TRY(rr::launch_sk_args(s8 ? rr::KDT_SCREEN8 : s16 ? rr::KDT_SCREEN16 : rr::KDT_SCREEN, h->metric, kt, 0,
+                                   sgrid, rr::kQSlots, a, cs));
       }
       if (timed) HIP_TRY(hipEventRecord(e1, cs));
       // results written in place (no exchange): this verify follows the previous one when that ran on the other
@@ -1505,6 +1583,8 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   if (const char* e = getenv("RR_AB_NO_VERIFY")) h->ab_no_verify = atoi(e) != 0;    // (A/B only: invalid results)
   if (const char* e = getenv("RR_HOST_PROF")) h->host_prof = atoi(e) != 0;
   if (const char* e = getenv("RR_FUSED_VERIFY")) h->fuse_verify = atoi(e) != 0;   // (A/B)
+  if (const char* e = getenv("RR_SCREEN_I8")) h->screen_i8 = atoi(e) != 0;         // (A/B: 0 = the f16 copy only)
+  if (const char* e = getenv("RR_STATIC_SCHEDULE")) h->dyn_sched = atoi(e) == 0;   // (A/B: 1 = rr_set_schedule(0))
   if (const char* e = getenv("RR_SCREEN_FULL_LISTS")) h->full_lists_env = atoi(e) != 0;   // (A/B: start with full lists)
   *out = h;
   return RR_OK;
@@ -1814,6 +1894,7 @@ static int search_staged_body(rr_handle* h, int32_t k) {
   h->last_narrow = screened(h, k, slots) && narrow_lists(h, k);
   h->last_full = h->full_lists;
   h->last_wide = h->screen_wide;
+  h->last_i8 = i8_active(h);
   h->last_blocks = screened(h, k, slots) ? (b + slots - 1) / slots : 0;
   h->last_seq0 = h->screen_seq + 1;
   h->last_settled = !h->last_screened;
@@ -1874,7 +1955,7 @@ int settle_screen(rr_handle* h, uint64_t flag, bool* rerun) {
   if (!h->last_screened || h->last_settled) return RR_OK;
   h->last_settled = true;
   const bool flagged = flag >= (uint64_t)h->last_seq0;
-  observe_settled(h, h->last_blocks, h->last_narrow, h->last_full, h->last_wide, flagged);
+  observe_settled(h, h->last_blocks, h->last_narrow, h->last_full, h->last_wide, h->last_i8, flagged);
   if (!flagged) return RR_OK;
   // the search's own queries (begin_stage keeps its buffer intact until it is settled); a batch staged
   // since stays staged
@@ -2017,6 +2098,7 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
   a.ticket = t;
   a.screened = h->last_screened;
   a.narrow = h->last_narrow;
+  a.i8 = h->last_i8;
   a.full = h->last_full;
   a.wide = h->last_wide;
   a.blocks = h->last_blocks;
@@ -2040,7 +2122,7 @@ int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx) {
   const size_t idx_off = res_off + ((kOutHead + cnt * 4 + 255) & ~(size_t)255);
   uint64_t flag = 0;
   memcpy(&flag, a.pin + res_off, sizeof flag);
-  if (a.screened) observe_settled(h, a.blocks, a.narrow, a.full, a.wide, flag >= (uint64_t)a.seq0);
+  if (a.screened) observe_settled(h, a.blocks, a.narrow, a.full, a.wide, a.i8, flag >= (uint64_t)a.seq0);
   if (a.screened && flag >= (uint64_t)a.seq0) {
     // a block needed the exact pass: this batch again, exactly (every rank of an exchange sees the same
     // flag here, so all re-run it together). A batch staged with rr_set_queries before this wait stays the
@@ -2161,17 +2243,34 @@ int rr_screen_copy(rr_handle* h, int32_t use, int32_t* present) {
     if (!use)   // every stream of the handle may still be screening from the copy
       if (int rc = sync_streams(h)) return rc;
     if (!use)
-      for (Shard& s : h->shards)
+      for (Shard& s : h->shards) {
+        HIP_TRY(hipSetDevice(s.dev));
+        free_i8(s);
         if (s.scr16) {
-          HIP_TRY(hipSetDevice(s.dev));
           HIP_TRY(hipFree(s.scr16));
           s.scr16 = nullptr;
         }
+      }
   }
   if (present) {
     bool all = !h->shards.empty();
     for (const Shard& s : h->shards) all = all && (s.scr16 != nullptr || s.rows() == 0);
     *present = all && h->screen_copy && h->loaded ? 1 : 0;
+  }
+  return RR_OK;
+}
+
+int rr_screen_int8(rr_handle* h, int32_t use, int32_t* active) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  if (h->failed) return failed_handle();
+  if (use >= 0) {
+    h->screen_i8 = use ? 1 : 0;
+    if (use) h->i8_off = false;   // re-armed (a copy exists only if the handle loaded with it on)
+  }
+  if (active) {
+    bool all = !h->shards.empty();
+    for (const Shard& s : h->shards) all = all && ((s.scr8 != nullptr && s.scr16 != nullptr) || s.rows() == 0);
+    *active = all && i8_active(h) && h->loaded ? 1 : 0;
   }
   return RR_OK;
 }

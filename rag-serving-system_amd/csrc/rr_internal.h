@@ -31,6 +31,9 @@ constexpr int KDT_SCREEN = 6;
 //   KDT_SCREEN16 : the same screen over an f16 copy of the fp32 rows (the values KDT_SCREEN rounds to in
 //                  registers, stored: half the bytes per screened search; rr_sk.hip DT 7)
 constexpr int KDT_SCREEN16 = 7;
+//   KDT_SCREEN8  : the screen over an int8 copy (per-row scale, per-row error norm; a quarter of the fp32 bytes)
+//                  against the query's two int8 pieces, v_mfma_i32_32x32x32_i8 (rr_sk.hip DT 8)
+constexpr int KDT_SCREEN8 = 8;
 
 // Smallest fused-kernel list width KT >= k (4, 8, 16, 32); 0 if k > RR_FUSED_KMAX.
 int fused_kt(int k);
@@ -89,6 +92,14 @@ struct SkArgs {
   const char* vcorpus;
   uint64_t* vsync;
   uint64_t vbase;
+  // int8 screen (KDT_SCREEN8): corpus = the int8 copy, read as n = ceil(rows8 / 2) kernel rows of two corpus rows each;
+  // sx8 / e8 [rows8] the rows' scales and error norms; q8 [2][32][d] the queries' int8 pieces and q8s [4][32] their
+  // scalars (launch_q8_prep)
+  const int8_t* q8;
+  const float* q8s;
+  const float* sx8;
+  const float* e8;
+  int64_t rows8;
 };
 
 // Split-K streaming kernel (rr_sk.hip): same output contract as launch_fused. sdt = KDT_* (0..3).
@@ -170,6 +181,12 @@ hipError_t launch_permute_f32(const float* in, float* out, int64_t nrows, int d,
 hipError_t launch_f32_to_bf16(const float* in, uint16_t* out, int64_t nrows, int d, hipStream_t s);
 // fp32 rows -> f16 (round to nearest even) in the same 8-element pair_unit layout as bf16 storage (the screen copy)
 hipError_t launch_f32_to_f16(const float* in, uint16_t* out, int64_t nrows, int d, hipStream_t s);
+// fp32 rows (natural order) -> the int8 screen copy: per row sx = max|x| / 127, x8 = clamp(rint(x / sx), +-127),
+// e = an upper bound of |x - sx * x8| (rr_kernels.hip f32_to_i8_kernel)
+hipError_t launch_f32_to_i8(const float* in, int64_t nrows, int d, int8_t* out, float* sx, float* e, hipStream_t s);
+// The int8 screen's query pieces for a block of b <= 32 queries (slots b..31 zeroed): q8 [2][32][d], q8s [4][32] =
+// |q|, sum|q|, the pieces' scale / 64, an upper bound of |q - scale * (p1 + p2 / 64)|
+hipError_t launch_q8_prep(const float* q, int b, int d, int8_t* q8, float* q8s, hipStream_t s);
 hipError_t launch_row_norms(int dtype, const void* corpus, int64_t n, int d, float* norms, hipStream_t s);
 hipError_t launch_synth(int kind, uint64_t seed, int64_t row_begin, int64_t n_rows, int d, float* out,
                         hipStream_t s);

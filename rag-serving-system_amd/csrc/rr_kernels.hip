@@ -798,6 +798,120 @@ __global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict_
   }
 }
 
+// fp32 rows (natural element order) -> the int8 screen copy (rr_sk.hip DT 8), one wave per row:
+//   sx = max|x| / 127 (0 for a zero row), x8 = clamp(rint(x / sx), -127, 127) — any x8 is valid, the bound uses e —
+//   e >= |x - sx x8|_2 (real arithmetic): the fp32 residuals' norm, each residual within 2^-24 (|x| + 2 |r|) of the
+//   real one (the product sx x8 and the subtraction round once each), so + 2^-22 max|x| sqrt(d) covers
+//   2^-24 (|x|_2 + sx sqrt(d)); the sum of squares (<= d / 64 + 6 roundings a chain) and the sqrt within 2^-14,
+//   covered by the 2^-12 relative bump.
+__global__ __launch_bounds__(256) void f32_to_i8_kernel(const float* __restrict__ in, int64_t n, int d,
+                                                        uint32_t* __restrict__ out, float* __restrict__ sx,
+                                                        float* __restrict__ e8) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const f32x4* src = (const f32x4*)(in + row * d);
+  float m = 0.f;
+  for (int c = lane; c < (d >> 2); c += 64) {
+    const f32x4 v = src[c];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  const float s = m > 0.f ? m / 127.0f : 0.f;
+  float ss = 0.f;
+  uint32_t* dst = out + row * (d >> 2);
+  for (int c = lane; c < (d >> 2); c += 64) {
+    const f32x4 v = src[c];
+    uint32_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x = v[j];
+      const float q = s > 0.f ? fminf(fmaxf(rintf(x / s), -127.0f), 127.0f) : 0.f;
+      const float r = x - s * q;
+      ss = fmaf(r, r, ss);
+      packed |= ((uint32_t)(int)q & 0xFFu) << (8 * j);
+    }
+    dst[c] = packed;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) ss += __shfl_xor(ss, off, 64);
+  if (lane == 0) {
+    sx[row] = s;
+    e8[row] = fmaf(sqrtf(ss), 1.0f + 0x1p-12f, m * sqrtf((float)d) * 0x1p-22f);
+  }
+}
+
+// The int8 screen's query pieces, one workgroup per query slot: s = max|q| / 127, p1 = clamp(rint(q / s)), p2 =
+// clamp(rint((q / s - p1) * 64)) — q ~ s (p1 + p2 / 64), the MFMAs' sum being x8 . (64 p1 + p2) — and eq >= the
+// residual's norm (real arithmetic; the same accounting as f32_to_i8_kernel). |q| and sum|q| in fp32 (the bound
+// bumps for their summation order). Slots >= b: zero pieces and scalars.
+__global__ __launch_bounds__(256) void q8_prep_kernel(const float* __restrict__ q, int b, int d,
+                                                      int8_t* __restrict__ q8, float* __restrict__ q8s) {
+  const int slot = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  __shared__ float red[3][4];
+  int8_t* p1 = q8 + (size_t)slot * d;
+  int8_t* p2 = q8 + (size_t)(kQSlots + slot) * d;
+  if (slot >= b) {
+    for (int e = tid; e < d; e += 256) {
+      p1[e] = 0;
+      p2[e] = 0;
+    }
+    if (tid < 4) q8s[tid * kQSlots + slot] = 0.f;
+    return;
+  }
+  const float* src = q + (size_t)slot * d;
+  float m = 0.f, s2 = 0.f, s1 = 0.f;
+  for (int e = tid; e < d; e += 256) {
+    const float x = src[e];
+    m = fmaxf(m, fabsf(x));
+    s2 = fmaf(x, x, s2);
+    s1 += fabsf(x);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    m = fmaxf(m, __shfl_xor(m, off, 64));
+    s2 += __shfl_xor(s2, off, 64);
+    s1 += __shfl_xor(s1, off, 64);
+  }
+  if (lane == 0) {
+    red[0][wv] = m;
+    red[1][wv] = s2;
+    red[2][wv] = s1;
+  }
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+  const float qn2 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  const float qsa = (red[2][0] + red[2][1]) + (red[2][2] + red[2][3]);
+  const float s = m > 0.f ? m / 127.0f : 0.f;
+  float se = 0.f;
+  for (int e = tid; e < d; e += 256) {
+    const float x = src[e];
+    float a = 0.f, c = 0.f;
+    if (s > 0.f) {
+      const float t = x / s;
+      a = fminf(fmaxf(rintf(t), -127.0f), 127.0f);
+      c = fminf(fmaxf(rintf((t - a) * 64.0f), -127.0f), 127.0f);
+    }
+    p1[e] = (int8_t)(int)a;
+    p2[e] = (int8_t)(int)c;
+    const float r = x - s * (a * 64.0f + c) * 0x1p-6f;
+    se = fmaf(r, r, se);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) se += __shfl_xor(se, off, 64);
+  __syncthreads();
+  if (lane == 0) red[0][wv] = se;
+  __syncthreads();
+  if (tid == 0) {
+    const float sev = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    q8s[slot] = sqrtf(qn2);
+    q8s[kQSlots + slot] = qsa * (1.0f + 0x1p-18f);
+    q8s[2 * kQSlots + slot] = s * 0x1p-6f;
+    q8s[3 * kQSlots + slot] = fmaf(sqrtf(sev), 1.0f + 0x1p-12f, m * sqrtf((float)d) * 0x1p-21f);
+  }
+}
+
 __global__ void unsplit_f32_kernel(const u32x4* __restrict__ in, const float* __restrict__ rscale, int64_t n,
                                    int d, float* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // one 8-element group
@@ -1030,6 +1144,19 @@ hipError_t launch_f32_to_f16(const float* in, uint16_t* out, int64_t nrows, int 
   const int64_t groups = nrows * (d >> 3);
   hipLaunchKernelGGL(f32_to_16_kernel<true>, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, in,
                      (u32x4*)out, nrows, d);
+  return hipGetLastError();
+}
+
+hipError_t launch_f32_to_i8(const float* in, int64_t nrows, int d, int8_t* out, float* sx, float* e, hipStream_t s) {
+  if (nrows < 1 || d % 4 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(f32_to_i8_kernel, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, s, in, nrows, d,
+                     (uint32_t*)out, sx, e);
+  return hipGetLastError();
+}
+
+hipError_t launch_q8_prep(const float* q, int b, int d, int8_t* q8, float* q8s, hipStream_t s) {
+  if (b < 1 || b > kQSlots || d < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(q8_prep_kernel, dim3(kQSlots), dim3(256), 0, s, q, b, d, q8, q8s);
   return hipGetLastError();
 }
 

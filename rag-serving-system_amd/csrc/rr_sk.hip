@@ -180,13 +180,15 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 // s_waitcnt vmcnt(n) for the n the issue sequence leaves (workgroup- or wave-uniform): 0, or one slab (4)
-// plus up to two single-instruction extras of wave 0 (per-row factors, chunk counter)
+// plus wave 0's single-instruction extras (per-row factors: 1, the int8 screen's 3; chunk counter)
 __device__ __forceinline__ void wait_vm_n(int n) {
   switch (n) {
     case 0: wait_vm<0>(); break;
     case 4: wait_vm<4>(); break;
     case 5: wait_vm<5>(); break;
-    default: wait_vm<6>(); break;
+    case 6: wait_vm<6>(); break;
+    case 7: wait_vm<7>(); break;
+    default: wait_vm<8>(); break;
   }
 }
 // One 4-byte-per-lane LDS-DMA load (the per-row factors of a tile: 64 lanes x 4 B), default policy.
@@ -261,6 +263,10 @@ template <int NS>
 struct QFrag<6, NS> { f16x8 c0[NS][2], c1[NS][2]; };          // screen: q = c0 + c1 (+ <= 2^-22 |q|)
 template <int NS>
 struct QFrag<7, NS> { f16x8 c0[NS][4]; };   // screen over the f16 copy: 4 K-steps per slab, q as one f16 piece
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+template <int NS>
+struct QFrag<8, NS> { i32x4 c1[NS][4], c2[NS][4]; };   // int8 screen: 4 K-steps of 32 per slab, two int8 pieces
 
 
 // LDS byte offset (within a slot) of 16-byte column position cp of tile row r (swizzled image)
@@ -389,6 +395,19 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
     if (rank < KT) akeys[rank] = me;
   }
   __syncthreads();
+}
+
+// The wide phase's bar (MODE 1 and the fused verify; ords of keys). vtail = the largest bound of any single list:
+// every key missing from every list is at most vtail. Two cases prove the block with one more pass over the lists:
+//   * the first pass's exact k-th key ek lies above vtail: the true k-th score is at least ek's, so only rows whose
+//     bound reaches ek can be in the top-k — and all of them are list entries (anything else is <= vtail < ek). R =
+//     the entries with bound >= ek: typically a few rows more than KT, where the bound is looser than KT - k
+//     ranks of the score distribution (the int8 screen, or a crowded top);
+//   * else, when the k-th largest bound lies above vtail (near-duplicate clusters): R = every entry above vtail.
+// Either way the exact k-th key of R is above vtail and the block is complete.
+__device__ __forceinline__ uint32_t wide_bar(uint64_t ek, uint64_t tb) {
+  const uint32_t e = (uint32_t)(ek >> 32), t = (uint32_t)(tb >> 32);
+  return ek != 0 && e > t ? e : t + 1;
 }
 
 // ---- Fused verify ---------------------------------------------------------------------------------------------
@@ -562,20 +581,23 @@ __device__ __forceinline__ void fused_verify(const SkArgs& a, const int vq, char
     const bool complete = ukt == 0 || (ek != 0 && (uint32_t)(ek >> 32) > (uint32_t)(ukt >> 32));
     const uint64_t tb = *vtail;
     const bool wide = !complete && lists_ok && a.wide_verify && !a.force_incomplete && qinfo[QS + vq] < 32768.0f &&
-                      (uint32_t)(akeys[a.k_out - 1] >> 32) > (uint32_t)(tb >> 32);
+                      ((uint32_t)(ek >> 32) > (uint32_t)(tb >> 32) ||
+                       (uint32_t)(akeys[a.k_out - 1] >> 32) > (uint32_t)(tb >> 32));
     vstate[0] = wide ? 1 : 0;
     vstate[1] = 0;
+    vstate[4] = (int)wide_bar(ek, tb);
     if (!wide) finish(complete);
   }
   __syncthreads();
   if (vstate[0] != 1) return;
 
-  // wide phase (MODE 1's): every list entry whose bound is above the largest single-list bound, rescored exactly
+  // wide phase (MODE 1's): every list entry whose bound reaches wide_bar, rescored exactly
   const uint32_t tb_ord = (uint32_t)(*vtail >> 32);
+  const uint32_t rbar = (uint32_t)vstate[4];
   for (int l = tid; l < a.nlists; l += kThreads) {
     const uint64_t* src = a.vin + ((size_t)vq * a.nlists + l) * (KT + 1);
     int c = 0;
-    while (c < KT && (uint32_t)(src[c] >> 32) > tb_ord) ++c;   // a prefix of the sorted list
+    while (c < KT && (uint32_t)(src[c] >> 32) >= rbar) ++c;   // a prefix of the sorted list
     if (c) {
       const int pos = atomicAdd(&vstate[1], c);
       for (int i = 0; i < c; ++i)
@@ -636,7 +658,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
-  constexpr bool SCR = DT == 6 || DT == 7;                      // the screen (upper bounds, "Screened search")
+  constexpr bool SCR = DT == 6 || DT == 7 || DT == 8;           // the screen (upper bounds, "Screened search")
   // The screen's per-lane lists hold KL keys, not KT: a query's LPQ lanes together still hold >= KT, and a lane drops
   // a key only below its own last entry. The workgroup reports the largest last entry of its full lanes as its FLOOR
   // (no key missing from its list is above max(the list's KT-th key, the floor)); the verify adds the floors to its
@@ -644,16 +666,23 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // (FL = 1: full lists, KL = KT — the handle switches to them when the short lists' floors stop the verify's
   // proofs, e.g. near-duplicate clusters whose copies crowd a few lanes; rr_api.cpp observe_settled)
   constexpr int KL = SCR && KT > 4 && !FL ? 4 : KT;
-  constexpr int EB = DT == 1 || DT == 7 ? 2 : 4;                // storage bytes per element
-  const int row_bytes = d * EB;
+  constexpr int EB = DT == 1 || DT == 7 ? 2 : DT == 8 ? 1 : 4;   // storage bytes per element
+  // the int8 screen reads two corpus rows as one kernel row (waves 0-3 the first, 4-7 the second): its tiles then
+  // carry 64 KiB like the f16 copy's, 64 corpus rows each (int8 tiles of 32 rows would halve every per-tile cost's
+  // share of the bytes it pays for)
+  constexpr int RPK = DT == 8 ? 2 : 1;
+  const int row_bytes = d * EB * RPK;
   constexpr int KS = NS * kSlabRowBytes;                        // bytes of a row per wave
   const int p0 = w * (KS / 16);                                 // first 16-byte storage unit of the slice
 
   float* red = (float*)(smem + ring_bytes(RS));
   constexpr int SW = (COS || SCR ? 1 : 0) + (DT == 2 ? 1 : 0);   // per-row factors (norm, split scale)
-  constexpr int FX = SW > 0 ? 1 : 0;                            // LDS-DMA instructions per tile for them
-  float* trow = (float*)(smem + ring_bytes(RS) + red_bytes(RS, QH));   // [4 tiles][2 factors][32 rows]
-  int* nxt = (int*)(trow + 4 * 64);                             // [2] next chunk (dynamic schedule), + pad
+  // LDS-DMA instructions per tile for them: one (64 lanes: 2 factors x 32 rows), or the int8 screen's three (norm,
+  // scale, error norm of 64 corpus rows)
+  constexpr int FX = DT == 8 ? 3 : SW > 0 ? 1 : 0;
+  constexpr int TRS = DT == 8 ? 192 : 64;                       // floats per factor slot
+  float* trow = (float*)(smem + ring_bytes(RS) + red_bytes(RS, QH));   // [4 tiles][TRS]
+  int* nxt = (int*)(trow + 4 * TRS);                            // [2] next chunk (dynamic schedule), + pad
   float* qinfo = (float*)(nxt + 4);                             // [QS] |q|, [QS] 2^-e / sum|q| / max|q|, [QS] int e
   int* qexp = (int*)(qinfo + 2 * QS);
 
@@ -668,7 +697,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   uint64_t* xk = (uint64_t*)(gvalid + 32);
   uint64_t* vfloor = xk + KT;   // MODE 1: the largest floor of the screen's lists (see KL)
   uint64_t* vtail = vfloor + 1; // MODE 1: the largest bound of any single list, max(KT-th key, floor) (wide verify)
-  int* vstate = (int*)(vtail + 1);   // MODE 1: [0] what the leader decided after the first check, [1] |R|
+  int* vstate = (int*)(vtail + 1);   // MODE 1: [0] what the leader decided after the first check, [1] |R|, [4] R's bar
   // MODE 1 reads its 32 gathered rows straight into registers (all loads issued at once: one latency), the
   // exact fragments the LDS image would give: lane (r, h) takes 16-byte units 4(i>>1) + 2h + (i&1) of slab j
   f32x4 vrow[MODE == 1 ? NS : 1][4];
@@ -727,10 +756,18 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // wave 0: the per-row factors of the tile at row base into factor slot ts (lanes 0-31: the norm, or the
   // split scale when there is no norm; lanes 32-63: the split scale next to a norm)
   auto issue_factors = [&](int64_t base, int ts) {
-    int64_t row = base + (lane & 31);
-    row = row < n ? row : n - 1;
-    const float* src = ((SW == 2 && lane >= 32) || (DT == 2 && !COS)) ? rscale : norms;
-    glds4(src + row, trow_lds + ts * 256);
+    if constexpr (DT == 8) {   // corpus rows 2 base + lane: norm, scale, error norm
+      int64_t row = 2 * base + lane;
+      row = row < a.rows8 ? row : a.rows8 - 1;
+      glds4(norms + row, trow_lds + ts * TRS * 4);
+      glds4(a.sx8 + row, trow_lds + ts * TRS * 4 + 256);
+      glds4(a.e8 + row, trow_lds + ts * TRS * 4 + 512);
+    } else {
+      int64_t row = base + (lane & 31);
+      row = row < n ? row : n - 1;
+      const float* src = ((SW == 2 && lane >= 32) || (DT == 2 && !COS)) ? rscale : norms;
+      glds4(src + row, trow_lds + ts * 256);
+    }
   };
 
   if constexpr (SCHED) {
@@ -850,6 +887,18 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
               qf.lo[j][t][e] = (__bf16)(x - (float)bh);
             }
           }
+        } else if constexpr (DT == 8) {
+          // the query prep kernel's int8 pieces (natural element order, padding slots zero): wave w's K-slice of the
+          // two-row kernel row is elements (w % 4) KS .. + KS of its corpus row; K-step t, lane half h: 16 elements
+          // at 32 t + 16 h of slab j — the 16-byte column 2t + h of the LDS image, as DT 7
+          const int8_t* p1 = a.q8 + (size_t)rq * d;
+          const int8_t* p2 = a.q8 + (size_t)(QS + rq) * d;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int e0 = (w & (kWaves / 2 - 1)) * KS + j * kSlabRowBytes + 32 * t + 16 * h;
+            qf.c1[j][t] = *(const i32x4*)(p1 + e0);
+            qf.c2[j][t] = *(const i32x4*)(p2 + e0);
+          }
         } else if constexpr (DT == 7) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) {   // the bf16 layout (position 2t + h, 8 elements), f16 pieces c0 + c1
@@ -928,6 +977,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         } else if constexpr (DT == 7) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) asm volatile("" : "+v"(qfs[qh].c0[j][t]));
+        } else if constexpr (DT == 8) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) asm volatile("" : "+v"(qfs[qh].c1[j][t]), "+v"(qfs[qh].c2[j][t]));
         } else {
 #pragma unroll
           for (int t = 0; t < 2; ++t) asm volatile("" : "+v"(qfs[qh].c0[j][t]), "+v"(qfs[qh].c1[j][t]));
@@ -977,11 +1029,13 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     // summed per query in wave order below. No second read of the query rows: every workgroup re-reading all 32
     // rows from L2 was the larger part of the launch's start-up (8-10 us). The order of these sums differs from
     // the exact path's |q|, so the bound takes a 2^-18 relative bump for it (rr_sk.hip epilogue).
-    const float ss = scr_ss + __shfl_xor(scr_ss, 32, 64), sa = scr_sa + __shfl_xor(scr_sa, 32, 64);
-    float* part = (float*)vW;
-    if (lane < 32) {
-      part[w * 32 + lane] = ss;
-      part[kWaves * 32 + w * 32 + lane] = sa;
+    if constexpr (DT != 8) {   // (the int8 screen's scalars come from the query prep kernel)
+      const float ss = scr_ss + __shfl_xor(scr_ss, 32, 64), sa = scr_sa + __shfl_xor(scr_sa, 32, 64);
+      float* part = (float*)vW;
+      if (lane < 32) {
+        part[w * 32 + lane] = ss;
+        part[kWaves * 32 + w * 32 + lane] = sa;
+      }
     }
     __syncthreads();
   } else if (COS || DT == 2) {
@@ -1067,14 +1121,20 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // epilogue lane mapping: wave w owns queries 4·QH·w + [0, 4·QH); LPQ lanes per query, each with DPL
   // consecutive tile rows (QH 1: 16 lanes x 2 rows, QH 2: 8 lanes x 4 rows)
   constexpr int LPQ = 16 / QH, DPL = 2 * QH;
+  constexpr int DPO = DPL * RPK;   // scores per lane and tile (the int8 screen: the two corpus rows of each kernel row)
   constexpr int J = (KT + LPQ - 1) / LPQ;   // (the epilogue's tighter bar: each lane's J-th list entry)
   static_assert(J <= KL, "the tighter bar reads each lane's J-th entry");
   const int qe = 4 * QH * w + lane / LPQ, er = DPL * (lane % LPQ);
   const bool qev = MODE == 1 ? qe == vq : qe < b;
   float qn = COS && !SCR ? qinfo[qe] : 0.f;
   const float qs = DT == 2 ? qinfo[QS + qe] : 1.f;
-  float qsa = 0.f;
-  if constexpr (SCR) {
+  float qsa = 0.f, q8sc = 0.f, q8eq = 0.f;
+  if constexpr (DT == 8) {
+    qn = a.q8s[qe];
+    qsa = a.q8s[QS + qe];
+    q8sc = a.q8s[2 * QS + qe];
+    q8eq = a.q8s[3 * QS + qe];
+  } else if constexpr (SCR) {
     const float* part = (const float*)vW;
     float s2 = 0.f, s1 = 0.f;
 #pragma unroll
@@ -1095,7 +1155,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // The metric epilogue of one tile: its summed scores svp (this lane's DPL rows), its first row bse and its factor
   // slot tsl. (Issuing it one tile late, in the next tile's MFMA shadow, measured -2 % on the 64-slot bf16 kernel
   // and neutral on the screen: profiles/r03/a/ab_pipelined_epilogue_rejected.txt.)
-  auto epilogue = [&](const float (&svp)[DPL], int64_t bse, int tsl) {
+  auto epilogue = [&](const float (&svp)[DPO], int64_t bse, int tsl) {
 #if defined(RR_SK_DIAG) && (RR_SK_DIAG & 1)
       // diagnostic builds only (tools/kbench_cfg5.hip): no epilogue, the sums kept live by one compare each
 #pragma unroll
@@ -1140,8 +1200,11 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         }
       }
       // rows of this tile (scalar; 32 except in the last tile): the screen's validity test is one 32-bit compare
-      const int rem = MODE == 0 ? (int)(n - bse < 32 ? n - bse : 32) : 32;
-      const uint32_t key_base = MODE == 0 ? idx_base + (uint32_t)bse : 0u;
+      // (the int8 screen: corpus rows of this 64-row tile, lane rows 2 er .. 2 er + 3)
+      const int rem = DT == 8 ? (int)(a.rows8 - 2 * bse < 64 ? a.rows8 - 2 * bse : 64)
+                              : MODE == 0 ? (int)(n - bse < 32 ? n - bse : 32) : 32;
+      const uint32_t key_base = MODE == 0 ? idx_base + (uint32_t)(RPK * bse) : 0u;
+      const int ero = RPK * er;   // this lane's first tile row
       // the exact paths' prefilter, rcp-free: s / den >= thr  <=  s >= thr * den (den > 0), evaluated as one fma of
       // per-tile terms; within 2^-20 relative of the quotient's own rounding, like the margin above
       float thq = 0.f, th8 = -INFINITY;
@@ -1153,8 +1216,17 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       }
       const float thf = th != 0 ? float_of_ord(th) : -INFINITY;   // dot: the bar's float (ord order = float order)
       // this lane's per-row factors, one vector LDS read each (factor 0 at [0, 32), factor 1 at [32, 64))
-      float fac0[DPL], fac1[DPL];
-      if constexpr (MODE == 0 && (COS || SCR || DT == 2)) {
+      float fac0[DPO], fac1[DPO], fac2[DPO];
+      if constexpr (DT == 8) {   // norm, scale, error norm of corpus rows 2 er .. 2 er + 3 (16-byte aligned)
+        const float* tf = trow + tsl * TRS + ero;
+        const f32x4 v0 = *(const f32x4*)tf, v1 = *(const f32x4*)(tf + 64), v2 = *(const f32x4*)(tf + 128);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          fac0[e] = v0[e];
+          fac1[e] = v1[e];
+          fac2[e] = v2[e];
+        }
+      } else if constexpr (MODE == 0 && (COS || SCR || DT == 2)) {
         const float* tf = trow + tsl * 64 + er;
         if constexpr (DPL == 4) {
           const f32x4 v0 = *(const f32x4*)tf;
@@ -1176,12 +1248,12 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           }
         }
       }
-      bool pass[DPL];
-      float sc[DPL], ndv[DPL];
-      int64_t rows[DPL];
+      bool pass[DPO];
+      float sc[DPO], ndv[DPO];
+      int64_t rows[DPO];
       bool anyp = false;
 #pragma unroll
-      for (int e = 0; e < DPL; ++e) {
+      for (int e = 0; e < DPO; ++e) {
         int64_t row;
         bool valid;
         float nd = 1.f;
@@ -1192,9 +1264,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           valid = qev && gvalid[er + e];
           if constexpr (COS) nd = gnorm[er + e];
         } else {
-          row = bse + er + e;
+          row = RPK * bse + ero + e;
           // (the screen keeps lists for padding query slots too: nobody reads them)
-          valid = SCR ? er + e < rem : qev && er + e < rem;
+          valid = SCR ? ero + e < rem : qev && ero + e < rem;
           if constexpr (DT == 2) s = s * (COS ? fac1[e] : fac0[e]) * qs;   // exact 2^e rescales
           if constexpr (COS || SCR) nd = fac0[e];
         }
@@ -1204,8 +1276,19 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         if constexpr (SCR) {
           // upper bound of the exact (DT 3) score, see "Screened search"; the relative bumps cover the
           // roundings of the bound's own arithmetic and of the reciprocal (<= 1 ulp)
-          const float eps = fmaf(a.eps_a * nd, qn, a.eps_b * fmaf(a.sqrt_d, nd, qsa));
-          float v = s + eps;
+          float v;
+          if constexpr (DT == 8) {
+            // int8 screen: s = x8 . (64 p1 + p2) exactly (int32, rounded once to fp32); x . q = sx s scale + q~ . rx
+            // + eq . x with |q~ . rx| <= (|q| + eq) e and |eq . x| <= eq |x|, plus the exact DT 3 score's own error
+            // (eps_a |x||q| + eps_b (sqrt(d) |x| + sum|q|), rr_api.cpp kScreen8EpsA/B); x 1.001 for the roundings of
+            // |q| and of these products, 2^-21 |est| for the three roundings of est
+            const float est = (s * fac1[e]) * q8sc;
+            const float eps = (fmaf(qn + q8eq, fac2[e], q8eq * nd) + fmaf(a.eps_a * nd, qn, a.eps_b * fmaf(a.sqrt_d, nd, qsa))) * 1.001f;
+            v = est + fmaf(fabsf(est), 0x1p-21f, eps);
+          } else {
+            const float eps = fmaf(a.eps_a * nd, qn, a.eps_b * fmaf(a.sqrt_d, nd, qsa));
+            v = s + eps;
+          }
           v += fabsf(v) * 0x1p-22f;
           float u;
           if constexpr (COS) {
@@ -1215,7 +1298,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           } else {
             u = v;
           }
-          if (valid && u >= thr) tk.insert(make_key(u, key_base + (uint32_t)(er + e)));   // (NaN: never)
+          if (valid && u >= thr) tk.insert(make_key(u, key_base + (uint32_t)(ero + e)));   // (NaN: never)
         } else if constexpr (COS) {
           // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
           if (DUMP && a.all_keys) {
@@ -1277,7 +1360,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #ifndef RR_SK_PIPE
 #define RR_SK_PIPE 0   // measured: -2 % on the 64-slot pass (12-16 B of spills), within noise on the screen
 #endif
-  constexpr bool PIPE = MODE == 0 && RR_SK_PIPE && KT <= 16 && !(QH == 2 && DT == 2) && (SCHED == 0 || CT >= 3);   // (else spills)
+  constexpr bool PIPE = MODE == 0 && RR_SK_PIPE && KT <= 16 && !(QH == 2 && DT == 2) && DT != 8 &&
+                        (SCHED == 0 || CT >= 3);   // (else spills)
   int64_t pbase = 0;   // PIPE: the previous tile's first row and factor slot
   int pts = 0;
   // Stagger (streaming passes): waves 4-7 — the SIMD partners of waves 0-3 — run each tile's epilogue one tile
@@ -1294,7 +1378,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #define RR_SK_STAGGER_PAR 0   // A/B only: defer the odd waves instead of waves 4-7
 #endif
   const bool defer = STG && (RR_SK_STAGGER_PAR ? (w & 1) != 0 : w >= 4);
-  float svd[DPL];
+  float svd[DPO];
   int64_t bsd = -1;   // first row of the deferred tile (-1: none)
   int tsd = 0;        // its factor slot (4 slots: wave 0 refills a slot three tiles after its tile at the earliest)
 
@@ -1311,6 +1395,34 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         const int rq = 32 * qh + r;
         *(f32x4*)(rb + (w * QS + rq) * kRedRow + 4 * ((2 * a4 + h) ^ (rq & 7))) = v;
       }
+  };
+  // int8 screen: each wave's two accumulators (pieces p1, p2) combined exactly, 64 a1 + a2 (|.| < 2^29), as int32 bits
+  auto write_partials8 = [&](float* rb, const i32x16 (&ia)[2]) {
+#pragma unroll
+    for (int a4 = 0; a4 < 4; ++a4) {
+      i32x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = ia[0][4 * a4 + i] * 64 + ia[1][4 * a4 + i];
+      *(i32x4*)(rb + (w * QS + r) * kRedRow + 4 * ((2 * a4 + h) ^ (r & 7))) = v;
+    }
+  };
+  // ... and summed exactly in int32 (|sum| < 2^31): waves 0-3 give the kernel rows' first corpus rows, 4-7 the second;
+  // sv = corpus rows 2 er, 2 er + 1, 2 er + 2, 2 er + 3, each rounded once to fp32
+  auto read_partials8 = [&](const float* rb, float (&sv)[DPO]) {
+    typedef int i32x2 __attribute__((ext_vector_type(2)));
+    i32x2 ev = {0, 0}, od = {0, 0};
+#pragma unroll
+    for (int ww = 0; ww < kWaves; ++ww) {
+      const i32x2 p = *(const i32x2*)(rb + (ww * QS + qe) * kRedRow + 4 * ((er >> 2) ^ (qe & 7)) + (er & 3));
+      if (ww < kWaves / 2) ev += p;
+      else od += p;
+    }
+    if constexpr (DPO == 4) {
+      sv[0] = (float)ev[0];
+      sv[1] = (float)od[0];
+      sv[2] = (float)ev[1];
+      sv[3] = (float)od[1];
+    }
   };
   // (two-float vectors: packed adds, each element summed in the same wave order)
   auto read_partials = [&](const float* rb, float (&sv)[DPL]) {
@@ -1354,6 +1466,10 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     for (int qh = 0; qh < QH; ++qh)
 #pragma unroll
       for (int i = 0; i < 16; ++i) accs[qh][i] = 0.f;
+    i32x16 iacc[DT == 8 ? 2 : 1];   // the int8 screen's accumulators (pieces p1, p2)
+    if constexpr (DT == 8)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) iacc[0][i] = iacc[1][i] = 0;
     // LA 2: after slab j's fragments are read, its slot takes slab j + 2 — of this tile, or slab 0 / 1 of the
     // next tile (found at slab NS - 2; wave 0 issues that tile's factors before its slab 0)
     auto issue_ahead = [&](auto jc) {
@@ -1373,7 +1489,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         if (next_base >= 0) {
           if (FX && w == 0) {
             issue_factors(next_base, (ts + 1) & 3);
-            n_is += 1;
+            n_is += FX;
           }
           issue(next_base, 0, slot);
           n_is += 4;
@@ -1410,7 +1526,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           if (next_base >= 0) {
             if (FX && w == 0) {
               issue_factors(next_base, (ts + 1) & 3);
-              extra0 += 1;
+              extra0 += FX;
             }
             issue(next_base, 0, slot ^ 1);
             nw = 4;
@@ -1448,6 +1564,16 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           for (int qh = 0; qh < QH; ++qh) accs[qh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[t], qfs[qh].c0[j][t], accs[qh], 0, 0, 0);
+        }
+      } else if constexpr (DT == 8) {   // int8 screen: 32 K per MFMA, both query pieces
+        i32x4 av[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) av[t] = *(const i32x4*)(sl + slab_off(r, 2 * t + h));
+        if constexpr (MODE == 0 && LA == 2) issue_ahead(jc);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          iacc[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[t], qfs[0].c1[j][t], iacc[0], 0, 0, 0);
+          iacc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[t], qfs[0].c2[j][t], iacc[1], 0, 0, 0);
         }
       } else if constexpr (DT == 2) {
         f16x8 ah[2], al[2];
@@ -1549,11 +1675,13 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         if (tcount > 0) lds_barrier();   // every wave has read the previous tile's partials
       }
       const unsigned long long pt2 = PH_NOW();
-      write_partials(rb, accs);
+      if constexpr (DT == 8) write_partials8(rb, iacc);
+      else write_partials(rb, accs);
       lds_barrier();   // (also publishes wave 0's LDS-DMA factors and its next-chunk word)
       const unsigned long long pt3 = PH_NOW();
-      float sv[DPL];
-      read_partials(rb, sv);
+      float sv[DPO];
+      if constexpr (DT == 8) read_partials8(rb, sv);
+      else read_partials(rb, sv);
 #if defined(RR_SK_DIAG) && (RR_SK_DIAG & 4)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       for (int e = 0; e < DPL; ++e) asm volatile("" : "+v"(sv[e]));
@@ -1561,7 +1689,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       const unsigned long long pt4 = PH_NOW();
       if (defer) {
 #pragma unroll
-        for (int e = 0; e < DPL; ++e) svd[e] = sv[e];
+        for (int e = 0; e < DPO; ++e) svd[e] = sv[e];
         bsd = base;
         tsd = ts;
       } else {
@@ -1727,9 +1855,12 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       // Not proven: the wide phase can still prove it when the k-th largest bound of all lies above the largest
       // bound of any single list (vtail): every key left out of every list is below that.
       const uint64_t tb = *vtail;
+      const uint32_t rbar = wide_bar(ek, tb);
       const bool wide = !complete && a.wide_verify && !a.force_incomplete && qinfo[QS + vq] < 32768.0f &&
-                        (uint32_t)(akeys[a.k_out - 1] >> 32) > (uint32_t)(tb >> 32);
+                        ((uint32_t)(ek >> 32) > (uint32_t)(tb >> 32) ||
+                         (uint32_t)(akeys[a.k_out - 1] >> 32) > (uint32_t)(tb >> 32));
       vstate[0] = wide ? 1 : 0;
+      vstate[4] = (int)rbar;
       VDIAG(0, akeys[a.k_out - 1]);
       VDIAG(1, tb);
       VDIAG(2, ek);
@@ -1742,17 +1873,19 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     __syncthreads();
     if (vstate[0] != 1) return;
 
-    // ---- wide phase: R = every list entry whose bound is above vtail (the rest: exact <= bound <= vtail), rescored
-    // with exactly the arithmetic of the first tile (same K split, MFMA order, wave order, epilogue), 32 rows a
-    // tile; complete when the exact k-th key is above vtail. Lists are disjoint (each workgroup its own rows).
+    // ---- wide phase: R = every list entry whose bound reaches R's bar (wide_bar; every key left out of the lists is
+    // at most vtail, below the bar), rescored with exactly the arithmetic of the first tile (same K split, MFMA order,
+    // wave order, epilogue), 32 rows a tile; complete when the exact k-th key is above vtail. Lists are disjoint (each
+    // workgroup its own rows).
     int* wl = (int*)(smem + kWideListOff);
     const uint32_t tb_ord = (uint32_t)(*vtail >> 32);
+    const uint32_t rbar = (uint32_t)vstate[4];
     if (tid == 0) vstate[1] = 0;
     __syncthreads();
     for (int l = tid; l < a.nlists; l += kThreads) {
       const uint64_t* src = a.vin + ((size_t)vq * a.nlists + l) * (KT + 1);
       int c = 0;
-      while (c < KT && (uint32_t)(src[c] >> 32) > tb_ord) ++c;   // a prefix of the sorted list
+      while (c < KT && (uint32_t)(src[c] >> 32) >= rbar) ++c;   // a prefix of the sorted list
       if (c) {
         const int pos = atomicAdd(&vstate[1], c);
         for (int i = 0; i < c; ++i)
@@ -1896,9 +2029,9 @@ hipError_t launch_ns(int ns, int kt, int grid, const SkArgs& a, hipStream_t s) {
   switch (ns) {
     case 1: return launch_kt<DT, 1, COS, RS, QH, MODE, SCHED, FL>(kt, grid, a, s);
     case 2: return launch_kt<DT, 2, COS, RS, QH, MODE, SCHED, FL>(kt, grid, a, s);
-    case 3: if constexpr (DT != 1 && DT != 7) return launch_kt<DT, 3, COS, RS, QH, MODE, SCHED, FL>(kt, grid, a, s);
+    case 3: if constexpr (DT != 1 && DT != 7 && DT != 8) return launch_kt<DT, 3, COS, RS, QH, MODE, SCHED, FL>(kt, grid, a, s);
             else return hipErrorInvalidValue;
-    case 4: if constexpr (DT != 1 && DT != 7) return launch_kt<DT, 4, COS, RS, QH, MODE, SCHED, FL>(kt, grid, a, s);
+    case 4: if constexpr (DT != 1 && DT != 7 && DT != 8) return launch_kt<DT, 4, COS, RS, QH, MODE, SCHED, FL>(kt, grid, a, s);
             else return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
@@ -1913,17 +2046,19 @@ hipError_t launch_metric(int metric, int ns, int kt, int grid, const SkArgs& a, 
 }  // namespace sk
 
 size_t sk_lds_bytes(int sdt, bool cos, int ring, int qslots) {
-  (void)sdt;
   (void)cos;
-  // + per-row factors [4][2][32], next-chunk words [4], query scalars [3][qslots], MODE 1 scratch: W [8][32] +
-  // akeys [32] keys, grow / gnorm / gvalid [32], xk [32] keys, the floors' and the list bounds' maxima, 2 ints
-  const size_t verify = (size_t)(kWaves * 32 + 32 + 32 + 3) * 8 + 3 * 32 * 4;
-  return sk::ring_bytes(ring) + sk::red_bytes(ring, qslots / 32) + 4 * 64 * 4 + 4 * 4 + 3 * qslots * 4 + verify;
+  // + per-row factors [4][64] (the int8 screen: [4][192]), next-chunk words [4], query scalars [3][qslots], MODE 1
+  // scratch: W [8][32] + akeys [32] keys, grow / gnorm / gvalid [32], xk [32] keys, the floors' and the list bounds'
+  // maxima, 6 ints
+  const size_t verify = (size_t)(kWaves * 32 + 32 + 32 + 5) * 8 + 3 * 32 * 4;
+  const size_t factors = (size_t)4 * (sdt == KDT_SCREEN8 ? 192 : 64) * 4;
+  return sk::ring_bytes(ring) + sk::red_bytes(ring, qslots / 32) + factors + 4 * 4 + 3 * qslots * 4 + verify;
 }
 
 bool sk_supports_64(int sdt) { return sdt == KDT_BF16 || sdt == KDT_F32_SPLIT; }
 int sk_slabs(int sdt, int d) {
-  const int eb = sdt == KDT_BF16 || sdt == KDT_SCREEN16 ? 2 : 4;
+  // (the int8 screen: kernel rows of two corpus rows, 2 d bytes)
+  const int eb = sdt == KDT_BF16 || sdt == KDT_SCREEN16 || sdt == KDT_SCREEN8 ? 2 : 4;
   const int ks = d * eb / kWaves;   // row bytes per wave
   if (d <= 0 || ks % sk::kSlabRowBytes != 0) return 0;
   const int ns = ks / sk::kSlabRowBytes;
@@ -1949,6 +2084,17 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
                  : sk::launch_metric<6, 2, 1, 0, 0, 1>(metric, ns, kt, grid, a, s);
     return dyn ? sk::launch_metric<6, 2, 1, 0, 1>(metric, ns, kt, grid, a, s)
                : sk::launch_metric<6, 2, 1>(metric, ns, kt, grid, a, s);
+  }
+  if (sdt == KDT_SCREEN8) {   // the screen over the int8 copy (a.corpus = that copy, a.n = ceil(a.rows8 / 2))
+    const int ns8 = sk_slabs(KDT_SCREEN8, a.d);
+    if (qslots != 32 || ring != 2 || !ns8 || !a.q8 || !a.q8s || !a.sx8 || !a.e8 || a.n != (a.rows8 + 1) / 2)
+      return hipErrorInvalidValue;
+    const bool dyn = a.dyn && a.ctr && kt <= 16;
+    if (a.full_lists)
+      return dyn ? sk::launch_metric<8, 2, 1, 0, 1, 1>(metric, ns8, kt, grid, a, s)
+                 : sk::launch_metric<8, 2, 1, 0, 0, 1>(metric, ns8, kt, grid, a, s);
+    return dyn ? sk::launch_metric<8, 2, 1, 0, 1>(metric, ns8, kt, grid, a, s)
+               : sk::launch_metric<8, 2, 1>(metric, ns8, kt, grid, a, s);
   }
   if (sdt == KDT_SCREEN16) {   // the screen over the f16 copy (a.corpus = that copy)
     const int ns16 = sk_slabs(KDT_SCREEN16, a.d);

@@ -42,7 +42,7 @@ RR_KERNEL_AUTO = 0
 RR_KERNEL_FUSED = 1
 RR_KERNEL_EXACT = 2
 RR_KERNEL_SCREEN_FALLBACK = 3
-RR_ABI_VERSION = 6
+RR_ABI_VERSION = 7
 
 DTYPES = {"fp32": RR_DTYPE_F32, "float32": RR_DTYPE_F32, "f32": RR_DTYPE_F32,
           "bf16": RR_DTYPE_BF16, "bfloat16": RR_DTYPE_BF16, "fp32-split": RR_DTYPE_F32_SPLIT}
@@ -78,6 +78,7 @@ SIGNATURES = {
     "rr_screen_stats": (_c_int, [_vp, _i64p, _i64p]),
     "rr_set_schedule": (_c_int, [_vp, _c_int]),
     "rr_screen_copy": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_i32)]),
+    "rr_screen_int8": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_i32)]),
     "rr_set_compute_streams": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_i32)]),
     "rr_last_shape": (_c_int, [_vp, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32)]),
     "rr_dist_info": (_c_int, [_vp, _ip, _ip]),
@@ -336,6 +337,14 @@ class Index:
         use=True keeps one from the next load, False frees it; returns whether it is in use."""
         p = _c_i32()
         _check(self._lib.rr_screen_copy(self._h, -1 if use is None else int(bool(use)), ctypes.byref(p)))
+        return bool(p.value)
+
+    def screen_int8(self, use: Optional[bool] = None) -> bool:
+        """The screened search's int8 copy (a quarter of the fp32 bytes per screen pass, a looser bound; results
+        unchanged): use=True screens it (re-armed), False screens the f16 copy; returns whether the next search
+        screens the int8 copy."""
+        p = _c_i32()
+        _check(self._lib.rr_screen_int8(self._h, -1 if use is None else int(bool(use)), ctypes.byref(p)))
         return bool(p.value)
 
     def screen_stats(self) -> Tuple[int, int]:

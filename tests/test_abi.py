@@ -15,7 +15,7 @@ HEADER = _lib.HEADER_PATH
 def header_functions():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(rr_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(rr_[a-z0-9_]+)\s*\(", text)))
 
 
 def header_defines():
@@ -42,7 +42,7 @@ def test_library_exports_every_header_symbol(lib):
 
 def test_exported_dynamic_symbols_match(lib):
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
-    exported = set(re.findall(r"\bT (rr_[a-z_]+)\b", out))
+    exported = set(re.findall(r"\bT (rr_[a-z0-9_]+)\b", out))
     assert exported == set(header_functions())
 
 

@@ -1,0 +1,119 @@
+"""The int8 screen (rr_sk.hip DT 8, fp32 storage with d a multiple of 512 up to 1024): the screened search's upper
+bounds from an int8 copy of the rows (per-row scale and error norm) against two int8 pieces of each query. Its bound
+is looser than the f16 copy's, so more rows reach the verify (its wide phase takes every list entry whose bound
+reaches the exact k-th score); results must stay BIT-IDENTICAL to the one-pass exact kernel, including on rows the
+int8 copy represents badly (one large element: the rest rounds to zero and only the error norm bounds the score)."""
+import numpy as np
+import pytest
+
+from oracle import synth
+from oracle.retriever_oracle import canonical_topk, exact_scores
+from parity_helpers import check_topk
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def Index(hip):
+    from rag_service_amd import Index as _Index
+    return _Index
+
+
+def _spiky_corpus(rng, n, d, q):
+    """Random rows of mixed norms, a zero row, and 64 rows built to be the queries' best matches while the int8 copy
+    loses them: a large spike in one element sets the row's scale, so the part aligned with the query rounds to 0."""
+    corpus = rng.standard_normal((n, d)).astype(np.float32) * rng.uniform(0.25, 4, size=(n, 1)).astype(np.float32)
+    corpus[n // 3] = 0.0
+    rows = rng.choice(n, size=min(64, n // 2), replace=False)
+    for j, r in enumerate(rows):
+        v = q[j % len(q)] / np.linalg.norm(q[j % len(q)]) * 0.9 + 0.05 * rng.standard_normal(d).astype(np.float32)
+        v[rng.integers(d)] = 60.0 * rng.choice([-1.0, 1.0])   # 60 >> the rest: sx ~ 0.47, every other element -> 0
+        corpus[r] = v.astype(np.float32)
+    return corpus
+
+
+@pytest.mark.parametrize("n,d,b,k", [(4099, 1024, 32, 5), (70001, 1024, 32, 10), (65536, 512, 20, 1),
+                                     (12345, 1024, 7, 16), (33, 1024, 32, 3)])
+@pytest.mark.parametrize("metric", ["cosine", "dot"])
+def test_int8_screen_equals_exact(Index, n, d, b, k, metric):
+    rng = np.random.default_rng(n + d + k)
+    q = rng.standard_normal((b, d)).astype(np.float32)
+    corpus = _spiky_corpus(rng, n, d, q)
+    ix = Index(dtype="fp32", metric=metric)
+    ix.load(corpus)
+    assert ix.screen_int8()
+    got = ix.search(q, k)
+    blocks, flagged, reruns, _ = ix.screen_counts_all()
+    assert blocks == 1 and reruns == flagged
+    ix.set_kernel("exact")
+    want = ix.search(q, k)
+    assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
+    ix.set_kernel("auto")
+    ix.screen_int8(False)
+    assert not ix.screen_int8()
+    f16 = ix.search(q, k)
+    assert np.array_equal(f16[1], want[1]) and np.array_equal(f16[0], want[0])
+    _, cidx = canonical_topk(exact_scores(corpus, q, metric), k)
+    tol = 1e-3 * (np.sqrt(d) * 4 if metric == "dot" else 1.0)
+    check_topk(got[1], got[0], cidx, corpus, q, metric, near_tie=1e-5 * np.sqrt(d) * 16, score_tol=tol)
+    ix.close()
+
+
+def test_int8_screen_proves_unit_norm_blocks_in_the_wide_phase(Index):
+    """The headline's data: with 16-entry lists the int8 bound leaves more than KT - k candidates above the exact
+    k-th score for many queries; the wide phase (entries whose bound reaches the exact k-th) proves them all — no
+    block re-runs — and the results equal the exact kernel's."""
+    corpus = synth.unit_norm_gaussian(1234, 262144, 1024)
+    q = synth.unit_norm_gaussian(5678, 128, 1024)
+    ix = Index(dtype="fp32", metric="cosine")
+    ix.load(corpus)
+    assert ix.screen_int8()
+    got = ix.search(q, 5)
+    blocks, flagged, reruns, wide = ix.screen_counts_all()
+    assert (blocks, flagged, reruns) == (4, 0, 0)
+    assert wide > 0   # (the f16 bound needs the wide phase for almost none)
+    ix.set_kernel("exact")
+    want = ix.search(q, 5)
+    assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
+    ix.close()
+
+
+def test_int8_screen_gives_way_to_the_f16_copy(Index):
+    """Adaptive: a window of settled blocks that re-ran (forced here) switches the handle to the f16 copy before
+    the per-lane lists grow; results stay exact throughout; a reload re-arms the int8 screen."""
+    rng = np.random.default_rng(3)
+    corpus = rng.standard_normal((20000, 1024)).astype(np.float32)
+    q = rng.standard_normal((32, 1024)).astype(np.float32)
+    ix = Index(dtype="fp32", metric="cosine")
+    ix.load(corpus)
+    ix.set_kernel("exact")
+    want = ix.search(q, 5)
+    ix.set_kernel("screen-fallback")
+    assert ix.screen_int8()
+    for _ in range(32):
+        got = ix.search(q, 5)
+        assert np.array_equal(got[1], want[1])
+    assert not ix.screen_int8()
+    assert ix.screen_state()[0] is False   # the f16 copy comes first; its lists are still short
+    ix.set_kernel("auto")
+    got = ix.search(q, 5)
+    assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
+    ix.load(corpus)
+    assert ix.screen_int8()
+    ix.close()
+
+
+def test_int8_screen_sharded_and_odd_rows(Index):
+    """Shards of odd row counts (the int8 copy's padding row) in one process, exchange path: identical to exact."""
+    rng = np.random.default_rng(11)
+    n, d = 30001, 1024
+    q = rng.standard_normal((32, d)).astype(np.float32)
+    corpus = _spiky_corpus(rng, n, d, q)
+    ix = Index(dtype="fp32", metric="cosine", devices=[0, 0, 0])
+    ix.load(corpus)
+    assert ix.screen_int8()
+    got = ix.search(q, 8)
+    ix.set_kernel("exact")
+    want = ix.search(q, 8)
+    assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
+    ix.close()
