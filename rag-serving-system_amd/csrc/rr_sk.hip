@@ -1280,7 +1280,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           if constexpr (DT == 8) {
             // int8 screen: s = x8 . (64 p1 + p2) exactly (int32, rounded once to fp32); x . q = sx s scale + q~ . rx
             // + eq . x with |q~ . rx| <= (|q| + eq) e and |eq . x| <= eq |x|, plus the exact DT 3 score's own error
-            // (eps_a |x||q| + eps_b (sqrt(d) |x| + sum|q|), rr_api.cpp kScreen8EpsA/B); x 1.001 for the roundings of
+            // (eps_a |x||q| + eps_b (sqrt(d) |x| + sum|q|), rr_api.cpp kScreen8EpsA/B; eps_b sum|q| also covers
+            // residuals whose squares underflow fp32 in e, |r| < 2^-63); x 1.001 for the roundings of
             // |q| and of these products, 2^-21 |est| for the three roundings of est
             const float est = (s * fac1[e]) * q8sc;
             const float eps = (fmaf(qn + q8eq, fac2[e], q8eq * nd) + fmaf(a.eps_a * nd, qn, a.eps_b * fmaf(a.sqrt_d, nd, qsa))) * 1.001f;
@@ -1372,7 +1373,11 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #ifndef RR_SK_STAGGER
 #define RR_SK_STAGGER 2   // 0 off, 1 the 64-slot pass only, 2 every streaming pass
 #endif
-  constexpr bool STG = MODE == 0 && !PIPE && !(QH == 2 && DT == 2) && DT != 6 && KT <= 16 &&   // (measured)
+#ifndef RR_SK_STAGGER8
+#define RR_SK_STAGGER8 1   // the int8 screen too (its 9-wave form then spills 6 VGPRs; 0: no stagger, no spills)
+#endif
+  constexpr bool STG = MODE == 0 && !PIPE && !(QH == 2 && DT == 2) && DT != 6 && (DT != 8 || RR_SK_STAGGER8) &&
+                       KT <= 16 &&   // (measured)
                        (RR_SK_STAGGER == 2 || (RR_SK_STAGGER == 1 && QH == 2));
 #ifndef RR_SK_STAGGER_PAR
 #define RR_SK_STAGGER_PAR 0   // A/B only: defer the odd waves instead of waves 4-7

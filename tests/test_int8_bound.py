@@ -1,0 +1,93 @@
+"""CPU restatement of the int8 screen's bound (rr_kernels.hip f32_to_i8_kernel / q8_prep_kernel, rr_sk.hip DT 8
+epilogue) in float32 numpy, checked against float64 dot products: the bound must hold for every row, including rows
+the int8 copy represents badly (a spike sets the scale and every other element rounds to zero), zero rows, tiny and
+huge magnitudes. This pins the ALGEBRA of the bound (Cauchy-Schwarz on the two residuals); the GPU tests
+(test_gpu_int8.py) pin the kernels against the exact kernel."""
+import numpy as np
+import pytest
+
+F = np.float32
+
+
+def quantize_rows(x):
+    m = np.abs(x).max(axis=1)
+    s = np.where(m > 0, m / F(127), F(0)).astype(F)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        q = np.where(s[:, None] > 0, np.clip(np.rint(x / s[:, None]), -127, 127), 0).astype(F)
+    r = (x - s[:, None] * q).astype(F)
+    e = (np.sqrt((r * r).sum(axis=1, dtype=F)) * F(1 + 2 ** -12) + m * F(np.sqrt(x.shape[1])) * F(2 ** -22)).astype(F)
+    return q.astype(np.int8), s, e
+
+
+def quantize_query(v):
+    m = F(np.abs(v).max())
+    s = F(m / F(127)) if m > 0 else F(0)
+    if s > 0:
+        t = (v / s).astype(F)
+        a = np.clip(np.rint(t), -127, 127).astype(F)
+        c = np.clip(np.rint((t - a) * F(64)), -127, 127).astype(F)
+    else:
+        a = c = np.zeros_like(v)
+    r = (v - s * (a * F(64) + c) * F(2 ** -6)).astype(F)
+    eq = F(np.sqrt((r * r).sum(dtype=F)) * F(1 + 2 ** -12) + m * F(np.sqrt(v.size)) * F(2 ** -21))
+    qn = F(np.sqrt((v * v).sum(dtype=F)))
+    qsa = F(np.abs(v).sum(dtype=F) * F(1 + 2 ** -18))
+    return a.astype(np.int8), c.astype(np.int8), F(s * F(2 ** -6)), eq, qn, qsa
+
+
+def bound(xq, sx, e, nd, p1, p2, qsc, eq, qn, qsa, eps_a=6e-5, eps_b=4e-8):
+    """(the eps_b term also covers squared residuals that underflow fp32: |r| < 2^-63 leaves e short by at most
+    2^-63 sqrt(d) |q|, far below eps_b sum|q|)"""
+    acc = xq.astype(np.int64) @ (64 * p1.astype(np.int64) + p2.astype(np.int64))   # exact, as the int32 MFMA sums
+    s = acc.astype(F)
+    est = (s * sx).astype(F) * qsc
+    sqrt_d = F(np.sqrt(xq.shape[1]) * (1 + 2 ** -20))
+    eps = ((qn + eq) * e + eq * nd + (F(eps_a) * nd * qn + F(eps_b) * (sqrt_d * nd + qsa))) * F(1.001)
+    v = est + np.abs(est) * F(2 ** -21) + eps
+    return v + np.abs(v) * F(2 ** -22)
+
+
+@pytest.mark.parametrize("kind", ["gauss", "spiky", "scaled", "tiny", "small", "huge", "zero_rows", "sparse"])
+def test_int8_bound_holds(kind):
+    rng = np.random.default_rng(sum(map(ord, kind)))
+    n, d = 3000, 1024
+    x = rng.standard_normal((n, d)).astype(F)
+    if kind == "spiky":
+        x *= F(0.05)
+        x[np.arange(n), rng.integers(0, d, n)] = F(60.0)
+    elif kind == "scaled":
+        x *= rng.uniform(1e-3, 1e3, size=(n, 1)).astype(F)
+    elif kind == "tiny":
+        x *= F(1e-30)
+    elif kind == "small":   # squared residuals below fp32's range (e reads 0), queries of normal size
+        x *= F(1e-20)
+    elif kind == "huge":
+        x *= F(1e4)
+    elif kind == "zero_rows":
+        x[::3] = 0
+    elif kind == "sparse":
+        x[rng.random((n, d)) < 0.97] = 0
+    xq, sx, e = quantize_rows(x)
+    nd = np.sqrt((x.astype(np.float64) ** 2).sum(axis=1)).astype(F)
+    for j in range(8):
+        v = rng.standard_normal(d).astype(F)
+        if j % 2:   # queries aligned with some rows (their true matches)
+            v = (x[rng.integers(n)] + F(0.1) * np.abs(x).max() * rng.standard_normal(d).astype(F)).astype(F)
+        u = bound(xq, sx, e, nd, *quantize_query(v))
+        exact = x.astype(np.float64) @ v.astype(np.float64)
+        assert np.all(u.astype(np.float64) >= exact), float(np.max(exact - u))
+
+
+def test_int8_bound_is_about_a_quarter_sigma_on_unit_norm_rows():
+    """The headline data: the slack (bound - exact) is ~0.008 on unit-norm d = 1024 rows — the number DESIGN §3.2
+    quotes (a quarter of the score distribution's sigma, 1/32)."""
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((4000, 1024)).astype(F)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    v = rng.standard_normal(1024).astype(F)
+    v /= np.linalg.norm(v)
+    xq, sx, e = quantize_rows(x)
+    u = bound(xq, sx, e, np.ones(len(x), F), *quantize_query(v))
+    slack = u.astype(np.float64) - x.astype(np.float64) @ v.astype(np.float64)
+    assert slack.min() >= 0
+    assert 0.006 < np.median(slack) < 0.010
