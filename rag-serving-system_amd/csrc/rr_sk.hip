@@ -1374,7 +1374,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #define RR_SK_STAGGER 2   // 0 off, 1 the 64-slot pass only, 2 every streaming pass
 #endif
 #ifndef RR_SK_STAGGER8
-#define RR_SK_STAGGER8 1   // the int8 screen too (its 9-wave form then spills 6 VGPRs; 0: no stagger, no spills)
+#define RR_SK_STAGGER8 0   // 1: the int8 screen too — its 9-wave form then spills 6 VGPRs and measured 4-8 % slower
+                           // (profiles/r04/ab/ab_i8_stagger.txt)
 #endif
   constexpr bool STG = MODE == 0 && !PIPE && !(QH == 2 && DT == 2) && DT != 6 && (DT != 8 || RR_SK_STAGGER8) &&
                        KT <= 16 &&   // (measured)

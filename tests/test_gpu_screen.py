@@ -69,8 +69,9 @@ def test_screen_rarely_falls_back_on_unit_norm_data(Index):
     ix.close()
 
 
+@pytest.mark.parametrize("i8", [True, False])
 @pytest.mark.parametrize("wide", [True, False])
-def test_screen_ties_take_the_exact_pass(Index, monkeypatch, wide):
+def test_screen_ties_take_the_exact_pass(Index, monkeypatch, wide, i8):
     """40 copies of one row spread over the corpus, queried with that row: 40 exactly tied top scores, more
     than the screen's global candidate list holds. The verify's wide phase rescores every list entry above the
     largest single-list bound (the copies lie in many workgroups' lists) and proves the top-k; without it
@@ -86,9 +87,13 @@ def test_screen_ties_take_the_exact_pass(Index, monkeypatch, wide):
         ix = Index(dtype="fp32", metric=metric)
         monkeypatch.delenv("RR_WIDE_VERIFY")
         ix.load(corpus)
+        assert ix.screen_int8() and ix.screen_int8(i8) == i8
         got = ix.search(q, 5)
         blocks, flagged, reruns, wide_slots = ix.screen_counts_all()
-        assert (blocks, flagged, reruns, wide_slots) == ((1, 0, 0, 1) if wide else (1, 1, 1, 0))
+        if i8:   # (the int8 bound also sends other query slots through the wide phase)
+            assert (blocks, flagged, reruns) == ((1, 0, 0) if wide else (1, 1, 1)) and (wide_slots >= 1) == wide
+        else:
+            assert (blocks, flagged, reruns, wide_slots) == ((1, 0, 0, 1) if wide else (1, 1, 1, 0))
         assert sorted(got[1][0]) == sorted(np.sort(np.append(dup, 123))[:5])
         ix.set_kernel("exact")
         want = ix.search(q, 5)
