@@ -294,11 +294,11 @@ def _plain_and_dist(Index, corpus):
 @pytest.mark.parametrize("layout", ["interleaved", "contiguous"])
 def test_screen_adapts_to_clustered_corpora(Index, layout):
     """The adaptive screen (rr_api.cpp observe_settled) on 1000 noisy copies of each of 100 SQuAD rows (sigma 0.01):
-    interleaved, every cluster's copies fall on a few lanes of each workgroup (a stride of 100 rows), overflow the
-    short per-lane lists and their floors stop every proof — after one window of 32 re-run blocks the handle
-    switches to full lists, and from then on the wide phase proves every block (no flags). Contiguous, a cluster
-    fills a few workgroups' lists even then: after a second window the handle pauses screening (the exact kernel
-    alone) for 1024 blocks. Decided from settled searches only, so a handle in multi-process mode (1-rank RCCL
+    interleaved, every cluster's copies fall on a few lanes of each workgroup (a stride of 100 rows) and the wide
+    phase, barred at the exact k-th score, proves every block with the short lists and the int8 copy (no flags, no
+    switch). Contiguous, a cluster fills a few workgroups' lists: after a window of re-run blocks the handle gives
+    the int8 copy up for the f16 one, after the next grows the per-lane lists, and after the next pauses screening
+    (the exact kernel alone) for 1024 blocks. Decided from settled searches only, so a handle in multi-process mode (1-rank RCCL
     communicator) switches at exactly the same searches as a plain one. Results bit-identical to the exact kernel
     at every step."""
     corpus, q = _clustered(100000, 0.01, layout, clusters=100)
@@ -314,20 +314,24 @@ def test_screen_adapts_to_clustered_corpora(Index, layout):
         for step in range(140):
             got = ix.search(q, 5)
             assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), step
-            hist.append(ix.screen_counts_all() + ix.screen_state())
+            hist.append(ix.screen_counts_all() + ix.screen_state() + (ix.screen_int8(),))
         hists.append(hist)
         ix.close()
     hist, hist_dist = hists
     assert [h[4:] for h in hist] == [h[4:] for h in hist_dist]          # the same switch points, step by step
     assert [h[:3] for h in hist] == [h[:3] for h in hist_dist]          # the same blocks, flags and re-runs
-    blocks, flagged, reruns, wide_slots, full, pause_left, pauses = hist[-1]
+    blocks, flagged, reruns, wide_slots, full, pause_left, pauses, i8 = hist[-1]
     print(layout, hist[40], hist[-1])
-    full_at = next(i for i, h in enumerate(hist) if h[4])
-    assert full_at % 32 == 31                                           # decided at the end of a 32-block window
     if layout == "interleaved":
-        assert pauses == 0 and blocks == 140
-        assert hist[-1][1] == hist[full_at][1] and wide_slots >= 32 * 50    # no flags once the lists are full
+        # r4: the wide phase bars at the exact k-th score once that clears the lists' tail, so the short lists prove
+        # every block of the interleaved clusters (r3 needed a window of re-runs and the full lists first)
+        assert flagged == 0 and pauses == 0 and not full and blocks == 140 and wide_slots >= 32 * 100
+        assert all(h[7] for h in hist)                                  # the int8 copy screens throughout
     else:
+        # the int8 copy gives way first, then the short lists, then screening pauses — each at a window's end
+        i8_off = next(i for i, h in enumerate(hist) if not h[7])
+        full_at = next(i for i, h in enumerate(hist) if h[4])
+        assert i8_off % 32 == 31 and full_at % 32 == 31 and i8_off < full_at
         pause_at = next(i for i, h in enumerate(hist) if h[6])
         assert pause_at % 32 == 31 and pauses == 1 and blocks == pause_at + 1   # then the exact kernel alone
         assert pause_left == 1024 - (139 - pause_at)
