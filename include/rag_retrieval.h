@@ -227,7 +227,8 @@ int rr_screen_copy(rr_handle* h, int32_t use, int32_t* present);
  * pieces of each query (v_mfma_i32_32x32x32_i8). Its upper bound (exact integer sums + the error norms, Cauchy-
  * Schwarz) is ~8x looser than the f16 copy's, so more rows reach the verify; results are bit-identical either way.
  * Adaptive: when more than 1 in 32 settled blocks of a window re-run, the handle screens the f16 copy instead (reset
- * at every load). Made at load time when it fits (default; RR_SCREEN_I8=0 at creation: not made). use = 1: screen it
+ * at every load). Made at load time for shards of at least 65536 rows when it fits (default; RR_SCREEN_I8=0 at
+ * creation: not made; RR_SCREEN_I8_MIN_ROWS: another row minimum). use = 1: screen it
  * (re-armed; from the next load if none was made), 0: screen the f16 copy, -1: leave as is. *active (may be null):
  * the next search screens the int8 copy on every local shard. */
 int rr_screen_int8(rr_handle* h, int32_t use, int32_t* active);

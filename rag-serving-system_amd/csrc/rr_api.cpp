@@ -78,12 +78,10 @@ struct Shard {
   void* corpus = nullptr;                // [rows][d] fp32 or bf16
   uint16_t* scr16 = nullptr;             // fp32 storage: f16 copy of the rows for the screened search (or null)
   // fp32 storage: the int8 screen's copy (rr_sk.hip DT 8; or null): [round_up(rows, 2)][d] int8 rows (a padding row
-  // of zeros), per row its scale and error norm ([rows]); per compute stream the queries' int8 pieces and scalars
+  // of zeros), per row its scale and error norm ([round_up(rows, 2)])
   int8_t* scr8 = nullptr;
   float* sx8 = nullptr;
   float* e8 = nullptr;
-  int8_t* q8[2] = {nullptr, nullptr};
-  float* q8s[2] = {nullptr, nullptr};
   float* norms = nullptr;                // [round_up(rows, 32) + 32] |row| (pad = 1)
   float* rscale = nullptr;               // [same] split-f16 row scale 2^-e (pad = 1)
   float* qbuf[2] = {nullptr, nullptr};   // staged queries, double-buffered ([q_cap][d] fp32 each): a new
@@ -229,6 +227,9 @@ struct rr_handle {
   int x_delay_us = 0;           // A/B: RR_X_EXCHANGE_DELAY_US, a stand-in for a slower exchange
   int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy)
   int screen_i8 = 1;            // ... and an int8 copy, screened first (rr_screen_int8; RR_SCREEN_I8=0 at creation: off)
+  int64_t i8_min_rows = 65536;  // ... for shards of at least this many rows (RR_SCREEN_I8_MIN_ROWS): below, a search is
+                                // launch-bound and lists holding a large share of the shard's rows leave the looser
+                                // bound little to prove with (a 1000-row corpus of real embeddings re-ran blocks)
   bool i8_off = false;          // adaptive: the int8 screen re-ran too often on this corpus, the f16 copy screens
   bool last_i8 = false;         // the last search screened the int8 copy
   int64_t narrow_settled = 0;   // settled screened blocks run with 16-entry lists where 2k + 2 wanted 32 (screen_kt)
@@ -380,7 +381,7 @@ int dmalloc(T** p, size_t bytes) {
 
 int free_shard(Shard& s) {
   hipSetDevice(s.dev);
-  void* ptrs[] = {s.corpus, s.scr16, s.scr8, s.sx8, s.e8, s.q8[0], s.q8[1], s.q8s[0], s.q8s[1], s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.wcount, s.ctr, s.shard_keys, s.gathered, s.out_base,
+  void* ptrs[] = {s.corpus, s.scr16, s.scr8, s.sx8, s.e8, s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.wcount, s.ctr, s.shard_keys, s.gathered, s.out_base,
                   s.full_keys, s.sort_temp, s.wcand, s.wfloor, s.wsel};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -409,15 +410,12 @@ int free_shard(Shard& s) {
   return RR_OK;
 }
 
-// Release the shard's int8 screen copy and its query buffers (current device = s.dev).
+// Release the shard's int8 screen copy (current device = s.dev).
 void free_i8(Shard& s) {
-  for (void* p : {(void*)s.scr8, (void*)s.sx8, (void*)s.e8, (void*)s.q8[0], (void*)s.q8[1], (void*)s.q8s[0],
-                  (void*)s.q8s[1]})
+  for (void* p : {(void*)s.scr8, (void*)s.sx8, (void*)s.e8})
     if (p) hipFree(p);
   s.scr8 = nullptr;
   s.sx8 = s.e8 = nullptr;
-  s.q8[0] = s.q8[1] = nullptr;
-  s.q8s[0] = s.q8s[1] = nullptr;
 }
 
 // Allocate the shard's corpus storage for the current range (and norms when cosine).
@@ -440,17 +438,14 @@ int alloc_corpus(rr_handle* h, Shard& s) {
     }
   }
   // the int8 copy (a quarter of the fp32 bytes; d a multiple of 512 up to 1024), next to the f16 one it falls back to
-  if (s.scr16 && h->screen_i8 && rr::sk_slabs(rr::KDT_SCREEN8, h->d) && hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+  if (s.scr16 && h->screen_i8 && rows >= h->i8_min_rows && rr::sk_slabs(rr::KDT_SCREEN8, h->d) &&
+      hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
     const int64_t r2 = (rows + 1) / 2 * 2;
     const size_t need8 = (size_t)r2 * h->d + 2 * (size_t)r2 * 4;
     if (free_b > need8 + (4ull << 30)) {
       bool ok = hipMalloc((void**)&s.scr8, (size_t)r2 * h->d) == hipSuccess;
       ok = ok && hipMalloc((void**)&s.sx8, (size_t)r2 * 4) == hipSuccess;
       ok = ok && hipMalloc((void**)&s.e8, (size_t)r2 * 4) == hipSuccess;
-      for (int i = 0; i < 2 && ok; ++i) {
-        ok = hipMalloc((void**)&s.q8[i], (size_t)2 * rr::kQSlots * h->d) == hipSuccess;
-        ok = ok && hipMalloc((void**)&s.q8s[i], (size_t)4 * rr::kQSlots * 4) == hipSuccess;
-      }
       // the padding row (odd row counts) is read as the second half of the last kernel row: zeros, scale 0
       if (ok && r2 > rows) {
         ok = hipMemset(s.scr8 + (size_t)rows * h->d, 0, h->d) == hipSuccess;
@@ -1204,13 +1199,10 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         a.eps_a = s16 ? kScreen16EpsA : kScreenEpsA;
         a.eps_b = s16 ? kScreen16EpsB : kScreenEpsB;
         if (s16) a.corpus = (const char*)s.scr16;
-        if (s8) {   // the queries' int8 pieces on this stream first (the previous block's screen here is done with them)
-          HIP_TRY(rr::launch_q8_prep(qb, bb, d, s.q8[bsi], s.q8s[bsi], cs));
+        if (s8) {   // (the kernel quantises the block's queries itself)
           a.corpus = (const char*)s.scr8;
           a.n = (s.rows() + 1) / 2;
           a.rows8 = s.rows();
-          a.q8 = s.q8[bsi];
-          a.q8s = s.q8s[bsi];
           a.sx8 = s.sx8;
           a.e8 = s.e8;
           a.eps_a = kScreen8EpsA;
@@ -1584,6 +1576,7 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   if (const char* e = getenv("RR_HOST_PROF")) h->host_prof = atoi(e) != 0;
   if (const char* e = getenv("RR_FUSED_VERIFY")) h->fuse_verify = atoi(e) != 0;   // (A/B)
   if (const char* e = getenv("RR_SCREEN_I8")) h->screen_i8 = atoi(e) != 0;         // (A/B: 0 = the f16 copy only)
+  if (const char* e = getenv("RR_SCREEN_I8_MIN_ROWS")) h->i8_min_rows = atoll(e);
   if (const char* e = getenv("RR_STATIC_SCHEDULE")) h->dyn_sched = atoi(e) == 0;   // (A/B: 1 = rr_set_schedule(0))
   if (const char* e = getenv("RR_SCREEN_FULL_LISTS")) h->full_lists_env = atoi(e) != 0;   // (A/B: start with full lists)
   *out = h;

@@ -13,9 +13,11 @@ from parity_helpers import check_topk
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def Index(hip):
+@pytest.fixture
+def Index(hip, monkeypatch):
+    """(the int8 copy is made for shards of any size here: RR_SCREEN_I8_MIN_ROWS=0)"""
     from rag_service_amd import Index as _Index
+    monkeypatch.setenv("RR_SCREEN_I8_MIN_ROWS", "0")
     return _Index
 
 
