@@ -78,10 +78,12 @@ struct Shard {
   void* corpus = nullptr;                // [rows][d] fp32 or bf16
   uint16_t* scr16 = nullptr;             // fp32 storage: f16 copy of the rows for the screened search (or null)
   // fp32 storage: the int8 screen's copy (rr_sk.hip DT 8; or null): [round_up(rows, 2)][d] int8 rows (a padding row
-  // of zeros), per row its scale and error norm ([round_up(rows, 2)])
+  // of zeros), per row its scale and error norm ([rows]); per compute stream the queries' int8 pieces and scalars
   int8_t* scr8 = nullptr;
   float* sx8 = nullptr;
   float* e8 = nullptr;
+  int8_t* q8[2] = {nullptr, nullptr};
+  float* q8s[2] = {nullptr, nullptr};
   float* norms = nullptr;                // [round_up(rows, 32) + 32] |row| (pad = 1)
   float* rscale = nullptr;               // [same] split-f16 row scale 2^-e (pad = 1)
   float* qbuf[2] = {nullptr, nullptr};   // staged queries, double-buffered ([q_cap][d] fp32 each): a new
@@ -381,7 +383,7 @@ int dmalloc(T** p, size_t bytes) {
 
 int free_shard(Shard& s) {
   hipSetDevice(s.dev);
-  void* ptrs[] = {s.corpus, s.scr16, s.scr8, s.sx8, s.e8, s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.wcount, s.ctr, s.shard_keys, s.gathered, s.out_base,
+  void* ptrs[] = {s.corpus, s.scr16, s.scr8, s.sx8, s.e8, s.q8[0], s.q8[1], s.q8s[0], s.q8s[1], s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.wcount, s.ctr, s.shard_keys, s.gathered, s.out_base,
                   s.full_keys, s.sort_temp, s.wcand, s.wfloor, s.wsel};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -410,12 +412,15 @@ int free_shard(Shard& s) {
   return RR_OK;
 }
 
-// Release the shard's int8 screen copy (current device = s.dev).
+// Release the shard's int8 screen copy and its query buffers (current device = s.dev).
 void free_i8(Shard& s) {
-  for (void* p : {(void*)s.scr8, (void*)s.sx8, (void*)s.e8})
+  for (void* p : {(void*)s.scr8, (void*)s.sx8, (void*)s.e8, (void*)s.q8[0], (void*)s.q8[1], (void*)s.q8s[0],
+                  (void*)s.q8s[1]})
     if (p) hipFree(p);
   s.scr8 = nullptr;
   s.sx8 = s.e8 = nullptr;
+  s.q8[0] = s.q8[1] = nullptr;
+  s.q8s[0] = s.q8s[1] = nullptr;
 }
 
 // Allocate the shard's corpus storage for the current range (and norms when cosine).
@@ -446,6 +451,10 @@ int alloc_corpus(rr_handle* h, Shard& s) {
       bool ok = hipMalloc((void**)&s.scr8, (size_t)r2 * h->d) == hipSuccess;
       ok = ok && hipMalloc((void**)&s.sx8, (size_t)r2 * 4) == hipSuccess;
       ok = ok && hipMalloc((void**)&s.e8, (size_t)r2 * 4) == hipSuccess;
+      for (int i = 0; i < 2 && ok; ++i) {
+        ok = hipMalloc((void**)&s.q8[i], (size_t)2 * rr::kQSlots * h->d) == hipSuccess;
+        ok = ok && hipMalloc((void**)&s.q8s[i], (size_t)4 * rr::kQSlots * 4) == hipSuccess;
+      }
       // the padding row (odd row counts) is read as the second half of the last kernel row: zeros, scale 0
       if (ok && r2 > rows) {
         ok = hipMemset(s.scr8 + (size_t)rows * h->d, 0, h->d) == hipSuccess;
@@ -1199,10 +1208,13 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         a.eps_a = s16 ? kScreen16EpsA : kScreenEpsA;
         a.eps_b = s16 ? kScreen16EpsB : kScreenEpsB;
         if (s16) a.corpus = (const char*)s.scr16;
-        if (s8) {   // (the kernel quantises the block's queries itself)
+        if (s8) {   // the queries' int8 pieces on this stream first (the previous block's screen here is done with them)
+          HIP_TRY(rr::launch_q8_prep(qb, bb, d, s.q8[bsi], s.q8s[bsi], cs));
           a.corpus = (const char*)s.scr8;
           a.n = (s.rows() + 1) / 2;
           a.rows8 = s.rows();
+          a.q8 = s.q8[bsi];
+          a.q8s = s.q8s[bsi];
           a.sx8 = s.sx8;
           a.e8 = s.e8;
           a.eps_a = kScreen8EpsA;

@@ -93,7 +93,10 @@ struct SkArgs {
   uint64_t* vsync;
   uint64_t vbase;
   // int8 screen (KDT_SCREEN8): corpus = the int8 copy, read as n = ceil(rows8 / 2) kernel rows of two corpus rows each;
-  // sx8 / e8 [rows8] the rows' scales and error norms (the kernel quantises the fp32 queries itself)
+  // sx8 / e8 [rows8] the rows' scales and error norms; q8 [2][32][d] the queries' int8 pieces and q8s [4][32] their
+  // scalars (launch_q8_prep)
+  const int8_t* q8;
+  const float* q8s;
   const float* sx8;
   const float* e8;
   int64_t rows8;
@@ -181,7 +184,9 @@ hipError_t launch_f32_to_f16(const float* in, uint16_t* out, int64_t nrows, int 
 // fp32 rows (natural order) -> the int8 screen copy: per row sx = max|x| / 127, x8 = clamp(rint(x / sx), +-127),
 // e = an upper bound of |x - sx * x8| (rr_kernels.hip f32_to_i8_kernel)
 hipError_t launch_f32_to_i8(const float* in, int64_t nrows, int d, int8_t* out, float* sx, float* e, hipStream_t s);
-
+// The int8 screen's query pieces for a block of b <= 32 queries (slots b..31 zeroed): q8 [2][32][d], q8s [4][32] =
+// |q|, sum|q|, the pieces' scale / 64, an upper bound of |q - scale * (p1 + p2 / 64)|
+hipError_t launch_q8_prep(const float* q, int b, int d, int8_t* q8, float* q8s, hipStream_t s);
 hipError_t launch_row_norms(int dtype, const void* corpus, int64_t n, int d, float* norms, hipStream_t s);
 hipError_t launch_synth(int kind, uint64_t seed, int64_t row_begin, int64_t n_rows, int d, float* out,
                         hipStream_t s);

@@ -775,9 +775,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       // The scheduler wave (a 9th wave: no corpus, no query, no inline-asm loads, so hipcc's own waits around
       // its atomic drain nothing else). Per chunk it takes the next free chunk from the counter and publishes
       // it in nxt[] before the chunk's first reduction barrier; the streaming waves read it at the chunk's last
-      // step. It passes exactly the barriers the streaming waves pass: one after the query scalars (the int8 screen:
-      // two, see its query quantisation), one per tile.
-      if constexpr (DT == 8) __syncthreads();
+      // step. It passes exactly the barriers the streaming waves pass: one after the query scalars, one per tile.
       __syncthreads();
       int64_t ck = g;
       int cp = 0;
@@ -890,7 +888,17 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
             }
           }
         } else if constexpr (DT == 8) {
-          // (quantised from the fp32 rows below, with the query's max over every wave's slice)
+          // the query prep kernel's int8 pieces (natural element order, padding slots zero): wave w's K-slice of the
+          // two-row kernel row is elements (w % 4) KS .. + KS of its corpus row; K-step t, lane half h: 16 elements
+          // at 32 t + 16 h of slab j — the 16-byte column 2t + h of the LDS image, as DT 7
+          const int8_t* p1 = a.q8 + (size_t)rq * d;
+          const int8_t* p2 = a.q8 + (size_t)(QS + rq) * d;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int e0 = (w & (kWaves / 2 - 1)) * KS + j * kSlabRowBytes + 32 * t + 16 * h;
+            qf.c1[j][t] = *(const i32x4*)(p1 + e0);
+            qf.c2[j][t] = *(const i32x4*)(p2 + e0);
+          }
         } else if constexpr (DT == 7) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) {   // the bf16 layout (position 2t + h, 8 elements), f16 pieces c0 + c1
@@ -978,88 +986,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         }
       }
   };
-  // The int8 screen quantises the queries itself (no separate launch in front of every screen): s = max|q| / 127,
-  // p1 = clamp(rint(q / s)), p2 = clamp(rint((q / s - p1) * 64)), so q ~ s (p1 + p2 / 64) and the MFMAs sum
-  // x8 . (64 p1 + p2); eq >= |q - s (p1 + p2/64)| for the bound (rr_kernels.hip f32_to_i8_kernel's accounting, 2^-21).
-  // Wave w's K-slice of the two-row kernel row is elements (w % 4) KS .. + KS of its corpus row (waves w and w + 4
-  // hold the same query elements); K-step t, lane half h: the 16 elements at 32 t + 16 h of slab j (the LDS image's
-  // 16-byte column 2t + h, as DT 7). Pass 1: every query's max|q| -> LDS, barrier; pass 2
-  // (this wave's slice, from L2): the pieces, and |q|^2, sum|q| and the residual's squares per slice -> LDS, summed
-  // per query in the epilogue. The scheduler wave passes the extra barrier too.
-  float* q8l = (float*)vW;   // [32] query maxima, then [3][4][32] slice sums (MODE 1's scratch, unused in MODE 0)
-  if constexpr (DT == 8) {
-    // pass 1: every lane of the 8 waves takes 1/16 of one query's row (lane group (w, lane / 16) = query 4 w + lane
-    // / 16): one L2 round trip, then a 16-lane max
-    {
-      const int qi = 4 * w + (lane >> 4), part = lane & 15, per = d >> 4;   // d % 256 == 0: per % 4 == 0
-      const float* src = queries + (size_t)(qi < b ? qi : 0) * d + part * per;
-      const uint32_t msk = opaque_mask(qi < b);
-      float mx = 0.f;
-      for (int e = 0; e < per; e += 4) {
-        const f32x4 v = zero_unless(*(const f32x4*)(src + e), msk);
-        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-      }
-#pragma unroll
-      for (int off = 8; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
-      if (part == 0) q8l[qi] = mx;
-    }
-    __syncthreads();
-    // pass 2: this lane's slice, 32 values (two K-steps) at a time — each group's loads behind an opaque pointer and a
-    // compiler fence, so hipcc neither keeps pass 1's values live nor hoists all 128 loads at once (both spilled)
-    const float* qrow = queries + (size_t)(r < b ? r : 0) * d + (w & (kWaves / 2 - 1)) * KS + 16 * h;
-    const uint32_t qmask = opaque_mask(r < b);
-    const float m = q8l[r];
-    const float sq = m > 0.f ? m / 127.0f : 0.f;
-    const float rs = m > 0.f ? 127.0f / m : 0.f;   // (any pieces are valid: the bound uses their actual residual)
-    float se = 0.f, s2 = 0.f, s1 = 0.f;
-#pragma unroll
-    for (int j = 0; j < NS; ++j)
-#pragma unroll
-      for (int t2 = 0; t2 < 4; t2 += 2) {
-        const float* gp = qrow + j * kSlabRowBytes + 32 * t2;
-        asm volatile("" : "+v"(gp)::"memory");
-        f32x4 v[2][4];
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-          for (int u = 0; u < 4; ++u) v[tt][u] = zero_unless(*(const f32x4*)(gp + 32 * tt + 4 * u), qmask);
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-          i32x4 w1, w2;
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            uint32_t b1 = 0, b2 = 0;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float x = v[tt][u][e], tq = x * rs;
-              const float a1 = fminf(fmaxf(rintf(tq), -127.0f), 127.0f);
-              const float a2 = fminf(fmaxf(rintf((tq - a1) * 64.0f), -127.0f), 127.0f);
-              b1 |= ((uint32_t)(int)a1 & 0xFFu) << (8 * e);
-              b2 |= ((uint32_t)(int)a2 & 0xFFu) << (8 * e);
-              const float rr = x - sq * (a1 * 64.0f + a2) * 0x1p-6f;
-              se = fmaf(rr, rr, se);
-              s2 = fmaf(x, x, s2);
-              s1 += fabsf(x);
-            }
-            w1[u] = (int)b1;
-            w2[u] = (int)b2;
-          }
-          // (done before the next group's loads: otherwise hipcc defers the arithmetic and keeps every value live)
-          asm volatile("" : "+v"(w1), "+v"(w2), "+v"(se), "+v"(s2), "+v"(s1));
-          qfs[0].c1[j][t2 + tt] = w1;
-          qfs[0].c2[j][t2 + tt] = w2;
-        }
-      }
-    se += __shfl_xor(se, 32, 64);
-    s2 += __shfl_xor(s2, 32, 64);
-    s1 += __shfl_xor(s1, 32, 64);
-    if (w < kWaves / 2 && h == 0) {
-      q8l[32 + w * 32 + r] = se;
-      q8l[160 + w * 32 + r] = s2;
-      q8l[288 + w * 32 + r] = s1;
-    }
-    pin_frags();
-  } else if constexpr (DT != 2) {
+  if constexpr (DT != 2) {
     build_frags();
     pin_frags();
   }
@@ -1202,20 +1129,11 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   float qn = COS && !SCR ? qinfo[qe] : 0.f;
   const float qs = DT == 2 ? qinfo[QS + qe] : 1.f;
   float qsa = 0.f, q8sc = 0.f, q8eq = 0.f;
-  if constexpr (DT == 8) {   // the query quantisation's max and per-slice sums (waves 0-3 cover d)
-    const float* q8l = (const float*)vW;
-    const float m = q8l[qe];
-    float se = 0.f, s2 = 0.f, s1 = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < kWaves / 2; ++ww) {
-      se += q8l[32 + ww * 32 + qe];
-      s2 += q8l[160 + ww * 32 + qe];
-      s1 += q8l[288 + ww * 32 + qe];
-    }
-    qn = sqrtf(s2);
-    qsa = s1 * (1.0f + 0x1p-18f);
-    q8sc = (m > 0.f ? m / 127.0f : 0.f) * 0x1p-6f;
-    q8eq = fmaf(sqrtf(se), 1.0f + 0x1p-12f, m * sqrtf((float)d) * 0x1p-21f);
+  if constexpr (DT == 8) {
+    qn = a.q8s[qe];
+    qsa = a.q8s[QS + qe];
+    q8sc = a.q8s[2 * QS + qe];
+    q8eq = a.q8s[3 * QS + qe];
   } else if constexpr (SCR) {
     const float* part = (const float*)vW;
     float s2 = 0.f, s1 = 0.f;
@@ -2175,7 +2093,7 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
   }
   if (sdt == KDT_SCREEN8) {   // the screen over the int8 copy (a.corpus = that copy, a.n = ceil(a.rows8 / 2))
     const int ns8 = sk_slabs(KDT_SCREEN8, a.d);
-    if (qslots != 32 || ring != 2 || !ns8 || !a.sx8 || !a.e8 || a.n != (a.rows8 + 1) / 2)
+    if (qslots != 32 || ring != 2 || !ns8 || !a.q8 || !a.q8s || !a.sx8 || !a.e8 || a.n != (a.rows8 + 1) / 2)
       return hipErrorInvalidValue;
     const bool dyn = a.dyn && a.ctr && kt <= 16;
     if (a.full_lists)
