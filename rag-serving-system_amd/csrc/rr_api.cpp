@@ -856,7 +856,7 @@ bool screened(const rr_handle* h, int k, int slots) {
 // read; the bench pays its re-run itself).
 //   * narrow (16-entry) lists -> 32-entry ones when more than 1 in 32 settled narrow blocks re-ran (over >= 64);
 //   * the int8 copy's screen -> the f16 copy's when more than 1 in 32 blocks of a window re-ran (its bound is ~8x
-//     looser: corpora whose top scores crowd within it);
+//     looser: corpora whose top scores crowd within it), with full lists at once when more than 1 in 2 re-ran;
 //   * windows of >= 32 settled screened blocks of the current configuration (list width, per-lane list form):
 //     short per-lane lists (4 keys + the workgroup's floor, rr_sk.hip KL) -> full lists (KT keys) when more than
 //     1 in 32 re-ran (each costs an exact pass, twice a screen: 3 % re-run cost more than the full lists do):
@@ -886,7 +886,13 @@ void observe_settled(rr_handle* h, int blocks, bool narrow, bool full, bool wide
   h->win_nf += nre;
   if (h->win_nb < 32) return;
   if (i8) {   // the int8 screen's looser bound first gives way to the f16 copy's
-    if (h->win_nf * 32 > h->win_nb) h->i8_off = true;
+    if (h->win_nf * 32 > h->win_nb) {
+      h->i8_off = true;
+      // most blocks re-ran: crowded near-duplicates that the f16 copy's short lists will not prove either — its full
+      // lists come with it, so a corpus the screen cannot prune still reaches the pause one window later, as before
+      // the int8 copy (profiles/r04/final/clustered.jsonl: contiguous clusters otherwise paid screen + re-run)
+      if (h->win_nf * 2 > h->win_nb) h->full_lists = true;
+    }
   } else if (!h->full_lists) {
     if (h->win_nf * 32 > h->win_nb) h->full_lists = true;
   } else if (h->win_nf * 2 > h->win_nb && !narrow) {
