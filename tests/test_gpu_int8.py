@@ -81,8 +81,9 @@ def test_int8_screen_proves_unit_norm_blocks_in_the_wide_phase(Index):
 
 
 def test_int8_screen_gives_way_to_the_f16_copy(Index):
-    """Adaptive: a window of settled blocks that re-ran (forced here) switches the handle to the f16 copy before
-    the per-lane lists grow; results stay exact throughout; a reload re-arms the int8 screen."""
+    """Adaptive: a window of settled blocks that re-ran (forced here) switches the handle to the f16 copy — with its
+    full per-lane lists, since every block re-ran — not yet to the pause; results stay exact throughout; a reload
+    re-arms the int8 screen."""
     rng = np.random.default_rng(3)
     corpus = rng.standard_normal((20000, 1024)).astype(np.float32)
     q = rng.standard_normal((32, 1024)).astype(np.float32)
@@ -96,7 +97,8 @@ def test_int8_screen_gives_way_to_the_f16_copy(Index):
         got = ix.search(q, 5)
         assert np.array_equal(got[1], want[1])
     assert not ix.screen_int8()
-    assert ix.screen_state()[0] is False   # the f16 copy comes first; its lists are still short
+    # every block re-ran (more than 1 in 2): the f16 copy takes over with its full per-lane lists at once
+    assert ix.screen_state() == (True, 0, 0)
     ix.set_kernel("auto")
     got = ix.search(q, 5)
     assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
