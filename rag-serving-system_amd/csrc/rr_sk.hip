@@ -712,7 +712,10 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // Workgroup g takes chunk g, then (SCHED) the next free chunk from a device counter — workgroups on CUs that
   // get a larger share of the HBM bandwidth take more chunks, so all of them finish together — or (static)
   // chunks g + G, g + 2G, ...
-  constexpr int CT = NS >= 4 ? 2 : NS == 3 ? 3 : NS == 2 ? 4 : 8;
+#ifndef RR_SK_CT8
+#define RR_SK_CT8 4   // the int8 screen's tiles per chunk (64 corpus rows each)
+#endif
+  constexpr int CT = DT == 8 ? RR_SK_CT8 : NS >= 4 ? 2 : NS == 3 ? 3 : NS == 2 ? 4 : 8;
   const int64_t G = gridDim.x, g = blockIdx.x;
   const int64_t T = (n + 31) / 32, C = (T + CT - 1) / CT;
 
