@@ -229,6 +229,7 @@ struct rr_handle {
   int x_delay_us = 0;           // A/B: RR_X_EXCHANGE_DELAY_US, a stand-in for a slower exchange
   int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy)
   int screen_i8 = 1;            // ... and an int8 copy, screened first (rr_screen_int8; RR_SCREEN_I8=0 at creation: off)
+  int ct8 = 0;                  // the int8 screen's tiles per chunk (0: by shard size; A/B: RR_SCREEN_CT8)
   int64_t i8_min_rows = 65536;  // ... for shards of at least this many rows (RR_SCREEN_I8_MIN_ROWS): below, a search is
                                 // launch-bound and lists holding a large share of the shard's rows leave the looser
                                 // bound little to prove with (a 1000-row corpus of real embeddings re-ran blocks)
@@ -1223,6 +1224,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
           a.q8s = s.q8s[bsi];
           a.sx8 = s.sx8;
           a.e8 = s.e8;
+          a.ct8 = h->ct8 > 0 ? h->ct8 : s.rows() < 500000 ? 2 : 4;   // (A/B: RR_SCREEN_CT8)
           a.eps_a = kScreen8EpsA;
           a.eps_b = kScreen8EpsB;
         }
@@ -1595,6 +1597,7 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   if (const char* e = getenv("RR_FUSED_VERIFY")) h->fuse_verify = atoi(e) != 0;   // (A/B)
   if (const char* e = getenv("RR_SCREEN_I8")) h->screen_i8 = atoi(e) != 0;         // (A/B: 0 = the f16 copy only)
   if (const char* e = getenv("RR_SCREEN_I8_MIN_ROWS")) h->i8_min_rows = atoll(e);
+  if (const char* e = getenv("RR_SCREEN_CT8")) h->ct8 = atoi(e);
   if (const char* e = getenv("RR_STATIC_SCHEDULE")) h->dyn_sched = atoi(e) == 0;   // (A/B: 1 = rr_set_schedule(0))
   if (const char* e = getenv("RR_SCREEN_FULL_LISTS")) h->full_lists_env = atoi(e) != 0;   // (A/B: start with full lists)
   *out = h;

@@ -100,6 +100,7 @@ struct SkArgs {
   const float* sx8;
   const float* e8;
   int64_t rows8;
+  int ct8;                 // tiles per chunk of the dynamic schedule (0: the kernel's default)
 };
 
 // Split-K streaming kernel (rr_sk.hip): same output contract as launch_fused. sdt = KDT_* (0..3).

@@ -712,10 +712,10 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // Workgroup g takes chunk g, then (SCHED) the next free chunk from a device counter — workgroups on CUs that
   // get a larger share of the HBM bandwidth take more chunks, so all of them finish together — or (static)
   // chunks g + G, g + 2G, ...
-#ifndef RR_SK_CT8
-#define RR_SK_CT8 4   // the int8 screen's tiles per chunk (64 corpus rows each)
-#endif
-  constexpr int CT = DT == 8 ? RR_SK_CT8 : NS >= 4 ? 2 : NS == 3 ? 3 : NS == 2 ? 4 : 8;
+  constexpr int CT0 = NS >= 4 ? 2 : NS == 3 ? 3 : NS == 2 ? 4 : 8;
+  // the int8 screen: a.ct8 tiles (of 64 corpus rows) per chunk — 2 on small shards, where a 4-tile chunk is a large
+  // share of a workgroup's work and the last ones leave a tail (profiles/r04/ab/ab_ct8.txt), else 4
+  const int CT = DT == 8 && a.ct8 > 0 ? a.ct8 : CT0;
   const int64_t G = gridDim.x, g = blockIdx.x;
   const int64_t T = (n + 31) / 32, C = (T + CT - 1) / CT;
 
@@ -1365,7 +1365,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #define RR_SK_PIPE 0   // measured: -2 % on the 64-slot pass (12-16 B of spills), within noise on the screen
 #endif
   constexpr bool PIPE = MODE == 0 && RR_SK_PIPE && KT <= 16 && !(QH == 2 && DT == 2) && DT != 8 &&
-                        (SCHED == 0 || CT >= 3);   // (else spills)
+                        (SCHED == 0 || CT0 >= 3);   // (else spills)
   int64_t pbase = 0;   // PIPE: the previous tile's first row and factor slot
   int pts = 0;
   // Stagger (streaming passes): waves 4-7 — the SIMD partners of waves 0-3 — run each tile's epilogue one tile
