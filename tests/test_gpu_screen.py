@@ -574,7 +574,8 @@ def test_fused_verify_matches_separate_verify(Index, layout, monkeypatch):
     if layout == "interleaved":     # the fused verify's wide phase proves what the separate one proves
         # (the fused launch's grid depends on whether the other stream is busy — half the CUs beside it — so its lists,
         # and which blocks the dynamic schedule leaves unproven, can differ by a block; the results never do)
-        assert flagged <= 2 and reruns == flagged and wide >= 32 and counts[False][1] == 0 and counts[False][3] >= 32
+        # (a flagged staged search that nobody fetched is superseded, not re-run: reruns <= flagged)
+        assert flagged <= 2 and reruns <= flagged and wide >= 32 and counts[False][1] == 0 and counts[False][3] >= 32
     else:
         assert flagged >= 1 and reruns >= 1
     ex.close()
