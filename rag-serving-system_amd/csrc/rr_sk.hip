@@ -1131,12 +1131,17 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   const bool qev = MODE == 1 ? qe == vq : qe < b;
   float qn = COS && !SCR ? qinfo[qe] : 0.f;
   const float qs = DT == 2 ? qinfo[QS + qe] : 1.f;
-  float qsa = 0.f, q8sc = 0.f, q8eq = 0.f;
+  float qsa = 0.f, q8sc = 0.f, q8e1 = 0.f, q8e2 = 0.f, q8e3 = 0.f;
   if constexpr (DT == 8) {
     qn = a.q8s[qe];
     qsa = a.q8s[QS + qe];
     q8sc = a.q8s[2 * QS + qe];
-    q8eq = a.q8s[3 * QS + qe];
+    // the bound's slack e Q1 + |x| Q2 + Q3 (see the epilogue), its per-query factors once: all terms are positive and
+    // each is rounded a few times, which the 1.001 margin covers
+    const float eq = a.q8s[3 * QS + qe];
+    q8e1 = (qn + eq) * 1.001f;
+    q8e2 = (eq + fmaf(a.eps_a, qn, a.eps_b * a.sqrt_d)) * 1.001f;
+    q8e3 = a.eps_b * qsa * 1.001f;
   } else if constexpr (SCR) {
     const float* part = (const float*)vW;
     float s2 = 0.f, s1 = 0.f;
@@ -1287,7 +1292,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
             // residuals whose squares underflow fp32 in e, |r| < 2^-63); x 1.001 for the roundings of
             // |q| and of these products, 2^-21 |est| for the three roundings of est
             const float est = (s * fac1[e]) * q8sc;
-            const float eps = (fmaf(qn + q8eq, fac2[e], q8eq * nd) + fmaf(a.eps_a * nd, qn, a.eps_b * fmaf(a.sqrt_d, nd, qsa))) * 1.001f;
+            // = ((|q| + eq) e + eq |x| + eps_a |x||q| + eps_b (sqrt(d) |x| + sum|q|)) x 1.001, factored per query
+            const float eps = fmaf(fac2[e], q8e1, fmaf(nd, q8e2, q8e3));
             v = est + fmaf(fabsf(est), 0x1p-21f, eps);
           } else {
             const float eps = fmaf(a.eps_a * nd, qn, a.eps_b * fmaf(a.sqrt_d, nd, qsa));

@@ -42,7 +42,12 @@ def bound(xq, sx, e, nd, p1, p2, qsc, eq, qn, qsa, eps_a=6e-5, eps_b=4e-8):
     s = acc.astype(F)
     est = (s * sx).astype(F) * qsc
     sqrt_d = F(np.sqrt(xq.shape[1]) * (1 + 2 ** -20))
-    eps = ((qn + eq) * e + eq * nd + (F(eps_a) * nd * qn + F(eps_b) * (sqrt_d * nd + qsa))) * F(1.001)
+    # the kernel's factored form: e Q1 + |x| Q2 + Q3 with per-query Q1 = (|q| + eq), Q2 = eq + eps_a |q| + eps_b sqrt(d),
+    # Q3 = eps_b sum|q|, each x 1.001
+    q1 = F((qn + eq) * F(1.001))
+    q2 = F((eq + (F(eps_a) * qn + F(eps_b) * sqrt_d)) * F(1.001))
+    q3 = F(F(eps_b) * qsa * F(1.001))
+    eps = (e * q1 + (nd * q2 + q3)).astype(F)
     v = est + np.abs(est) * F(2 ** -21) + eps
     return v + np.abs(v) * F(2 ** -22)
 
