@@ -121,3 +121,25 @@ def test_int8_screen_sharded_and_odd_rows(Index):
     want = ix.search(q, 8)
     assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
     ix.close()
+
+
+@pytest.mark.parametrize("ct", ["2", "4"])
+def test_int8_screen_chunk_sizes(Index, monkeypatch, ct):
+    """The int8 screen's dynamic-schedule chunk (2 tiles of 64 rows below 500k rows per shard, else 4; RR_SCREEN_CT8
+    forces either): any chunk size gives the exact kernel's results, on the static schedule too."""
+    monkeypatch.setenv("RR_SCREEN_CT8", ct)
+    rng = np.random.default_rng(int(ct))
+    n, d = 150001, 1024
+    q = rng.standard_normal((32, d)).astype(np.float32)
+    corpus = _spiky_corpus(rng, n, d, q)
+    ix = Index(dtype="fp32", metric="cosine")
+    ix.load(corpus)
+    assert ix.screen_int8()
+    got = [ix.search(q, 5)]
+    ix.set_schedule(False)
+    got.append(ix.search(q, 5))
+    ix.set_kernel("exact")
+    want = ix.search(q, 5)
+    for g in got:
+        assert np.array_equal(g[1], want[1]) and np.array_equal(g[0], want[0])
+    ix.close()
