@@ -1465,7 +1465,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #ifndef RR_SK_PRIO
 #define RR_SK_PRIO 1
 #endif
-  if (MODE == 0 && ((RR_SK_PRIO == 1 && w >= 4) || (RR_SK_PRIO == 2 && w < 4))) __builtin_amdgcn_s_setprio(1);
+  // (not the int8 screen, which runs without the stagger: +1.5-3 % without it, profiles/r04/ab/ab_i8_prio.txt)
+  if (MODE == 0 && DT != 8 && ((RR_SK_PRIO == 1 && w >= 4) || (RR_SK_PRIO == 2 && w < 4))) __builtin_amdgcn_s_setprio(1);
   unsigned long long ph_t = PH_NOW();
   (void)ph_t;
   SK_PROBE(1);
