@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 7
+#define RR_ABI_VERSION 8
 
 /* error codes */
 #define RR_OK             0
@@ -140,7 +140,9 @@ int rr_shard_range(const rr_handle* h, int i, int64_t* begin, int64_t* end);
 /* Overwrite existing corpus rows in place: host_rows (n_rows x d fp32) replace the rows at the given global indices
  * (each in [0, n_total); a repeated index keeps its last row). Rows outside the local shards are skipped, so every
  * rank of a world may pass the same list. Converted and indexed exactly like loaded rows (storage dtype, per-row
- * norms, the screening copy). Settles and synchronises the handle first. (The reference has no update path: its
+ * norms, the screening copies). Settles and synchronises the handle first. Under rr_init_dist EVERY rank must call it
+ * (a collective: the ranks agree by an RCCL min whether the screen's f16 range still holds for every rank's rows).
+ * (The reference has no update path: its
  * corpus is replaced by reloading, retriever.py:576-582; rr_load stays that path.) */
 int rr_update_rows(rr_handle* h, const float* host_rows, const int64_t* row_idx, int64_t n_rows, int32_t d);
 
@@ -213,6 +215,16 @@ int rr_set_schedule(rr_handle* h, int dynamic);
  * identical. *in_use (may be null): the streams in use (1 or 2). Synchronises the handle's streams when the
  * setting changes. */
 int rr_set_compute_streams(rr_handle* h, int32_t n, int32_t* in_use);
+
+/* Carried verify of the screened search (fp32 storage, the f16 / int8 copy's screen, k <= 13; default on): screened
+ * blocks run on ONE compute stream and a block's exact verify is launched inside the NEXT screened block's screen —
+ * 32 more workgroups verify the previous block's query slots and then join the screen — so a stream of searches costs
+ * one launch per block and the verifying CUs stream rows as soon as they are done. A block's verify runs alone
+ * (flushed) whenever its results, flag or lists are needed first: rr_fetch_results, rr_synchronize, rr_search,
+ * rr_search_async, rr_wait, any other kind of search. Results are bit-identical either way; with it on,
+ * rr_set_compute_streams' two streams are not used. on: 1 / 0 / -1 (leave as is); *in_use (may be null): the
+ * setting. Synchronises the handle when the setting changes. (RR_CARRY_VERIFY=0 at rr_create: off.) */
+int rr_set_carry_verify(rr_handle* h, int32_t on, int32_t* in_use);
 
 /* The screened search's f16 copy (fp32 storage): the screen pass reads an f16 copy of the rows — exactly the
  * values it would round the fp32 rows to in registers — so it streams half the bytes; the verify and every

@@ -115,8 +115,8 @@ struct Shard {
   int* pin_scount = nullptr;             // pinned staging of scount / wcount reads (rr_screen_counts)
   uint32_t* ctr = nullptr;               // split-K chunk counters (dynamic schedule), 0 between launches: one per
                                          // compute stream, kCtrStride words apart; then (words 2 and 3 x kCtrStride)
-                                         // each compute stream's 64-bit count of fused-verify screen workgroups
-  uint64_t vbase[2] = {0, 0};            // ... that count when the stream's next fused launch begins
+  int pend_nlists = 0;                   // the pending (carried) verify's list count: its screen's grid here
+  int pend_nlists_next = 0;              // (the block being enqueued)
   uint64_t* shard_keys = nullptr;        // [32][k_cap] this shard's top-k (all-gather send buffer)
   uint64_t* gathered = nullptr;          // [world][32][k_cap] (all-gather receive buffer)
   // pipelined exchange (k <= RR_FUSED_KMAX, world > 1): the exchange of search i (all-gather + final
@@ -169,6 +169,15 @@ struct Shard {
 
 // One in-flight rr_search_async batch: a pinned buffer that carries its queries to the device and,
 // stream-ordered after the search, its results back.
+// A screened block whose verify is not launched yet: it runs in the next screened block's screen launch (rr_sk.hip
+// carry_verify) or alone when something needs the block's results first (flush_verify). Its lists are in candidate half
+// p, its queries in query buffer qpar; results in place (no exchange) or its keys + flag word in px_keys[x].
+struct PendVerify {
+  bool on = false;
+  int q0 = 0, bb = 0, k = 0, kt = 0, slots = 0, x = 0, p = 0, seq = 0, qpar = 0;
+  bool force = false;   // RR_KERNEL_SCREEN_FALLBACK when the block was enqueued (test hook: report it incomplete)
+};
+
 struct AsyncSlot {
   char* pin = nullptr;
   size_t cap = 0;
@@ -234,6 +243,7 @@ struct rr_handle {
                                 // launch-bound and lists holding a large share of the shard's rows leave the looser
                                 // bound little to prove with (a 1000-row corpus of real embeddings re-ran blocks)
   bool i8_off = false;          // adaptive: the int8 screen re-ran too often on this corpus, the f16 copy screens
+  bool i8_all = false;          // every shard of the world holds an int8 copy (agreed across ranks at load: finish_all)
   bool last_i8 = false;         // the last search screened the int8 copy
   int64_t narrow_settled = 0;   // settled screened blocks run with 16-entry lists where 2k + 2 wanted 32 (screen_kt)
   int64_t narrow_reruns = 0;    // ... of them re-run exactly
@@ -250,7 +260,10 @@ struct rr_handle {
   int wide_verify = 1;          // the verify's wide phase (A/B: RR_WIDE_VERIFY=0)
   bool host_prof = false;       // RR_HOST_PROF=1 (diagnostics)
   HostProf hp;
-  bool fuse_verify = false;     // the exchange path's screens verify their own lists (RR_FUSED_VERIFY=1; slower)
+  // Carried verify (rr_set_carry_verify; RR_CARRY_VERIFY=0 at creation: off): screened blocks run on one compute stream
+  // and each block's verify rides in the next block's screen launch (rr_sk.hip carry_verify)
+  int carry = 1;
+  PendVerify pend;
   bool ab_no_verify = false;    // A/B only (RR_AB_NO_VERIFY=1): skip the screened search's verify launch — results
                                 // invalid; measures what the verify's launch costs the step
   // adaptive screen (observe_settled): the screen's per-lane lists grow from 4 keys to KT once blocks flag, and
@@ -504,37 +517,47 @@ int finish_corpus(rr_handle* h, Shard& s, bool* screen_ok) {
   return wait_stream(h, s, s.stream, "the corpus norms");
 }
 
+// Multi-process mode: every rank's verdicts v[0..n) (0 / 1) reduced to their minimum, element-wise (one RCCL min on
+// shard 0's stream), so that data-dependent path choices agree across ranks. `what` names the agreement in errors;
+// `scale` multiplies the deadline (ranks reach a load's agreement at different times). Without rr_init_dist: v as is.
+int agree_min(rr_handle* h, int* v, int n, const char* what, int scale) {
+  if (!h->dist) return RR_OK;
+  Shard& s = h->shards[0];
+  HIP_TRY(hipSetDevice(s.dev));
+  int* dv = nullptr;
+  HIP_TRY(hipMalloc((void**)&dv, (size_t)n * sizeof(int)));
+  int rc = RR_OK;
+  hipError_t e = hipMemcpyAsync(dv, v, (size_t)n * sizeof(int), hipMemcpyHostToDevice, s.stream);
+  if (e == hipSuccess) {
+    const ncclResult_t r = ncclAllReduce(dv, dv, n, ncclInt32, ncclMin, s.comm, s.stream);
+    if (r != ncclSuccess) rc = fail(RR_E_RCCL, "%s failed: %s", what, ncclGetErrorString(r));
+  }
+  if (e == hipSuccess && rc == RR_OK) rc = wait_stream(h, s, s.stream, what, scale);
+  if (e == hipSuccess && rc == RR_OK) e = hipMemcpy(v, dv, (size_t)n * sizeof(int), hipMemcpyDeviceToHost);
+  if (!h->failed) hipFree(dv);
+  if (rc) return rc;
+  if (e != hipSuccess) return fail(RR_E_HIP, "%s failed: %s", what, hipGetErrorString(e));
+  return RR_OK;
+}
+
 // Finish every local shard; the screened search is allowed only when every shard's range allows it — in a
 // multi-process world every rank's shard: the ranks must take the same path, since the screen's list width sizes
-// the all-gather and the re-run decisions issue collectives (an RCCL min over the ranks' verdicts).
+// the all-gather and the re-run decisions issue collectives (an RCCL min over the ranks' verdicts). Likewise whether
+// EVERY shard holds an int8 copy (each rank allocates its own when its shard is large enough and HBM has room): the
+// adaptive screen judges int8-screened searches by their own rule (observe_settled), and ranks must judge alike.
 int finish_all(rr_handle* h) {
-  bool ok = true;
+  bool ok = true, i8 = true;
   for (Shard& s : h->shards) {
     bool sok = false;
     if (int rc = finish_corpus(h, s, &sok)) return rc;
     ok = ok && sok;
+    i8 = i8 && (s.scr8 != nullptr || s.rows() == 0);
   }
-  if (h->dist) {
-    Shard& s = h->shards[0];
-    HIP_TRY(hipSetDevice(s.dev));
-    int* dv = nullptr;
-    HIP_TRY(hipMalloc((void**)&dv, sizeof(int)));
-    int all = 0;
-    int rc = RR_OK;
-    hipError_t e = hipMemsetD32Async((hipDeviceptr_t)dv, ok ? 1 : 0, 1, s.stream);
-    if (e == hipSuccess) {
-      const ncclResult_t r = ncclAllReduce(dv, dv, 1, ncclInt32, ncclMin, s.comm, s.stream);
-      if (r != ncclSuccess) rc = fail(RR_E_RCCL, "screen-range agreement failed: %s", ncclGetErrorString(r));
-    }
-    // ranks finish loading at different times: a generous multiple of the deadline
-    if (e == hipSuccess && rc == RR_OK) rc = wait_stream(h, s, s.stream, "the ranks' screen-range agreement", 10);
-    if (e == hipSuccess && rc == RR_OK) e = hipMemcpy(&all, dv, sizeof(int), hipMemcpyDeviceToHost);
-    if (!h->failed) hipFree(dv);
-    if (rc) return rc;
-    if (e != hipSuccess) return fail(RR_E_HIP, "screen-range agreement failed: %s", hipGetErrorString(e));
-    ok = all != 0;
-  }
-  h->screen_ok = ok;
+  int v[2] = {ok ? 1 : 0, i8 ? 1 : 0};
+  // ranks finish loading at different times: a generous multiple of the deadline
+  if (int rc = agree_min(h, v, 2, "the ranks' screen-range agreement", 10)) return rc;
+  h->screen_ok = v[0] != 0;
+  h->i8_all = v[1] != 0;
   return RR_OK;
 }
 
@@ -672,6 +695,7 @@ int drop_work_buffers(rr_handle* h) {
   h->screen_pause = h->pauses = 0;
   h->last_screened = false;
   h->last_settled = true;
+  h->pend.on = false;   // (its buffers are gone: the search it belonged to is discarded with them)
   h->qpar = 0;
   h->loaded = false;
   return RR_OK;
@@ -749,7 +773,6 @@ int ensure_buffers(rr_handle* h, int b, int k) {
       ((volatile int*)s.pin_scount)[0] = ((volatile int*)s.pin_scount)[1] = 0;
       if (int rc = dmalloc(&s.ctr, 4 * kCtrStride * sizeof(uint32_t))) return rc;
       HIP_TRY(hipMemset(s.ctr, 0, 4 * kCtrStride * sizeof(uint32_t)));
-      s.vbase[0] = s.vbase[1] = 0;
     }
     if ((h->world > 1 || h->dist) && !s.px_keys[0]) {
       for (int p = 0; p < kXSlots; ++p) {
@@ -955,7 +978,8 @@ int collect_timing(rr_handle* h) {
 // Measured against one stream and every CU screening (profiles/r02/ab/ab_screen_grid*.txt): +23-45 % per step at
 // 125k-250k rows, +2-5 % at 1M-2M.
 constexpr int kVerifyCUs = 32;
-bool two_streams(const rr_handle* h, const Shard&) { return h->streams == 2; }
+// (carry mode: one compute stream — the next block's launch carries this block's verify, so blocks cannot overlap)
+bool two_streams(const rr_handle* h, const Shard&) { return h->streams == 2 && !h->carry; }
 // Screen workgroups on shard s; `alone`: no screened block is in flight on the other stream (its last verify has
 // completed: a single search, or the first of a burst), so nothing overlaps this one and every CU screens.
 int screen_grid(const rr_handle* h, const Shard& s, bool alone) {
@@ -1121,6 +1145,45 @@ rr::SkArgs sk_base(const rr_handle* h, const Shard& s, const float* qb, int bb) 
   return a;
 }
 
+// The verify's arguments (MODE 1, or a carried verify's fields of a screen launch) for screened block v on shard s:
+// its screen's nlists lists in candidate half v.p; results in place, or (exchange) this shard's exact keys and the
+// block's flag word in px_keys[v.x] (else the flag is the result buffer's head).
+void verify_args(const rr_handle* h, const Shard& s, const PendVerify& v, int nlists, rr::SkArgs* a) {
+  const bool multi = h->world > 1 || h->dist;
+  a->vin = s.cand + (size_t)v.p * cand_half(s);
+  a->nlists = nlists;
+  a->k_out = v.k;
+  a->out_scores = multi ? nullptr : s.out_scores + (size_t)v.q0 * v.k;
+  a->out_idx = multi ? nullptr : s.out_idx + (size_t)v.q0 * v.k;
+  a->out_keys = multi ? s.px_keys[v.x] : nullptr;
+  a->flag = multi ? s.px_keys[v.x] + (size_t)v.slots * v.kt : (uint64_t*)s.out_base;
+  a->count = s.scount;
+  a->force_incomplete = v.force ? 1 : 0;
+  a->wide_verify = h->wide_verify;
+  a->wide_count = s.wcount;
+}
+
+int enqueue_exchange_px(rr_handle* h, int p, int x, int q0, int bb, int k, int kt, int slots, bool scr);
+
+// Launch the pending carried verify on its own (MODE 1, 32 workgroups, on `stream` after its screen) and, with an
+// exchange step, the block's exchange: whenever something needs that block's results, flag or candidate lists before
+// the next screened launch would carry it.
+int flush_verify(rr_handle* h) {
+  if (!h->pend.on) return RR_OK;
+  const PendVerify v = h->pend;
+  h->pend.on = false;
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    rr::SkArgs a = sk_base(h, s, s.qbuf[v.qpar] + (size_t)v.q0 * h->d, v.bb);
+    verify_args(h, s, v, s.pend_nlists, &a);
+    a.seq = v.seq;
+    HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, v.kt, 1, rr::kQSlots, rr::kQSlots, a, s.stream));
+  }
+  if (h->world > 1 || h->dist)
+    if (int rc = enqueue_exchange_px(h, v.p, v.x, v.q0, v.bb, v.k, v.kt, v.slots, true)) return rc;
+  return RR_OK;
+}
+
 // Enqueue the device pipeline for query block [q0, q0 + bb) (bb <= slots) on every local shard.
 int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
   const int d = h->d;
@@ -1131,6 +1194,14 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
   const bool local_multi = multi && !h->dist;
   const int p = h->parity;
   const int x = h->xslot;   // pipelined-exchange buffer set of this block
+  // Carried verify (rr_sk.hip carry_verify): a screened block on the dynamic schedule over the f16 / int8 copy (every
+  // shard) defers its verify into the next such launch; a pending verify of another list width is flushed first, and
+  // every other kind of block flushes it (enqueue_block).
+  bool cm = scr && h->carry && h->dyn_sched && kt <= 16 && !h->ab_no_verify;
+  for (const Shard& s : h->shards) cm = cm && s.rows() > 0 && s.scr16 && h->screen_copy && rr::sk_slabs(rr::KDT_SCREEN16, d);
+  if (h->pend.on && (!cm || h->pend.kt != kt))
+    if (int rc = flush_verify(h)) return rc;
+  const bool carrying = cm && h->pend.on;
   if (scr || wk) {
     ++h->screen_seq;
     ++h->screen_blocks;
@@ -1191,24 +1262,19 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       const bool s16 = s.scr16 && h->screen_copy && rr::sk_slabs(rr::KDT_SCREEN16, d);
       // the int8 copy: a quarter of the fp32 bytes, a bound ~8x looser (more rows reach the verify's wide phase)
       const bool s8 = s16 && s.scr8 && i8_active(h);
-      // Fused verify (rr_sk.hip fused_verify): with an exchange step the verify writes keys, not result rows, so the
-      // screen's last 32 workgroups can verify in the same launch; the screen then always takes every CU.
-      const int full_grid = screen_grid(h, s, true);
-      const bool fuse = multi && h->fuse_verify && !h->ab_no_verify && s.rows() > 0 && s16 && !s8 && h->dyn_sched && kt <= 16 &&
-                        2 * rr::sk_slabs(rr::KDT_SCREEN16, d) <= 4 && full_grid >= 2 * rr::kQSlots;
       const bool alone = !two || s.last_vsi < 0 || s.last_vsi == bsi ||
                          hipEventQuery(s.ev_q[s.last_vq][s.last_vsi]) == hipSuccess;
-      // A fused launch must have its whole grid resident (its verifiers wait for every workgroup's lists): alone it
-      // takes every CU; beside the other stream's fused launch each takes half, so the two always fit together (a
-      // workgroup left waiting for a CU the other launch holds would hold back this block's verify by a whole screen).
-      const int sgrid = fuse ? (alone ? full_grid : std::max(2 * rr::kQSlots, std::min(full_grid, s.cus / 2)))
-                             : screen_grid(h, s, alone);
+      // Carried verify (rr_sk.hip carry_verify): this block's verify is deferred into the next screened block's launch
+      // (or a flush); when the previous block's is pending, 32 more workgroups verify it first and then join this
+      // screen. The launch takes every CU.
+      int sgrid = screen_grid(h, s, alone);
+      if (cm) sgrid = carrying ? std::max(1, sgrid - rr::kQSlots) + rr::kQSlots : sgrid;
       const int64_t tl = h->host_prof ? now_ns() : 0;
       if (timed) HIP_TRY(hipEventRecord(e0, cs));
       if (s.rows() > 0) {
         rr::SkArgs a = sk_base(h, s, qb, bb);
         a.out = candp;
-        a.clear_word = multi ? s.px_keys[x] + (size_t)slots * kt : nullptr;   // the verify below may raise it
+        a.clear_word = multi ? s.px_keys[x] + (size_t)slots * kt : nullptr;   // the verify of this block may raise it
         a.ctr = s.ctr + (cs == s.stream ? 0 : kCtrStride);
         a.sqrt_d = sqrtf((float)d) * (1.0f + 0x1p-20f);
         a.full_lists = h->full_lists ? 1 : 0;
@@ -1228,49 +1294,37 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
           a.eps_a = kScreen8EpsA;
           a.eps_b = kScreen8EpsB;
         }
-        if (fuse) {   // the verify's arguments (below) on the screen's launch
-          a.fuse = 1;
+        if (carrying) {   // the previous screened block's verify in workgroups [0, 32)
+          const PendVerify& pv = h->pend;
+          verify_args(h, s, pv, s.pend_nlists, &a);
+          a.carry = 1;
           a.vcorpus = (const char*)s.corpus;
-          a.vsync = (uint64_t*)(s.ctr + (2 + bsi) * kCtrStride);
-          a.vbase = s.vbase[bsi];
-          s.vbase[bsi] += (uint64_t)sgrid;
-          a.vin = candp;
-          a.nlists = sgrid;
-          a.k_out = k;
-          a.out_keys = s.px_keys[x];
-          a.flag = s.px_keys[x] + (size_t)slots * kt;
-          a.count = s.scount;
-          a.seq = seq;
-          a.force_incomplete = h->kernel == RR_KERNEL_SCREEN_FALLBACK;
-          a.wide_verify = h->wide_verify;
-          a.wide_count = s.wcount;
+          a.vqueries = s.qbuf[pv.qpar] + (size_t)pv.q0 * d;
+          a.vb = pv.bb;
+          a.vseq = pv.seq;
         }
         HIP_TRY(rr::launch_sk_args(s8 ? rr::KDT_SCREEN8 : s16 ? rr::KDT_SCREEN16 : rr::KDT_SCREEN, h->metric, kt, 0,
                                    sgrid, rr::kQSlots, a, cs));
       }
       if (timed) HIP_TRY(hipEventRecord(e1, cs));
-      // results written in place (no exchange): this verify follows the previous one when that ran on the other
-      // stream (the same rows of the result buffer)
-      if (two && !multi && s.last_vsi >= 0 && s.last_vsi != bsi)
-        HIP_TRY(hipStreamWaitEvent(vs, s.ev_q[s.last_vq][s.last_vsi], 0));
-      if (s.rows() > 0 && !h->ab_no_verify && !fuse) {
-        rr::SkArgs v = sk_base(h, s, qb, bb);
-        v.vin = candp;
-        v.nlists = sgrid;
-        v.k_out = k;
-        v.out_scores = multi ? nullptr : osc;
-        v.out_idx = multi ? nullptr : oix;
-        v.out_keys = multi ? s.px_keys[x] : nullptr;
-        // the block's flag word: the result buffer's head, or (exchange) the word after this shard's keys
-        v.flag = multi ? s.px_keys[x] + (size_t)slots * kt : (uint64_t*)s.out_base;
-        v.count = s.scount;
-        v.seq = seq;
-        v.force_incomplete = h->kernel == RR_KERNEL_SCREEN_FALLBACK;
-        v.wide_verify = h->wide_verify;
-        v.wide_count = s.wcount;
-        HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 1, rr::kQSlots, rr::kQSlots, v, vs));
-      } else if (!h->ab_no_verify && !fuse) {   // a shard without rows contributes empty lists and no flag
-        HIP_TRY(hipMemsetAsync(s.px_keys[x], 0, ((size_t)slots * kt + 1) * 8, vs));
+      if (cm) {
+        s.pend_nlists_next = sgrid;   // this block's lists, verified by the next screened launch or a flush
+      } else {
+        // results written in place (no exchange): this verify follows the previous one when that ran on the other
+        // stream (the same rows of the result buffer)
+        if (two && !multi && s.last_vsi >= 0 && s.last_vsi != bsi)
+          HIP_TRY(hipStreamWaitEvent(vs, s.ev_q[s.last_vq][s.last_vsi], 0));
+        if (s.rows() > 0 && !h->ab_no_verify) {
+          rr::SkArgs v = sk_base(h, s, qb, bb);
+          PendVerify me;
+          me.q0 = q0, me.bb = bb, me.k = k, me.kt = kt, me.slots = slots, me.x = x, me.p = p, me.seq = seq;
+          me.force = h->kernel == RR_KERNEL_SCREEN_FALLBACK;
+          verify_args(h, s, me, sgrid, &v);
+          v.seq = seq;
+          HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 1, rr::kQSlots, rr::kQSlots, v, vs));
+        } else if (!h->ab_no_verify) {   // a shard without rows contributes empty lists and no flag
+          HIP_TRY(hipMemsetAsync(s.px_keys[x], 0, ((size_t)slots * kt + 1) * 8, vs));
+        }
       }
       if (h->host_prof) {
         h->hp.ns[3] += now_ns() - tl;
@@ -1403,6 +1457,21 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       if (!multi) HIP_TRY(rr::launch_decode(s.shard_keys, bb, k, osc, oix, s.stream));
     }
   }
+  if (cm) {   // the carried block's exchange (its keys are written by this launch), then this block is pending
+    if (carrying && multi) {
+      const PendVerify& pv = h->pend;
+      if (int rc = enqueue_exchange_px(h, pv.p, pv.x, pv.q0, pv.bb, pv.k, pv.kt, pv.slots, true)) return rc;
+    }
+    PendVerify& me = h->pend;
+    me.on = true;
+    me.q0 = q0, me.bb = bb, me.k = k, me.kt = kt, me.slots = slots, me.x = x, me.p = p, me.seq = seq;
+    me.qpar = h->qpar;
+    me.force = h->kernel == RR_KERNEL_SCREEN_FALLBACK;
+    for (Shard& s : h->shards) s.pend_nlists = s.pend_nlists_next;
+    h->parity ^= 1;
+    if (multi) h->xslot = (x + 1) % h->xslots;
+    return RR_OK;
+  }
   if (!multi) {
     if (scr) h->parity ^= 1;
     return RR_OK;
@@ -1472,6 +1541,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
 // after everything on cstream2, and later cstream2 blocks follow it.
 int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
   const bool scr = screened(h, k, slots);
+  if (!scr)   // a pending carried verify reads the candidate lists and writes results this block may rewrite
+    if (int rc = flush_verify(h)) return rc;
   if (!scr)
     for (Shard& s : h->shards) {
       HIP_TRY(hipSetDevice(s.dev));
@@ -1594,7 +1665,7 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   if (const char* e = getenv("RR_WIDE_VERIFY")) h->wide_verify = atoi(e) ? 1 : 0;   // (A/B)
   if (const char* e = getenv("RR_AB_NO_VERIFY")) h->ab_no_verify = atoi(e) != 0;    // (A/B only: invalid results)
   if (const char* e = getenv("RR_HOST_PROF")) h->host_prof = atoi(e) != 0;
-  if (const char* e = getenv("RR_FUSED_VERIFY")) h->fuse_verify = atoi(e) != 0;   // (A/B)
+  if (const char* e = getenv("RR_CARRY_VERIFY")) h->carry = atoi(e) != 0;   // (A/B: 0 = a verify launch per block)
   if (const char* e = getenv("RR_SCREEN_I8")) h->screen_i8 = atoi(e) != 0;         // (A/B: 0 = the f16 copy only)
   if (const char* e = getenv("RR_SCREEN_I8_MIN_ROWS")) h->i8_min_rows = atoll(e);
   if (const char* e = getenv("RR_SCREEN_CT8")) h->ct8 = atoi(e);
@@ -1762,12 +1833,16 @@ int rr_update_rows(rr_handle* h, const float* host_rows, const int64_t* row_idx,
   for (int64_t i = 0; i < n_rows; ++i)
     if (row_idx[i] < 0 || row_idx[i] >= h->n_total)
       return fail(RR_E_INVALID, "row index %lld outside [0, %lld)", (long long)row_idx[i], (long long)h->n_total);
-  // the screen reads fp32 rows as f16 (|x| < 2^15): decided over every given row, on the host — every rank of a world
-  // passes the same rows, so the ranks agree without a collective
+  // the screen reads fp32 rows as f16 (|x| < 2^15): decided over every given row, on the host, then agreed across the
+  // ranks (an RCCL min: a rank given other rows than its peers must not keep screening while they stop — the list
+  // width sizes the all-gather)
   bool in_range = true;
   for (int64_t e = 0; e < n_rows * (int64_t)d && in_range; ++e) in_range = fabsf(host_rows[e]) < 32768.0f;   // NaN: no
   // the last search may still be re-run from the rows about to change: settle it, and let every stream drain
   if (int rc = rr_synchronize(h)) return rc;
+  int agreed = in_range ? 1 : 0;
+  if (int rc = agree_min(h, &agreed, 1, "the ranks' row-update range agreement", 10)) return rc;
+  in_range = agreed != 0;
   const size_t eb = elem_bytes(h->dtype);
   const bool norms = (h->metric == RR_METRIC_COSINE || kdt_of(h->dtype) == rr::KDT_F32_MFMA) &&
                      kdt_of(h->dtype) != rr::KDT_F32_SPLIT;   // (the split computes its own)
@@ -1908,7 +1983,8 @@ static int search_staged_body(rr_handle* h, int32_t k) {
   h->last_narrow = screened(h, k, slots) && narrow_lists(h, k);
   h->last_full = h->full_lists;
   h->last_wide = h->screen_wide;
-  h->last_i8 = i8_active(h);
+  // judged by the int8 rule only when every shard (of every rank) screened the int8 copy: rank-consistent
+  h->last_i8 = i8_active(h) && h->i8_all;
   h->last_blocks = screened(h, k, slots) ? (b + slots - 1) / slots : 0;
   h->last_seq0 = h->screen_seq + 1;
   h->last_settled = !h->last_screened;
@@ -1942,6 +2018,7 @@ int rr_last_shape(const rr_handle* h, int32_t* b, int32_t* k) {
 namespace {
 
 int sync_streams(rr_handle* h) {
+  if (int rc = flush_verify(h)) return rc;   // (a carried verify still pending: its block's results are owed)
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
     for (hipStream_t st : {s.stream, s.xstream, s.xstream2, s.cstream2})
@@ -2080,6 +2157,7 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
   h->qpar = nq;
   h->cur_b = b;
   if (int rc = rr_search_staged(h, k)) return rc;
+  if (int rc = flush_verify(h)) return rc;   // (the copy below reads this search's results)
   // results come back on the stream that wrote them last: the exchange stream when there is an exchange
   // (the serial k > 32 exchange also orders it after itself), else the compute stream
   Shard& s0 = h->shards[0];
@@ -2137,6 +2215,9 @@ int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx) {
   uint64_t flag = 0;
   memcpy(&flag, a.pin + res_off, sizeof flag);
   if (a.screened) observe_settled(h, a.blocks, a.narrow, a.full, a.wide, a.i8, flag >= (uint64_t)a.seq0);
+  // this ticket's search, if it is still the handle's last one, is settled here: a later rr_synchronize /
+  // rr_fetch_results must neither observe it again nor re-run it a second time
+  if (a.screened && h->last_screened && !h->last_settled && h->last_seq0 == a.seq0) h->last_settled = true;
   if (a.screened && flag >= (uint64_t)a.seq0) {
     // a block needed the exact pass: this batch again, exactly (every rank of an exchange sees the same
     // flag here, so all re-run it together). A batch staged with rr_set_queries before this wait stays the
@@ -2246,6 +2327,19 @@ int rr_set_compute_streams(rr_handle* h, int32_t n, int32_t* in_use) {
     h->streams = n;
   }
   if (in_use) *in_use = h->shards.empty() ? 1 : (two_streams(h, h->shards[0]) ? 2 : 1);
+  return RR_OK;
+}
+
+int rr_set_carry_verify(rr_handle* h, int32_t on, int32_t* in_use) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  if (h->failed) return failed_handle();
+  if (on < -1 || on > 1) return fail(RR_E_INVALID, "carry verify %d (-1 = as is, 0, 1)", on);
+  if (on >= 0 && (on != 0) != (h->carry != 0)) {
+    if (int rc = rr_synchronize(h)) return rc;   // (flushes a pending verify)
+    for (Shard& s : h->shards) s.last_vsi = -1;
+    h->carry = on;
+  }
+  if (in_use) *in_use = h->carry ? 1 : 0;
   return RR_OK;
 }
 

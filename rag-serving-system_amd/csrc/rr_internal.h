@@ -84,14 +84,15 @@ struct SkArgs {
   uint64_t* floors;
   // MODE 0, KT 32, 32 slots: every key instead of lists, all_keys[q * n + row] for q < b (full-sort path)
   uint64_t* all_keys;
-  // Fused verify (MODE 0, the f16-copy screen on the dynamic schedule, KT <= 16): the screen's last 32 workgroups to
-  // finish verify one query slot each (the MODE 1 fields above: vin = out, nlists = grid, k_out, out_keys, flag,
-  // count, seq, force_incomplete, wide_verify, wide_count) over the fp32 rows vcorpus. vsync: the compute stream's
-  // count of screen workgroups that finished (never reset); vbase: its value when this launch began.
-  int fuse;
+  // Carried verify (MODE 0, the f16- or int8-copy screen on the dynamic schedule, KT <= 16; rr_sk.hip carry_verify):
+  // workgroups [0, 32) of the launch first verify one query slot each of the PREVIOUS screened block (the MODE 1 fields
+  // above: vin = that block's lists, nlists = its screen's grid, k_out, out_scores / out_idx / out_keys, flag, count,
+  // force_incomplete, wide_verify, wide_count), over the fp32 rows vcorpus with that block's queries vqueries (vb of
+  // them) and sequence number vseq, then join this screen on the dynamic counter.
+  int carry;
   const char* vcorpus;
-  uint64_t* vsync;
-  uint64_t vbase;
+  const float* vqueries;
+  int vb, vseq;
   // int8 screen (KDT_SCREEN8): corpus = the int8 copy, read as n = ceil(rows8 / 2) kernel rows of two corpus rows each;
   // sx8 / e8 [rows8] the rows' scales and error norms; q8 [2][32][d] the queries' int8 pieces and q8s [4][32] their
   // scalars (launch_q8_prep)

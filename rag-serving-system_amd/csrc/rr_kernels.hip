@@ -799,11 +799,13 @@ __global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict_
 }
 
 // fp32 rows (natural element order) -> the int8 screen copy (rr_sk.hip DT 8), one wave per row:
-//   sx = max|x| / 127 (0 for a zero row), x8 = clamp(rint(x / sx), -127, 127) — any x8 is valid, the bound uses e —
-//   e >= |x - sx x8|_2 (real arithmetic): the fp32 residuals' norm, each residual within 2^-24 (|x| + 2 |r|) of the
-//   real one (the product sx x8 and the subtraction round once each), so + 2^-22 max|x| sqrt(d) covers
-//   2^-24 (|x|_2 + sx sqrt(d)); the sum of squares (<= d / 64 + 6 roundings a chain) and the sqrt within 2^-14,
-//   covered by the 2^-12 relative bump.
+//   sx = max|x| / 127 (0 for a zero row), x8 = clamp(rint(t), -127, 127) with t = x / sx — any x8 is valid, the bound
+//   uses e — and e >= |x - sx x8|_2 (real arithmetic), computed in the scale's units so that no square underflows:
+//   t - x8 is exact, and x / sx - t is within 2^-24 |t| (IEEE division; 2^-149 if t is subnormal), so
+//   |x - sx x8|_2 <= sx |t - x8|_2 + 2^-24 (1 + 2^-23) |x|_2 + sx sqrt(d) 2^-149, |x|_2 <= sqrt(d) max|x|. The sum of
+//   squares of t - x8 (in [-1/2, 1/2]: <= d / 4 + 6 roundings a chain, squares below 2^-126 add <= 2^-116 in all) and
+//   the sqrt and product within 2^-14, covered by the 2^-12 relative bump; 2^-22 sqrt(d) max|x| covers the division
+//   term 4x over, and 2^-140 what the products round away when max|x| is itself near fp32's underflow.
 __global__ __launch_bounds__(256) void f32_to_i8_kernel(const float* __restrict__ in, int64_t n, int d,
                                                         uint32_t* __restrict__ out, float* __restrict__ sx,
                                                         float* __restrict__ e8) {
@@ -826,9 +828,9 @@ __global__ __launch_bounds__(256) void f32_to_i8_kernel(const float* __restrict_
     uint32_t packed = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float x = v[j];
-      const float q = s > 0.f ? fminf(fmaxf(rintf(x / s), -127.0f), 127.0f) : 0.f;
-      const float r = x - s * q;
+      const float t = s > 0.f ? v[j] / s : 0.f;
+      const float q = fminf(fmaxf(rintf(t), -127.0f), 127.0f);
+      const float r = t - q;   // exact
       ss = fmaf(r, r, ss);
       packed |= ((uint32_t)(int)q & 0xFFu) << (8 * j);
     }
@@ -838,16 +840,18 @@ __global__ __launch_bounds__(256) void f32_to_i8_kernel(const float* __restrict_
   for (int off = 32; off >= 1; off >>= 1) ss += __shfl_xor(ss, off, 64);
   if (lane == 0) {
     sx[row] = s;
-    e8[row] = fmaf(sqrtf(ss), 1.0f + 0x1p-12f, m * sqrtf((float)d) * 0x1p-22f);
+    e8[row] = fmaf(s * sqrtf(ss), 1.0f + 0x1p-12f, fmaf(m, sqrtf((float)d) * 0x1p-22f, 0x1p-140f));
   }
 }
 
-// The int8 screen's query pieces, one wave per query slot: s = max|q| / 127, p1 = clamp(rint(q / s)), p2 =
-// clamp(rint((q / s - p1) * 64)) — q ~ s (p1 + p2 / 64), the MFMAs' sum being x8 . (64 p1 + p2) — and eq >= the
-// residual's norm (real arithmetic; the same accounting as f32_to_i8_kernel). |q| and sum|q| in fp32 (the bound
-// bumps for their summation order). Slots >= b: zero pieces and scalars. One 64-lane workgroup per slot: it runs
-// beside the other stream's screen. (Quantising in the screen itself instead — every workgroup redoing all 32
-// queries, two L2 passes — measured 8-13 us longer per launch than this launch: profiles/r04/ab/int8/.)
+// The int8 screen's query pieces, one wave per query slot: s = max|q| / 127, t = q / s, p1 = clamp(rint(t)), p2 =
+// clamp(rint((t - p1) * 64)) — q ~ s (p1 + p2 / 64), the MFMAs' sum being x8 . (64 p1 + p2) — and eq >= the
+// residual's norm (real arithmetic), in the scale's units as f32_to_i8_kernel: t - p1 - p2 / 64 is exact (each step
+// by Sterbenz), so |q - s (p1 + p2 / 64)|_2 <= s |t - p1 - p2/64|_2 (x 1 + 2^-12) + 2^-21 sqrt(d) max|q| + 2^-140.
+// |q| and sum|q| in fp32 (the bound bumps for their summation order). Slots >= b: zero pieces and scalars. One 64-lane
+// workgroup per slot: it runs beside the other stream's screen. (Quantising in the screen itself instead — every
+// workgroup redoing all 32 queries, two L2 passes — measured 8-13 us longer per launch than this launch:
+// profiles/r04/ab/int8/.)
 __global__ __launch_bounds__(64) void q8_prep_kernel(const float* __restrict__ q, int b, int d,
                                                      int8_t* __restrict__ q8, float* __restrict__ q8s) {
   const int slot = blockIdx.x, lane = threadIdx.x;
@@ -885,16 +889,16 @@ __global__ __launch_bounds__(64) void q8_prep_kernel(const float* __restrict__ q
     uint32_t w1 = 0, w2 = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float x = v[j];
-      float a = 0.f, cc = 0.f;
+      float a = 0.f, cc = 0.f, r = 0.f;
       if (s > 0.f) {
-        const float t = x / s;
+        const float t = v[j] / s;
         a = fminf(fmaxf(rintf(t), -127.0f), 127.0f);
-        cc = fminf(fmaxf(rintf((t - a) * 64.0f), -127.0f), 127.0f);
+        const float ta = t - a;   // exact
+        cc = fminf(fmaxf(rintf(ta * 64.0f), -127.0f), 127.0f);
+        r = ta - cc * 0x1p-6f;    // exact
       }
       w1 |= ((uint32_t)(int)a & 0xFFu) << (8 * j);
       w2 |= ((uint32_t)(int)cc & 0xFFu) << (8 * j);
-      const float r = x - s * (a * 64.0f + cc) * 0x1p-6f;
       se = fmaf(r, r, se);
     }
     *(uint32_t*)(p1 + 4 * c) = w1;
@@ -906,7 +910,7 @@ __global__ __launch_bounds__(64) void q8_prep_kernel(const float* __restrict__ q
     q8s[slot] = sqrtf(s2);
     q8s[kQSlots + slot] = s1 * (1.0f + 0x1p-18f);
     q8s[2 * kQSlots + slot] = s * 0x1p-6f;
-    q8s[3 * kQSlots + slot] = fmaf(sqrtf(se), 1.0f + 0x1p-12f, m * sqrtf((float)d) * 0x1p-21f);
+    q8s[3 * kQSlots + slot] = fmaf(s * sqrtf(se), 1.0f + 0x1p-12f, fmaf(m, sqrtf((float)d) * 0x1p-21f, 0x1p-140f));
   }
 }
 

@@ -329,7 +329,7 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
   // the floors' and the list bounds' maxima: a wave-wide max, one LDS word per wave (not one LDS atomic per list on a
   // single address: 2 x 256 of those serialised to ~7 us)
   const uint64_t fwv = wave_max_u64(fl), twv = wave_max_u64(tl);
-  if (lane == 0) {
+  if (lane == 0 && wv < kWaves) {   // (a carried verify's 9th wave, the screen's scheduler, only passes the barriers)
     fw[wv] = fwv;
     tw[wv] = twv;
   }
@@ -357,7 +357,7 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
     const int g8 = nlp / 16 * 4;       // the first half's end, in 16-byte units (multiple of 4)
     int rank = 0;
     if (hh < nl && me != 0) rank = half ? count_above(me, g8, nlp / 2) : count_above(me, 0, g8);
-    if (half) part[hh] = rank;
+    if (half == 1) part[hh] = rank;
     __syncthreads();
     if (!half && hh < nl && me != 0 && rank + part[hh] == KT - 1) hs[0] = me;
   } else if (tid < nl && tk.v[0] != 0) {
@@ -410,48 +410,52 @@ __device__ __forceinline__ uint32_t wide_bar(uint64_t ek, uint64_t tb) {
   return ek != 0 && e > t ? e : t + 1;
 }
 
-// ---- Fused verify ---------------------------------------------------------------------------------------------
-// The f16-copy screen on the dynamic schedule (DT 7, SCHED 1, KT <= 16) can verify its own lists (SkArgs::fuse): the
-// last 32 workgroups to finish the screen wait until every workgroup has published its lists, then each verifies one
-// query slot — exactly the MODE 1 verify (same candidates, same exact DT 3 arithmetic: K split over the 8 waves,
-// MFMA order, wave order of the partial sums, the cosine quotient and clip; the same completeness proof and wide
-// phase), so results are bit-identical. No kernel boundary between the screen and its verify, and no CUs held back
-// for a separate verify launch. Registers: the 9-wave screen's budget (168 VGPRs), so the verify here keeps no
-// per-lane lists: a tile's 32 exact keys go through LDS and the top-KT is kept by rank selection.
-// LDS (all free after the screen): [0, 16 KiB) the list merge's scratch, [16, 20 KiB) the query, [20 KiB, ring end)
-// the wide phase's rows; the partial block of the screen (red) for the K-partials; the MODE 1 scalars block.
-constexpr int kFvQueryOff = 16384;
-constexpr int kFvWideOff = 20480;
-constexpr int kFvWideCap = (int)((ring_bytes(2) - kFvWideOff) / 4);
+// ---- Carried verify ------------------------------------------------------------------------------------------
+// A screen on the dynamic schedule (DT 7 / DT 8, SCHED 1, KT <= 16) can carry the PREVIOUS screened block's verify
+// (SkArgs::carry): workgroups [0, 32) verify one query slot each of that block — whose screen ended with the previous
+// launch, so its lists are complete — and then join this block's screen, taking chunks from the dynamic counter; the
+// other workgroups screen from the start. One launch per search block instead of a screen and a separate verify, and
+// the 32 verifying CUs stream corpus rows as soon as they are done. The verify is exactly MODE 1's (same candidates,
+// same exact DT 3 arithmetic: K split over the 8 waves, MFMA order, wave order of the partial sums, the cosine
+// quotient and clip; the same completeness proof and wide phase), so results are bit-identical. Registers: the
+// 9-wave screen's budget (168 VGPRs), so this verify keeps no per-lane lists — a tile's 32 exact keys go through LDS
+// and the top-KT is kept by rank selection — and splits the query from LDS per tile. The 9th wave (the screen's
+// scheduler) passes every barrier and does no work here.
+// LDS (free before the screen starts): [0, 16 KiB) the list merge's scratch, [16, 20 KiB) the query, [20 KiB, ring
+// end) the wide phase's rows; the screen's partial block (red) for the K-partials; the MODE 1 scalars block.
+constexpr int kCvQueryOff = 16384;
+constexpr int kCvWideOff = 20480;
+constexpr int kCvWideCap = (int)((ring_bytes(2) - kCvWideOff) / 4);
 
 template <int NSV, int KT, bool COS>
-__device__ __forceinline__ void fused_verify(const SkArgs& a, const int vq, char* smem, float* red, float* qinfo,
+__device__ __forceinline__ void carry_verify(const SkArgs& a, const int vq, char* smem, float* red, float* qinfo,
                                              uint64_t* akeys, int* grow, float* gnorm, int* gvalid, uint64_t* xk,
-                                             uint64_t* vfloor, uint64_t* vtail, int* vstate, uint64_t* tkeys,
-                                             const bool lists_ok) {
+                                             uint64_t* vfloor, uint64_t* vtail, int* vstate, uint64_t* tkeys) {
   constexpr int QS = 32;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
+  const bool sw = w < kWaves;   // a streaming wave (not the scheduler)
   const int d = a.d;
   const uint32_t idx_base = a.idx_base;
   const char* __restrict__ vcorpus = a.vcorpus;
   const int row_bytes = d * 4;
   constexpr int KSV = NSV * kSlabRowBytes;   // bytes of a row per wave (fp32 rows)
   const int p0 = w * (KSV / 16);
-  float* qv = (float*)(smem + kFvQueryOff);
-  int* wl = (int*)(smem + kFvWideOff);
-  if (vq >= a.b) {   // padding slot: keep the exchange buffer uniform
+  float* qv = (float*)(smem + kCvQueryOff);
+  int* wl = (int*)(smem + kCvWideOff);
+  if (vq >= a.vb) {   // padding slot: keep the exchange buffer uniform
     if (a.out_keys && tid < KT) a.out_keys[(size_t)vq * KT + tid] = 0;
     return;
   }
   // the query into LDS; |q| and max |q| by wave 0 exactly as the exact pass computes them
-  for (int e = 4 * tid; e < d; e += 4 * kThreads) *(f32x4*)(qv + e) = *(const f32x4*)(a.queries + (size_t)vq * d + e);
+  const float* __restrict__ vqs = a.vqueries;
+  for (int e = 4 * tid; e < d; e += 4 * kThreads) *(f32x4*)(qv + e) = *(const f32x4*)(vqs + (size_t)vq * d + e);
   if (w == 0) {
     const int nc = d >> 2;
     f32x4 v[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int cc = lane + 64 * c;
-      v[c] = zero_unless(((const f32x4*)a.queries)[(size_t)vq * nc + (cc < nc ? cc : 0)], opaque_mask(cc < nc));
+      v[c] = zero_unless(((const f32x4*)vqs)[(size_t)vq * nc + (cc < nc ? cc : 0)], opaque_mask(cc < nc));
     }
     float ss = 0.f, m = 0.f;
 #pragma unroll
@@ -489,40 +493,42 @@ __device__ __forceinline__ void fused_verify(const SkArgs& a, const int vq, char
 
   // exact keys of the 32 rows grow[] (gvalid: 0 -> key 0) into tkeys[]: the DT 3 tile of the full pass with query vq
   auto score_tile = [&]() {
-    const char* src = vcorpus + (int64_t)grow[r] * row_bytes + (size_t)w * KSV;
-    f32x4 vr[NSV][4];
+    if (sw) {
+      const char* src = vcorpus + (int64_t)grow[r] * row_bytes + (size_t)w * KSV;
+      f32x4 vr[NSV][4];
 #pragma unroll
-    for (int j = 0; j < NSV; ++j)
+      for (int j = 0; j < NSV; ++j)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        vr[j][i] = *(const f32x4*)(src + j * kSlabRowBytes + ((4 * (i >> 1) + 2 * h + (i & 1)) << 4));
-    f32x16 acc;
+        for (int i = 0; i < 4; ++i)
+          vr[j][i] = *(const f32x4*)(src + j * kSlabRowBytes + ((4 * (i >> 1) + 2 * h + (i & 1)) << 4));
+      f32x16 acc;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 #pragma unroll
-    for (int j = 0; j < NSV; ++j)
+      for (int j = 0; j < NSV; ++j)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const float x[8] = {vr[j][2 * t].x, vr[j][2 * t].y, vr[j][2 * t].z, vr[j][2 * t].w,
-                            vr[j][2 * t + 1].x, vr[j][2 * t + 1].y, vr[j][2 * t + 1].z, vr[j][2 * t + 1].w};
-        bf16x8 b0, b1, b2, c0, c1, c2;
-        split3(x, b0, b1, b2);
-        const f32x4 qa = *(const f32x4*)(qv + 4 * inv_pair(p0 + 8 * j + 4 * t + 2 * h));
-        const f32x4 qb = *(const f32x4*)(qv + 4 * inv_pair(p0 + 8 * j + 4 * t + 2 * h + 1));
-        const float qx[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
-        split3(qx, c0, c1, c2);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c0, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c1, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c0, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c1, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c2, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, c0, acc, 0, 0, 0);
+        for (int t = 0; t < 2; ++t) {
+          const float x[8] = {vr[j][2 * t].x, vr[j][2 * t].y, vr[j][2 * t].z, vr[j][2 * t].w,
+                              vr[j][2 * t + 1].x, vr[j][2 * t + 1].y, vr[j][2 * t + 1].z, vr[j][2 * t + 1].w};
+          bf16x8 b0, b1, b2, c0, c1, c2;
+          split3(x, b0, b1, b2);
+          const f32x4 qa = *(const f32x4*)(qv + 4 * inv_pair(p0 + 8 * j + 4 * t + 2 * h));
+          const f32x4 qb = *(const f32x4*)(qv + 4 * inv_pair(p0 + 8 * j + 4 * t + 2 * h + 1));
+          const float qx[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+          split3(qx, c0, c1, c2);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c0, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c1, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c0, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c1, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c2, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, c0, acc, 0, 0, 0);
+        }
+      // every column holds query vq: column 0's partials (lanes 0 and 32: docs 8a + 4h + i), summed in wave order
+      if (r == 0) {
+#pragma unroll
+        for (int a4 = 0; a4 < 4; ++a4)
+          *(f32x4*)(red + w * 32 + 8 * a4 + 4 * h) = (f32x4){acc[4 * a4], acc[4 * a4 + 1], acc[4 * a4 + 2], acc[4 * a4 + 3]};
       }
-    // every column holds query vq: column 0's partials (lanes 0 and 32: docs 8a + 4h + i), summed in wave order
-    if (r == 0) {
-#pragma unroll
-      for (int a4 = 0; a4 < 4; ++a4)
-        *(f32x4*)(red + w * 32 + 8 * a4 + 4 * h) = (f32x4){acc[4 * a4], acc[4 * a4 + 1], acc[4 * a4 + 2], acc[4 * a4 + 3]};
     }
     __syncthreads();
     if (tid < 32) {
@@ -558,9 +564,9 @@ __device__ __forceinline__ void fused_verify(const SkArgs& a, const int vq, char
     __syncthreads();
   };
   auto finish = [&](bool complete) {   // (thread 0)
-    complete = complete && lists_ok && qinfo[QS + vq] < 32768.0f && !a.force_incomplete;
+    complete = complete && qinfo[QS + vq] < 32768.0f && !a.force_incomplete;
     if (!complete)
-      if (__hip_atomic_fetch_max(a.flag, (uint64_t)a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint64_t)a.seq)
+      if (__hip_atomic_fetch_max(a.flag, (uint64_t)a.vseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint64_t)a.vseq)
         __hip_atomic_fetch_add(a.count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (vq == 0) __hip_atomic_fetch_add(a.count + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (a.out_keys)
@@ -580,7 +586,7 @@ __device__ __forceinline__ void fused_verify(const SkArgs& a, const int vq, char
     const uint64_t ek = xk[a.k_out - 1];
     const bool complete = ukt == 0 || (ek != 0 && (uint32_t)(ek >> 32) > (uint32_t)(ukt >> 32));
     const uint64_t tb = *vtail;
-    const bool wide = !complete && lists_ok && a.wide_verify && !a.force_incomplete && qinfo[QS + vq] < 32768.0f &&
+    const bool wide = !complete && a.wide_verify && !a.force_incomplete && qinfo[QS + vq] < 32768.0f &&
                       ((uint32_t)(ek >> 32) > (uint32_t)(tb >> 32) ||
                        (uint32_t)(akeys[a.k_out - 1] >> 32) > (uint32_t)(tb >> 32));
     vstate[0] = wide ? 1 : 0;
@@ -601,12 +607,12 @@ __device__ __forceinline__ void fused_verify(const SkArgs& a, const int vq, char
     if (c) {
       const int pos = atomicAdd(&vstate[1], c);
       for (int i = 0; i < c; ++i)
-        if (pos + i < kFvWideCap) wl[pos + i] = (int)((int64_t)(0xFFFFFFFFu - (uint32_t)src[i]) - idx_base);
+        if (pos + i < kCvWideCap) wl[pos + i] = (int)((int64_t)(0xFFFFFFFFu - (uint32_t)src[i]) - idx_base);
     }
   }
   __syncthreads();
   const int nr = vstate[1];
-  if (nr > kFvWideCap) {
+  if (nr > kCvWideCap) {
     if (tid == 0) finish(false);
     return;
   }
@@ -698,6 +704,18 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   uint64_t* vfloor = xk + KT;   // MODE 1: the largest floor of the screen's lists (see KL)
   uint64_t* vtail = vfloor + 1; // MODE 1: the largest bound of any single list, max(KT-th key, floor) (wide verify)
   int* vstate = (int*)(vtail + 1);   // MODE 1: [0] what the leader decided after the first check, [1] |R|, [4] R's bar
+  // ---- carried verify (see carry_verify): workgroups [0, 32) verify the previous block's query slots first, then
+  // join this screen on the dynamic counter (NJ of them: no static first chunk)
+  constexpr bool CARRY = MODE == 0 && SCHED == 1 && QH == 1 && (DT == 7 || DT == 8) && KT <= 16;
+  const int NJ = CARRY && a.carry ? kQSlots : 0;   // joiners
+  const bool joiner = (int)blockIdx.x < NJ;
+  if constexpr (CARRY) {
+    if (joiner) {
+      carry_verify<2 * NS, KT, COS>(a, (int)blockIdx.x, smem, red, qinfo, akeys, grow, gnorm, gvalid, xk, vfloor, vtail,
+                                    vstate, vW);
+      __syncthreads();   // (the verify's LDS is the screen's from here)
+    }
+  }
   // MODE 1 reads its 32 gathered rows straight into registers (all loads issued at once: one latency), the
   // exact fragments the LDS image would give: lane (r, h) takes 16-byte units 4(i>>1) + 2h + (i&1) of slab j
   f32x4 vrow[MODE == 1 ? NS : 1][4];
@@ -716,7 +734,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // the int8 screen: a.ct8 tiles (of 64 corpus rows) per chunk — 2 on small shards, where a 4-tile chunk is a large
   // share of a workgroup's work and the last ones leave a tail (profiles/r04/ab/ab_ct8.txt), else 4
   const int CT = DT == 8 && a.ct8 > 0 ? a.ct8 : CT0;
-  const int64_t G = gridDim.x, g = blockIdx.x;
+  // the statically scheduled workgroups: G of them, workgroup g's first chunk is chunk g (joiners: g < 0)
+  const int64_t G = (int64_t)gridDim.x - NJ, g = (int64_t)blockIdx.x - NJ;
   const int64_t T = (n + 31) / 32, C = (T + CT - 1) / CT;
 
   // LDS-DMA lane mapping: instruction i of a slab covers tile rows 8i + lane/8, 16-byte column
@@ -778,9 +797,20 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       // The scheduler wave (a 9th wave: no corpus, no query, no inline-asm loads, so hipcc's own waits around
       // its atomic drain nothing else). Per chunk it takes the next free chunk from the counter and publishes
       // it in nxt[] before the chunk's first reduction barrier; the streaming waves read it at the chunk's last
-      // step. It passes exactly the barriers the streaming waves pass: one after the query scalars, one per tile.
-      __syncthreads();
+      // step. It passes exactly the barriers the streaming waves pass: (a joiner's first-chunk barrier,) one after the
+      // query scalars, one per tile.
       int64_t ck = g;
+      if (joiner) {   // a joiner's first chunk from the counter, published to the streaming waves (nxt[2])
+        if (lane == 0) {
+          const uint32_t old = __hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const int64_t nc = G + (int64_t)old;
+          nxt[2] = (int)(nc < C ? nc : C);
+          if ((int64_t)old == C - 2 + NJ) __hip_atomic_store(a.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        ck = nxt[2];
+      }
+      __syncthreads();
       int cp = 0;
       while (ck < C) {
         const int tic = (int)(C - ck == 1 ? T - ck * CT : CT);
@@ -788,8 +818,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           const uint32_t old = __hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           const int64_t nc = G + (int64_t)old;
           nxt[cp] = (int)(nc < C ? nc : C);
-          // the launch's last dequeue resets the counter for the next launch on this stream
-          if ((int64_t)old == C - 2) __hip_atomic_store(a.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // the launch's last dequeue resets the counter for the next launch on this stream: every chunk but the last
+          // asks once, and so does every joiner for its first chunk — C - 1 + NJ dequeues per launch
+          if ((int64_t)old == C - 2 + NJ) __hip_atomic_store(a.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         for (int t = 0; t < tic; ++t) lds_barrier();
         if (ck == C - 1) break;
@@ -811,7 +842,14 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #endif
   constexpr int LA = NS >= 2 ? (QH == 1 ? RR_SK_LOOKAHEAD : RR_SK_LA64) : 1;   // (64 slots: measured faster with 1)
   int pend = 0;   // LA 2: vector-memory ops this wave issued after the slab it waits for next
-  int64_t chunk = g, base = chunk * CT * 32;
+  int64_t chunk = g;
+  if constexpr (CARRY) {
+    if (joiner) {   // (the scheduler wave published this joiner's first chunk)
+      __syncthreads();
+      chunk = nxt[2];
+    }
+  }
+  int64_t base = chunk * CT * 32;
   if constexpr (MODE == 0) {
     if (chunk < C) {   // prologue: the first tile's factors and slab 0 (and 1)
       if (FX && w == 0) issue_factors(base, 0);
@@ -819,31 +857,6 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       if constexpr (LA == 2) {
         issue(base, 1, 1);
         pend = 4;
-      }
-#ifndef RR_SK_WARM
-#define RR_SK_WARM 0   // A/B only: 3 measured 4-5 % slower at 125k rows (profiles/r03/c/ab_warm_rejected.txt)
-#endif
-      // Start-up warming (A/B): the next RR_SK_WARM tiles of the first chunk touched into L2 (one 4-byte LDS-DMA load
-      // per 128-byte line of this wave's slice, landing in a scratch word block nobody reads) while the query
-      // fragments are built. Waits only grow (the slab waits count these as later ops): results are unchanged.
-      if constexpr (RR_SK_WARM > 0 && LA == 2) {
-        const int tic0 = (int)(C - chunk == 1 ? T - chunk * CT : CT);
-        const unsigned warm_lds = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)((char*)(qexp + QS) + 2048));
-        int nwarm = 0;
-#pragma unroll
-        for (int t = 1; t <= RR_SK_WARM; ++t) {
-          if (t < tic0) {
-            int64_t row = base + 32 * t + (lane & 31);
-            row = row < n ? row : n - 1;
-#pragma unroll
-            for (int j0 = 0; j0 < NS; j0 += 2) {
-              const int j = j0 + (lane >> 5) < NS ? j0 + (lane >> 5) : NS - 1;
-              glds4(wave_src + row * row_bytes + j * kSlabRowBytes, warm_lds);
-              ++nwarm;
-            }
-          }
-        }
-        pend += nwarm;
       }
     }
   }
@@ -1141,7 +1154,10 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     const float eq = a.q8s[3 * QS + qe];
     q8e1 = (qn + eq) * 1.001f;
     q8e2 = (eq + fmaf(a.eps_a, qn, a.eps_b * a.sqrt_d)) * 1.001f;
-    q8e3 = a.eps_b * qsa * 1.001f;
+    // + 2^-110 absolute: the exact DT 3 score's products that fall below fp32's normal range, and every rounding of
+    // this bound's own arithmetic in the subnormal range, for rows and queries both tiny; + Q2 2^-69: the row norm |x|
+    // (fp32 sum of squares) reads short by at most sqrt(d) 2^-74.5 when the squares underflow
+    q8e3 = fmaf(q8e2, 0x1p-69f, fmaf(a.eps_b * qsa, 1.001f, 0x1p-110f));
   } else if constexpr (SCR) {
     const float* part = (const float*)vW;
     float s2 = 0.f, s1 = 0.f;
@@ -1151,7 +1167,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       s1 += part[kWaves * 32 + ww * 32 + qe];
     }
     qn = sqrtf(s2);
-    qsa = s1 * (1.0f + 0x1p-18f);
+    // (+ what eps_b >= 2^-25 turns into the int8 screen's absolute terms, q8e3: 2^-110 for subnormal products and
+    // roundings, and (eps_a |q| + eps_b sqrt(d)) 2^-69 for a row norm whose squares underflowed — eps_a / eps_b < 2^14)
+    qsa = fmaf(s1, 1.0f + 0x1p-18f, fmaf(qn, 0x1p-55f, 0x1p-63f));
   }
 
   TopK<KL> tk;
@@ -1364,16 +1382,6 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       }
   };
 
-  // Pipelined K-partial exchange (streaming passes; see the loop). The scheduler wave's next-chunk word is read one
-  // barrier later than it is published, which holds for chunks of >= 3 tiles (the dynamic schedule's 2-tile chunks,
-  // 4 slabs per row slice, keep the plain order).
-#ifndef RR_SK_PIPE
-#define RR_SK_PIPE 0   // measured: -2 % on the 64-slot pass (12-16 B of spills), within noise on the screen
-#endif
-  constexpr bool PIPE = MODE == 0 && RR_SK_PIPE && KT <= 16 && !(QH == 2 && DT == 2) && DT != 8 &&
-                        (SCHED == 0 || CT0 >= 3);   // (else spills)
-  int64_t pbase = 0;   // PIPE: the previous tile's first row and factor slot
-  int pts = 0;
   // Stagger (streaming passes): waves 4-7 — the SIMD partners of waves 0-3 — run each tile's epilogue one tile
   // late, after issuing the next tile's MFMAs, its summed scores kept in registers across the barrier. Partners
   // that reach the same phase together (matrix work, epilogue, barrier) leave the matrix core idle while both run
@@ -1386,13 +1394,12 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #define RR_SK_STAGGER8 0   // 1: the int8 screen too — its 9-wave form then spills 6 VGPRs and measured 4-8 % slower
                            // (profiles/r04/ab/ab_i8_stagger.txt)
 #endif
-  constexpr bool STG = MODE == 0 && !PIPE && !(QH == 2 && DT == 2) && DT != 6 && (DT != 8 || RR_SK_STAGGER8) &&
+  // (Rejected and removed: exchanging a tile's K-partials one tile late behind the next tile's MFMAs, -2 % on the
+  // 64-slot pass, profiles/r03/b/ab_pipelined_exchange_rejected.txt; deferring the odd waves instead of 4-7.)
+  constexpr bool STG = MODE == 0 && !(QH == 2 && DT == 2) && DT != 6 && (DT != 8 || RR_SK_STAGGER8) &&
                        KT <= 16 &&   // (measured)
                        (RR_SK_STAGGER == 2 || (RR_SK_STAGGER == 1 && QH == 2));
-#ifndef RR_SK_STAGGER_PAR
-#define RR_SK_STAGGER_PAR 0   // A/B only: defer the odd waves instead of waves 4-7
-#endif
-  const bool defer = STG && (RR_SK_STAGGER_PAR ? (w & 1) != 0 : w >= 4);
+  const bool defer = STG && w >= 4;
   float svd[DPO];
   int64_t bsd = -1;   // first row of the deferred tile (-1: none)
   int tsd = 0;        // its factor slot (4 slots: wave 0 refills a slot three tiles after its tile at the earliest)
@@ -1669,24 +1676,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       continue;
     }
 #endif
-    if constexpr (PIPE) {
-      // Pipelined exchange: this tile's MFMAs are issued; the previous tile's partials are summed and its epilogue
-      // runs while they execute, then this tile's partials go to LDS. The barrier that publishes a tile's partials
-      // is passed one tile later, behind the next tile's matrix work, instead of right after the MFMAs drain.
-      if (tcount > 0) {
-        lds_barrier();   // every wave wrote the previous tile's partials (and wave 0 its LDS-DMA factors / nxt)
-        float sv[DPL];
-        const float* rp = red + (red_bufs(RS, QH) == 2 ? (size_t)((tcount - 1) & 1) * kWaves * QS * kRedStride : 0);
-        read_partials(rp, sv);
-        if constexpr (red_bufs(RS, QH) == 1) lds_barrier();   // every wave has read them: the block is free
-        write_partials(rb, accs);
-        epilogue(sv, pbase, pts);
-      } else {
-        write_partials(rb, accs);
-      }
-      pbase = base;
-      pts = ts;
-    } else {
+    {
       if constexpr (red_bufs(RS, QH) == 1) {
         if (tcount > 0) lds_barrier();   // every wave has read the previous tile's partials
       }
@@ -1736,14 +1726,6 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     }
   }
   if (defer && bsd >= 0) epilogue(svd, bsd, tsd);   // the last tile's deferred epilogue
-  if constexpr (PIPE) {
-    if (tcount > 0) {   // the last tile's partials
-      lds_barrier();
-      float sv[DPL];
-      read_partials(red + (red_bufs(RS, QH) == 2 ? (size_t)((tcount - 1) & 1) * kWaves * QS * kRedStride : 0), sv);
-      epilogue(sv, pbase, pts);
-    }
-  }
 #if defined(RR_SK_DIAG) && (RR_SK_DIAG & 4)
   if (MODE == 0 && lane == 0)
     for (int i = 0; i < 8; ++i) phase_cycles[((size_t)blockIdx.x * 9 + w) * 8 + i] = ph[i];
@@ -1786,7 +1768,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     // the screen's lists go query-major, [QS][grid][KT + 1] — KT keys, then the workgroup's floor (see KL): each
     // verify workgroup then reads its query's lists as one contiguous block (the other paths' merge_kernel reads
     // [grid][QS][KT])
-    uint64_t* dst = a.out + (SCR ? ((size_t)qe * G + g) * (KT + 1) : ((size_t)g * QS + qe) * KT);
+    // (one list per workgroup of the launch, joiners included: list slot = blockIdx.x of gridDim.x)
+    uint64_t* dst = a.out + (SCR ? ((size_t)qe * gridDim.x + blockIdx.x) * (KT + 1)
+                                 : ((size_t)blockIdx.x * QS + qe) * KT);
     if constexpr (SCR) {   // before any pop: a full lane's last entry bounds every key it dropped
       const uint64_t fl = group_max_u64<LPQ>(tk.v[KL - 1]);
       if (lane % LPQ == 0) dst[KT] = KL < KT ? fl : 0;   // (KL = KT: the lists are the exact top-KT)
@@ -1796,37 +1780,6 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       const uint64_t m = group_max_u64<LPQ>(tk.v[0]);
       if (m != 0 && tk.v[0] == m) tk.pop();
       if (lane % LPQ == 0) dst[rnd] = m;
-    }
-    if constexpr (DT == 7 && SCHED == 1 && QH == 1 && KT <= 16) {
-      if (a.fuse) {   // fused verify (see fused_verify): the last 32 workgroups verify one query slot each
-        // The stream's 64-bit counter of finished screen workgroups is never reset: this launch's workgroups are the
-        // ones counted from vbase (the host adds each fused launch's grid), so even a verifier that gave up waiting
-        // cannot leave the next launch miscounted.
-        int* fv = vstate;   // [2] this workgroup's finishing rank, [3] every list published in time
-        __threadfence();    // this workgroup's lists: visible to every XCD before it counts itself done
-        __syncthreads();
-        if (tid == 0)
-          fv[2] = (int)(__hip_atomic_fetch_add(a.vsync, (uint64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) -
-                        a.vbase);
-        __syncthreads();
-        const int tkt = fv[2];
-        if (tkt < (int)G - QS) return;
-        if (tid == 0) {   // wait for the other workgroups' lists; bounded (a miss flags the block: exact re-run)
-          bool ok = false;
-          for (int it = 0; it < (1 << 21); ++it) {
-            if (__hip_atomic_load(a.vsync, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= a.vbase + (uint64_t)G) {
-              ok = true;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-          }
-          fv[3] = ok ? 1 : 0;
-        }
-        __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        fused_verify<2 * NS, KT, COS>(a, tkt - ((int)G - QS), smem, red, qinfo, akeys, grow, gnorm, gvalid, xk, vfloor,
-                                      vtail, vstate, vW, fv[3] != 0);
-      }
     }
   } else if constexpr (MODE == 1) {
     // The wave that owns query slot vq (QH 1: queries 4w..4w+3) merges its lanes' lists into xk; its leader lane
@@ -2092,6 +2045,10 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
   }
   // the screen: dynamic schedule (9-wave form) when asked for and the lists fit its registers; short or full
   // per-lane lists (a.full_lists)
+  // a carried verify (a.carry): the f16 / int8 copy's screen on the dynamic schedule, KT <= 16, more than 32 workgroups
+  if (a.carry && (sdt == KDT_SCREEN || !(a.dyn && a.ctr && kt <= 16) || grid <= kQSlots || !a.vin || !a.vqueries ||
+                  !a.vcorpus || a.vb < 1 || a.vb > kQSlots))
+    return hipErrorInvalidValue;
   if (sdt == KDT_SCREEN) {
     if (qslots != 32 || ring != 2) return hipErrorInvalidValue;
     const bool dyn = a.dyn && a.ctr && kt <= 16;

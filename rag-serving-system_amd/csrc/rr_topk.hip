@@ -209,7 +209,8 @@ hipError_t launch_topk_sorted(const uint64_t* in, int b, int64_t seg, int64_t k,
                        s, a, c, k, run);
     std::swap(a, c);
   }
-  if (a != out) hipMemcpyAsync(out, a, (size_t)total * 8, hipMemcpyDeviceToDevice, s);
+  if (a != out)   // an odd number of merge passes left the result in the scratch run buffer
+    if (hipError_t e = hipMemcpyAsync(out, a, (size_t)total * 8, hipMemcpyDeviceToDevice, s)) return e;
   return hipGetLastError();
 }
 

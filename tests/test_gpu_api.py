@@ -155,3 +155,65 @@ def test_update_rows_equals_reload(lib, dtype, devices):
             ex.close()
         up.close()
         fresh.close()
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0]])
+def test_update_rows_refreshes_the_int8_copy(lib, monkeypatch, devices):
+    """rr_update_rows on a handle that screens the int8 copy (RR_SCREEN_I8_MIN_ROWS=0: the copy is made for this small
+    corpus; d = 1024): the updated rows' int8 values, scales and error norms (store_rows -> f32_to_i8_kernel on single
+    rows) are refreshed in place, so the int8 screen's bound stays valid for them — results bit-identical to a handle
+    loaded with the modified corpus and to the exact kernel, rows that became the queries' best matches included
+    (a stale int8 row would drop true top-k rows without any flag)."""
+    rng = np.random.default_rng(12)
+    n, d = 5003, 1024
+    corpus = rng.standard_normal((n, d)).astype(np.float32)
+    q = rng.standard_normal((32, d)).astype(np.float32)
+    idx = np.array([3, 1999, 2501, 2502, n - 1, 4000], dtype=np.int64)
+    new = rng.standard_normal((len(idx), d)).astype(np.float32)
+    for j, r in enumerate(idx[:4]):                  # near-copies of queries: each becomes its query's top row
+        new[j] = q[2 * j] + 0.01 * rng.standard_normal(d).astype(np.float32)
+    new[5, 7] = 25.0                                 # a spike: every other element of its int8 row rounds to 0
+    changed = corpus.copy()
+    changed[idx] = new
+    for metric in ("cosine", "dot"):
+        monkeypatch.setenv("RR_SCREEN_I8_MIN_ROWS", "0")
+        up = lib.Index(devices=devices, dtype="fp32", metric=metric)
+        fresh = lib.Index(devices=devices, dtype="fp32", metric=metric)
+        monkeypatch.delenv("RR_SCREEN_I8_MIN_ROWS")
+        up.load(corpus)
+        up.search(q, 5)
+        up.update_rows(new, idx)
+        fresh.load(changed)
+        assert up.screen_int8() and fresh.screen_int8()
+        ex = lib.Index(devices=devices, dtype="fp32", metric=metric)
+        ex.load(changed)
+        ex.set_kernel("exact")
+        for k in (1, 5, 10):
+            want = ex.search(q, k)
+            for h in (up, fresh):
+                got = h.search(q, k)
+                assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), (metric, k)
+        assert all(want[1][2 * j, 0] == idx[j] for j in range(4)) or metric == "dot"
+        assert up.screen_int8()                      # still screening the int8 copy
+        for h in (up, fresh, ex):
+            h.close()
+
+
+def test_wait_settles_its_search_once(lib, monkeypatch):
+    """rr_wait settles the search of its ticket: a later rr_synchronize / rr_fetch_results does not observe it a
+    second time (the adaptive screen's windows count it once) nor re-run a flagged one again. Forced
+    fallbacks (RR_KERNEL_SCREEN_FALLBACK) flag every block: one wait = one re-run, then a synchronize adds none."""
+    rng = np.random.default_rng(13)
+    corpus = rng.standard_normal((4099, 512)).astype(np.float32)
+    q = rng.standard_normal((32, 512)).astype(np.float32)
+    ix = lib.Index(dtype="fp32", metric="cosine")
+    ix.load(corpus)
+    want = ix.search(q, 5)
+    ix.set_kernel("screen-fallback")
+    _, f0, r0, _ = ix.screen_counts_all()
+    got = ix.wait(ix.search_async(q, 5))
+    assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
+    ix.synchronize()
+    _, f1, r1, _ = ix.screen_counts_all()
+    assert (f1 - f0, r1 - r0) == (1, 1)
+    ix.close()

@@ -154,23 +154,33 @@ def _tiny_cases():
     big = big[(big - 97) % 613 >= 16]
     top[big] = -q[rng.integers(0, b, big.size)] * np.float32(4.0)
     cases.append(("tiny_top_rows", top, q))
+    # rows AND queries tiny together: the int8 screen's scale product sx * q8sc and its estimate
+    # fall into fp32's subnormal range, the exact kernel's smaller split products below fp32's normal range
+    cases.append(("both_2^-60", (base.astype(np.float64) * 2.0 ** -60).astype(np.float32),
+                  (q.astype(np.float64) * 2.0 ** -60).astype(np.float32)))
     return cases
 
 
-@pytest.mark.parametrize("case", range(7))
+@pytest.mark.parametrize("i8", [False, True])
+@pytest.mark.parametrize("case", range(8))
 @pytest.mark.parametrize("metric", ["cosine", "dot"])
-def test_screen_subnormal_range(Index, case, metric):
+def test_screen_subnormal_range(Index, monkeypatch, case, metric, i8):
     """f16-subnormal magnitudes: rows scaled by 2^-14 / 2^-18 / 2^-22, tiny queries, mixed
-    per-row scales and tiny top rows. The screened search (f16 copy, and the fp32-reading screen) must return
-    results BIT-IDENTICAL to the one-pass exact kernel, and the oracle's top-k (fp64 scores; index swaps only
-    between numerically tied documents, relative to the scores' own scale)."""
+    per-row scales, tiny top rows, and rows and queries both at 2^-60. Through the int8 copy (i8: the copy made for
+    this 20011-row corpus, RR_SCREEN_I8_MIN_ROWS=0), the f16 copy, and the fp32-reading screen,
+    the screened search must return results BIT-IDENTICAL to the one-pass exact kernel, and the oracle's top-k (fp64
+    scores; index swaps only between numerically tied documents, relative to the scores' own scale)."""
     name, corpus, q = _tiny_cases()[case]
     ex = Index(dtype="fp32", metric=metric)
     ex.load(corpus)
     ex.set_kernel("exact")
+    if i8:
+        monkeypatch.setenv("RR_SCREEN_I8_MIN_ROWS", "0")
     ix = Index(dtype="fp32", metric=metric)
+    monkeypatch.delenv("RR_SCREEN_I8_MIN_ROWS", raising=False)
     ix.load(corpus)
     assert ix.screen_copy()
+    assert ix.screen_int8() == i8
     exact = exact_scores(corpus, q, metric)
     for k in (1, 5, 10):
         want = ex.search(q, k)
@@ -178,8 +188,12 @@ def test_screen_subnormal_range(Index, case, metric):
         assert np.array_equal(got16[1], want[1]) and np.array_equal(got16[0], want[0]), (name, k)
         _, cidx = canonical_topk(exact, k)
         scale = float(np.max(np.abs(np.take_along_axis(exact, cidx, axis=1))))
-        check_topk(got16[1], got16[0], cidx, corpus, q, metric, near_tie=2e-5 * scale + 1e-30,
-                   score_tol=1e-3 * max(scale, 1e-30) if metric == "dot" else 1e-3)
+        if name == "both_2^-60":   # (the exact kernel's own rounding of its sub-normal-range split products)
+            check_topk(got16[1], got16[0], cidx, corpus, q, metric, near_tie=1e-3 * scale + 1e-300,
+                       score_tol=1e-3 * max(scale, 1e-300) if metric == "dot" else 1e-3)
+        else:
+            check_topk(got16[1], got16[0], cidx, corpus, q, metric, near_tie=2e-5 * scale + 1e-30,
+                       score_tol=1e-3 * max(scale, 1e-30) if metric == "dot" else 1e-3)
     blocks16, flagged16 = ix.screen_stats()
     ix.screen_copy(False)                                      # DT 6: the fp32 rows rounded to f16 in registers
     for k in (1, 5, 10):
@@ -188,7 +202,8 @@ def test_screen_subnormal_range(Index, case, metric):
         assert np.array_equal(got32[1], want[1]) and np.array_equal(got32[0], want[0]), (name, k)
     blocks, flagged = ix.screen_stats()
     assert blocks == 6 and blocks16 == 3
-    print(f"{name} {metric}: flagged {flagged16}/3 (f16 copy), {flagged - flagged16}/3 (fp32 screen)")
+    print(f"{name} {metric}: flagged {flagged16}/3 ({'int8' if i8 else 'f16'} copy), "
+          f"{flagged - flagged16}/3 (fp32 screen)")
     ix.close()
     ex.close()
 
@@ -486,19 +501,23 @@ def test_narrow_lists_switch_to_wide(Index):
 
 
 @pytest.mark.parametrize("devices", [[0], [0, 0]])
-def test_two_compute_streams_match_one(Index, devices):
-    """Screened blocks alternate between two compute streams (the default): a mixed sequence of staged searches
-    (several back to back, then fetched), multi-block batches, other k, another kind of search in between, and
-    four asynchronous searches in flight gives, step by step, exactly the one-stream results."""
+def test_carry_and_two_streams_match_one(Index, devices, monkeypatch):
+    """The screened search's three enqueue forms give, step by step, exactly the same results: the carried verify
+    (the default: each block's verify rides in the next screened block's launch, flushed when results are needed),
+    two alternating compute streams (carry off), and one stream with a verify launch per block. A mixed sequence of
+    staged searches (several back to back, then fetched), multi-block batches, list widths that change between
+    searches (a pending verify of another width is flushed), another kind of search in between (k = 40), and four
+    asynchronous searches in flight, forced re-runs included."""
     corpus = synth.unit_norm_gaussian(31, 40000, 1024)
     qa = synth.unit_norm_gaussian(32, 32, 1024)
     qb = synth.unit_norm_gaussian(33, 77, 1024)
     qs = [synth.unit_norm_gaussian(34 + i, 1 + 19 * i, 1024) for i in range(6)]
 
-    def run(streams):
+    def run(mode):
         ix = Index(devices=devices, dtype="fp32", metric="cosine")
         ix.load(corpus)
-        assert ix.compute_streams(streams) == streams
+        assert ix.carry_verify(mode == "carry") == (mode == "carry")
+        assert ix.compute_streams(2 if mode == "two" else 1) == (2 if mode == "two" else 1)
         out = []
         ix.set_queries(qa)
         for k in (5, 5, 7):
@@ -507,6 +526,10 @@ def test_two_compute_streams_match_one(Index, devices):
         ix.set_queries(qb)
         ix.search_staged(10)
         ix.search_staged(3)
+        out.append(ix.fetch())
+        ix.set_queries(qa)
+        for k in (5, 2, 2, 5):                     # list widths 16, 8, 8, 16: carried, flushed, carried, flushed
+            ix.search_staged(k)
         out.append(ix.fetch())
         out.append(ix.search(qa, 40))            # large k: another kind of search between screened ones
         out.append(ix.search(qb, 12))
@@ -520,6 +543,9 @@ def test_two_compute_streams_match_one(Index, devices):
         ix.set_kernel("screen-fallback")          # every block flagged: rr_wait re-stages and re-runs exactly
         tickets = [ix.search_async(q, 6) for q in qs[:3]]
         out += [ix.wait(t) for t in tickets]
+        ix.set_queries(qb)                        # flagged staged blocks, settled at the fetch: re-run exactly
+        ix.search_staged(6)
+        out.append(ix.fetch())
         ix.set_kernel("auto")
         tickets = []
         for q in qs:                               # the serving pattern: a new batch per search, 2 in flight
@@ -530,52 +556,56 @@ def test_two_compute_streams_match_one(Index, devices):
         ix.close()
         return out
 
-    for (s1, i1), (s2, i2) in zip(run(1), run(2)):
-        assert np.array_equal(i1, i2) and np.array_equal(s1, s2)
+    ref = run("one")
+    for mode in ("carry", "two"):
+        for (s1, i1), (s2, i2) in zip(ref, run(mode)):
+            assert np.array_equal(i1, i2) and np.array_equal(s1, s2), mode
 
 
+@pytest.mark.parametrize("i8", [False, True])
+@pytest.mark.parametrize("exchange", [False, True])
 @pytest.mark.parametrize("layout", ["interleaved", "contiguous"])
-def test_fused_verify_matches_separate_verify(Index, layout, monkeypatch):
-    """With an exchange step (here a 1-rank RCCL communicator) the screen's last 32 workgroups verify their own lists
-    in the same launch (rr_sk.hip fused_verify) instead of a separate verify launch. On near-duplicate clusters —
-    interleaved: the wide phase proves every query slot; contiguous: blocks flag and re-run exactly — the fused
-    handle's results, flags, re-runs and wide-phase proofs equal the separate-verify handle's (RR_FUSED_VERIFY=0),
-    and both equal the exact kernel, for k = 5 and 10, over back-to-back staged searches too."""
+def test_carried_verify_matches_separate_verify(Index, layout, exchange, i8, monkeypatch):
+    """The carried verify (rr_sk.hip carry_verify: 32 workgroups of block i + 1's screen launch verify block i, then
+    join the screen) against a verify launch per block (RR_CARRY_VERIFY=0), through the f16 copy and the int8 copy
+    (i8: RR_SCREEN_I8_MIN_ROWS=0), with and without an exchange step (a 1-rank RCCL communicator: the carried block's
+    keys are exchanged after the launch that verified them). On near-duplicate clusters — interleaved: the wide phase
+    proves the query slots; contiguous: blocks flag and re-run exactly — both handles return the exact kernel's
+    results bit for bit, for single searches and back-to-back staged ones, and count the same screened blocks."""
     from rag_service_amd import get_unique_id
     corpus, q = _clustered(60000, 0.01, layout)
     ex = Index(dtype="fp32", metric="cosine")
     ex.load(corpus)
     ex.set_kernel("exact")
-    handles = {}
-    for fused in (True, False):
-        monkeypatch.setenv("RR_FUSED_VERIFY", "1" if fused else "0")
-        ix = Index(dtype="fp32", metric="cosine")
-        monkeypatch.delenv("RR_FUSED_VERIFY")
-        ix.init_dist(1, 0, get_unique_id())
-        ix.load(corpus)
-        ix.set_schedule(True)
-        handles[fused] = ix
     counts = {}
-    for fused, ix in handles.items():
+    for carry in (True, False):
+        monkeypatch.setenv("RR_CARRY_VERIFY", "1" if carry else "0")
+        if i8:
+            monkeypatch.setenv("RR_SCREEN_I8_MIN_ROWS", "0")
+        ix = Index(dtype="fp32", metric="cosine")
+        monkeypatch.delenv("RR_CARRY_VERIFY")
+        monkeypatch.delenv("RR_SCREEN_I8_MIN_ROWS", raising=False)
+        if exchange:
+            ix.init_dist(1, 0, get_unique_id())
+        ix.load(corpus)
+        assert ix.carry_verify() == carry and ix.screen_int8() == i8
         for k in (5, 10):
             want = ex.search(q, k)
             got = ix.search(q, k)
-            assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), (fused, k)
+            assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), (carry, k)
             ix.set_queries(q)
             for _ in range(6):
                 ix.search_staged(k)
             got = ix.fetch()
-            assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), (fused, k, "staged")
-        counts[fused] = ix.screen_counts_all()
+            assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), (carry, k, "staged")
+        counts[carry] = ix.screen_counts_all()
         ix.close()
-    print(layout, counts)
+    print(layout, exchange, i8, counts)
     blocks, flagged, reruns, wide = counts[True]
     assert blocks == counts[False][0] == 14
-    if layout == "interleaved":     # the fused verify's wide phase proves what the separate one proves
-        # (the fused launch's grid depends on whether the other stream is busy — half the CUs beside it — so its lists,
-        # and which blocks the dynamic schedule leaves unproven, can differ by a block; the results never do)
-        # (a flagged staged search that nobody fetched is superseded, not re-run: reruns <= flagged)
-        assert flagged <= 2 and reruns <= flagged and wide >= 32 and counts[False][1] == 0 and counts[False][3] >= 32
-    else:
-        assert flagged >= 1 and reruns >= 1
+    assert reruns <= flagged          # (a flagged staged search that nobody fetched is superseded, not re-run)
+    if layout == "contiguous":
+        assert flagged >= 1 and reruns >= 1 and counts[False][1] >= 1
+    elif not i8:                      # the f16 copy's wide phase proves every interleaved block either way
+        assert flagged == counts[False][1] == 0 and wide >= 32 and counts[False][3] >= 32
     ex.close()

@@ -10,34 +10,42 @@ F = np.float32
 
 
 def quantize_rows(x):
+    """f32_to_i8_kernel: t = x / sx, x8 = clamp(rint(t)); e from the scaled residual t - x8 (exact), so no square
+    underflows: e = sx |t - x8| (1 + 2^-12) + 2^-22 sqrt(d) max|x| + 2^-140."""
     m = np.abs(x).max(axis=1)
     s = np.where(m > 0, m / F(127), F(0)).astype(F)
-    with np.errstate(divide="ignore", invalid="ignore"):
-        q = np.where(s[:, None] > 0, np.clip(np.rint(x / s[:, None]), -127, 127), 0).astype(F)
-    r = (x - s[:, None] * q).astype(F)
-    e = (np.sqrt((r * r).sum(axis=1, dtype=F)) * F(1 + 2 ** -12) + m * F(np.sqrt(x.shape[1])) * F(2 ** -22)).astype(F)
+    with np.errstate(divide="ignore", invalid="ignore", under="ignore"):
+        t = np.where(s[:, None] > 0, x / s[:, None], F(0)).astype(F)
+        q = np.clip(np.rint(t), -127, 127).astype(F)
+        r = (t - q).astype(F)
+        e = ((s * np.sqrt((r * r).sum(axis=1, dtype=F))).astype(F) * F(1 + 2 ** -12)
+             + (m * F(np.sqrt(x.shape[1]) * 2 ** -22) + F(2 ** -140))).astype(F)
     return q.astype(np.int8), s, e
 
 
 def quantize_query(v):
+    """q8_prep_kernel: t = q / s, p1 = clamp(rint(t)), p2 = clamp(rint((t - p1) 64)); eq from the exact scaled
+    residual t - p1 - p2 / 64."""
     m = F(np.abs(v).max())
     s = F(m / F(127)) if m > 0 else F(0)
-    if s > 0:
-        t = (v / s).astype(F)
-        a = np.clip(np.rint(t), -127, 127).astype(F)
-        c = np.clip(np.rint((t - a) * F(64)), -127, 127).astype(F)
-    else:
-        a = c = np.zeros_like(v)
-    r = (v - s * (a * F(64) + c) * F(2 ** -6)).astype(F)
-    eq = F(np.sqrt((r * r).sum(dtype=F)) * F(1 + 2 ** -12) + m * F(np.sqrt(v.size)) * F(2 ** -21))
-    qn = F(np.sqrt((v * v).sum(dtype=F)))
-    qsa = F(np.abs(v).sum(dtype=F) * F(1 + 2 ** -18))
-    return a.astype(np.int8), c.astype(np.int8), F(s * F(2 ** -6)), eq, qn, qsa
+    with np.errstate(under="ignore"):
+        if s > 0:
+            t = (v / s).astype(F)
+            a = np.clip(np.rint(t), -127, 127).astype(F)
+            ta = (t - a).astype(F)
+            c = np.clip(np.rint(ta * F(64)), -127, 127).astype(F)
+            r = (ta - c * F(2 ** -6)).astype(F)
+        else:
+            a = c = r = np.zeros_like(v)
+        eq = F(F(s * np.sqrt((r * r).sum(dtype=F))) * F(1 + 2 ** -12)
+               + (m * F(np.sqrt(v.size) * 2 ** -21) + F(2 ** -140)))
+        qn = F(np.sqrt((v * v).sum(dtype=F)))
+        qsa = F(np.abs(v).sum(dtype=F) * F(1 + 2 ** -18))
+        return a.astype(np.int8), c.astype(np.int8), F(s * F(2 ** -6)), eq, qn, qsa
 
 
 def bound(xq, sx, e, nd, p1, p2, qsc, eq, qn, qsa, eps_a=6e-5, eps_b=4e-8):
-    """(the eps_b term also covers squared residuals that underflow fp32: |r| < 2^-63 leaves e short by at most
-    2^-63 sqrt(d) |q|, far below eps_b sum|q|)"""
+    """The DT 8 epilogue's upper bound of x . q (nd: the fp32 row norm the kernel reads, short when squares underflow)."""
     acc = xq.astype(np.int64) @ (64 * p1.astype(np.int64) + p2.astype(np.int64))   # exact, as the int32 MFMA sums
     s = acc.astype(F)
     est = (s * sx).astype(F) * qsc
@@ -46,17 +54,25 @@ def bound(xq, sx, e, nd, p1, p2, qsc, eq, qn, qsa, eps_a=6e-5, eps_b=4e-8):
     # Q3 = eps_b sum|q|, each x 1.001
     q1 = F((qn + eq) * F(1.001))
     q2 = F((eq + (F(eps_a) * qn + F(eps_b) * sqrt_d)) * F(1.001))
-    q3 = F(F(eps_b) * qsa * F(1.001))
+    # (+ the absolute 2^-110 and Q2 2^-69 for row norms whose squares underflow, rr_sk.hip q8e3)
+    q3 = F(q2 * F(2 ** -69) + (F(eps_b) * qsa * F(1.001) + F(2 ** -110)))
     eps = (e * q1 + (nd * q2 + q3)).astype(F)
     v = est + np.abs(est) * F(2 ** -21) + eps
     return v + np.abs(v) * F(2 ** -22)
 
 
-@pytest.mark.parametrize("kind", ["gauss", "spiky", "scaled", "tiny", "small", "huge", "zero_rows", "sparse"])
+KINDS = ["gauss", "spiky", "scaled", "tiny", "small", "huge", "zero_rows", "sparse",
+         # rows AND queries tiny together: the scales' product sx q8sc, the estimate and the
+         # residual terms fall into fp32's subnormal range
+         "both_2^-60", "both_2^-64", "rows_2^-100_q_2^-30", "rows_2^-30_q_2^-100", "rows_2^-120"]
+
+
+@pytest.mark.parametrize("kind", KINDS)
 def test_int8_bound_holds(kind):
     rng = np.random.default_rng(sum(map(ord, kind)))
     n, d = 3000, 1024
     x = rng.standard_normal((n, d)).astype(F)
+    qscale = 1.0
     if kind == "spiky":
         x *= F(0.05)
         x[np.arange(n), rng.integers(0, d, n)] = F(60.0)
@@ -72,13 +88,26 @@ def test_int8_bound_holds(kind):
         x[::3] = 0
     elif kind == "sparse":
         x[rng.random((n, d)) < 0.97] = 0
+    elif kind.startswith("both_"):
+        e = int(kind.split("^")[1])
+        x = (x.astype(np.float64) * 2.0 ** e).astype(F)
+        qscale = 2.0 ** e
+    elif kind.startswith("rows_"):
+        parts = kind.split("_")
+        x = (x.astype(np.float64) * 2.0 ** int(parts[1].split("^")[1])).astype(F)
+        if len(parts) > 2:
+            qscale = 2.0 ** int(parts[3].split("^")[1])
     xq, sx, e = quantize_rows(x)
-    nd = np.sqrt((x.astype(np.float64) ** 2).sum(axis=1)).astype(F)
+    with np.errstate(under="ignore"):   # the fp32 norm the kernels read (row_norms_kernel): squares may underflow
+        nd = np.sqrt((x * x).sum(axis=1, dtype=F)).astype(F)
     for j in range(8):
         v = rng.standard_normal(d).astype(F)
         if j % 2:   # queries aligned with some rows (their true matches)
             v = (x[rng.integers(n)] + F(0.1) * np.abs(x).max() * rng.standard_normal(d).astype(F)).astype(F)
-        u = bound(xq, sx, e, nd, *quantize_query(v))
+            v = (v.astype(np.float64) / max(float(np.abs(v).max()), 1e-300)).astype(F)
+        v = (v.astype(np.float64) * qscale).astype(F)
+        with np.errstate(under="ignore"):
+            u = bound(xq, sx, e, nd, *quantize_query(v))
         exact = x.astype(np.float64) @ v.astype(np.float64)
         assert np.all(u.astype(np.float64) >= exact), float(np.max(exact - u))
 

@@ -8,6 +8,7 @@
 #   smoke          __graft_entry__.smoke()
 #   bench          the driver's bench command (PMC child pass, CPU baseline)
 #   bench:<name>:<args>   a short bench.py run (no CPU baseline, variants, ingest or PMC pass) with extra args
+#   benchenv:<name>:<VAR=value[,...]>:<args>   the same with environment settings (A/B knobs such as RR_CARRY_VERIFY=0)
 #   prof           bench + rocprofv3 --kernel-trace --stats of the same command (tools/prof_round.sh)
 #   trace_x125k    rocprofv3 kernel + memory-copy trace of the 1-rank RCCL exchange path at the 8-GPU shard size
 #                  (Queue_Id / Stream_Id per kernel), QUEUES=4 default
@@ -32,6 +33,9 @@ step() {
     bench:*) IFS=: read -r _ name bargs <<< "$1"
              (cd /tmp && timeout -k 10 300 python3 "$R/bench.py" --gpus 1 --no-cpu-baseline --variants= --ingest-rows 0 \
                --no-pmc $bargs > "$O/bench_$name.json" 2> "$O/bench_$name.err") ;;
+    benchenv:*) IFS=: read -r _ name benv bargs <<< "$1"
+             (cd /tmp && env $benv timeout -k 10 300 python3 "$R/bench.py" --gpus 1 --no-cpu-baseline --variants= \
+               --ingest-rows 0 --no-pmc $bargs > "$O/bench_$name.json" 2> "$O/bench_$name.err") ;;
     prof) bash "$R/tools/prof_round.sh" "gpurun_out/${OUT:-r4}/prof" ;;
     trace_x125k)
       Q=${QUEUES:-4}
