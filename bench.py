@@ -206,7 +206,7 @@ def main() -> None:
                          "pipelined host-inclusive loop")
     ap.add_argument("--timing-every", type=int, default=0,
                     help="bracket the similarity kernel with HIP events on every N-th timed step "
-                         "(0: every step when --steps < 100, else every 10th)")
+                         "(0: every 5th step when --steps < 100, else every 10th)")
     ap.add_argument("--steady-steps", type=int, default=2000,
                     help="back-to-back steps timed again after the latency loop (steady-state rate, reported "
                          "beside value; BASELINE.md: >= 1000 steps)")
@@ -254,7 +254,8 @@ def main() -> None:
 
 
 def run(args, stage: dict) -> None:
-    every = args.timing_every or (1 if args.steps < 100 else 10)
+    # (HIP events on every 5th step of a short window: two event records per timed step are host work in the window)
+    every = args.timing_every or (5 if args.steps < 100 else 10)
 
     from rag_service_amd import Index, get_unique_id
     from rag_service_amd import _lib
@@ -359,35 +360,28 @@ def run(args, stage: dict) -> None:
     fp32_floor = n_local * args.dim * 4 + args.batch * args.dim * 4
     avg_kernel_s = (kern_ms / max(launches, 1)) / 1e3
     step_s = elapsed / args.steps
-    # screened blocks with the carried verify (the fp32 default): one launch per step — block i's screen with block
-    # i - 1's verify in 32 more workgroups that then join the screen — on one compute stream; with two compute
-    # streams (carry off) block i + 1's screen starts while block i's drains, so a launch's event span covers about
-    # two steps and is no duration of its own. Either way one launch per step: the launch's time is the step time,
-    # and `achieved` = its algorithmic bytes / ms_per_step (the sustained HBM rate of the path). The screen kernel by
-    # itself (no carried verify, one stream, every CU) is measured below.
-    carry = args.dtype == "fp32" and ix.carry_verify()
+    # screened blocks on two compute streams (the fp32 default): block i + 1's screen starts while block i's screen
+    # drains and its verify runs, so each launch's event span covers about two steps and is no duration of its
+    # own. One launch per step: the launch's time is then the step time, and `achieved` = its algorithmic bytes /
+    # ms_per_step (the sustained HBM rate of the path). The kernel alone (one stream, every CU) is measured below.
     streams = ix.compute_streams() if args.dtype == "fp32" else 1
-    overlap = streams == 2 or carry
+    overlap = streams == 2
     launch_s = step_s if overlap else avg_kernel_s
     achieved = alg_bytes / launch_s / 1e9 if launches else None
     consistent = bool(launches) and launch_s <= step_s * 1.001
     st_launch_s = (st_el / args.steady_steps) if overlap else (st_ms / max(st_n, 1) / 1e3)
     alone = None
     if overlap and not args.pmc_child:
-        # the same screen kernel with one compute stream and no carried verify (every CU screening, nothing
-        # overlapping, a verify launch after it): the screen launch's own duration by HIP events on every launch,
-        # after the GPU has been busy for the loops above
-        ix.carry_verify(False)
+        # the same screen kernel with one compute stream (every CU screening, nothing overlapping): its own launch
+        # duration by HIP events on every launch, after the GPU has been busy for the loops above
         ix.compute_streams(1)
         a_el, a_ms, a_n = timed_steps(ix, args.k, 40, 5, dist, cuda_sync, 1)
-        ix.compute_streams(streams)
-        ix.carry_verify(carry)
+        ix.compute_streams(2)
         a_kern = a_ms / max(a_n, 1) / 1e3
         alone = {"kernel_avg_us": round(a_kern * 1e6, 2), "frac": round(alg_bytes / a_kern / 1e9 / HBM_PEAK_GBS, 4),
                  "ms_per_step": round(a_el / 40 * 1e3, 4), "launches": a_n,
-                 "note": "carry_verify(False) + compute_streams(1): the screen on every CU, one launch at a time "
-                         "(its verify a separate launch), 40 steps after the loops above; HIP events around every "
-                         "screen launch"}
+                 "note": "compute_streams(1): the screen on every CU, one launch at a time, 40 steps after the loops "
+                         "above; HIP events around every launch"}
     if args.pmc_child:            # only the fused-kernel launches matter to the parent's PMC parse
         ix.close()
         return
@@ -505,17 +499,12 @@ def run(args, stage: dict) -> None:
                          "kernel_alone": alone,
                          "kernel_timing": (f"HIP events on the kernel's stream around every {every}-th "
                                            f"similarity-kernel launch of the timed region ({launches} launches)"
-                                           + ("; carried verify: one launch per step (block i's screen + block "
-                                              "i - 1's verify, then those workgroups join the screen), "
-                                              "kernel_avg_us and achieved use the step time; kernel_alone is the "
-                                              "screen by itself" if carry else
-                                              "; two compute streams: consecutive launches overlap, kernel_span_us is "
+                                           + ("; two compute streams: consecutive launches overlap, kernel_span_us is "
                                               "a launch's event span, kernel_avg_us and achieved use the step time "
                                               "(one launch per step); kernel_alone is the kernel by itself"
                                               if overlap else "")),
                          "kernel_le_step": consistent,
                          "compute_streams": streams,
-                         "carry_verify": bool(carry),
                          "step_frac": round(alg_bytes / step_s / 1e9 / HBM_PEAK_GBS, 4),
                          "step_frac_note": "algorithmic bytes of one launch / ms_per_step: the sustained fraction of "
                                            "peak over the timed steps (with two compute streams the launches overlap "

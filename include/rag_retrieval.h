@@ -216,16 +216,6 @@ int rr_set_schedule(rr_handle* h, int dynamic);
  * setting changes. */
 int rr_set_compute_streams(rr_handle* h, int32_t n, int32_t* in_use);
 
-/* Carried verify of the screened search (fp32 storage, the f16 / int8 copy's screen, k <= 13; default on): screened
- * blocks run on ONE compute stream and a block's exact verify is launched inside the NEXT screened block's screen —
- * 32 more workgroups verify the previous block's query slots and then join the screen — so a stream of searches costs
- * one launch per block and the verifying CUs stream rows as soon as they are done. A block's verify runs alone
- * (flushed) whenever its results, flag or lists are needed first: rr_fetch_results, rr_synchronize, rr_search,
- * rr_search_async, rr_wait, any other kind of search. Results are bit-identical either way; with it on,
- * rr_set_compute_streams' two streams are not used. on: 1 / 0 / -1 (leave as is); *in_use (may be null): the
- * setting. Synchronises the handle when the setting changes. (RR_CARRY_VERIFY=0 at rr_create: off.) */
-int rr_set_carry_verify(rr_handle* h, int32_t on, int32_t* in_use);
-
 /* The screened search's f16 copy (fp32 storage): the screen pass reads an f16 copy of the rows — exactly the
  * values it would round the fp32 rows to in registers — so it streams half the bytes; the verify and every
  * result still come from the fp32 rows (bit-identical results either way). The copy costs 2 bytes per element

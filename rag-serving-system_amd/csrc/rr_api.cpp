@@ -115,8 +115,6 @@ struct Shard {
   int* pin_scount = nullptr;             // pinned staging of scount / wcount reads (rr_screen_counts)
   uint32_t* ctr = nullptr;               // split-K chunk counters (dynamic schedule), 0 between launches: one per
                                          // compute stream, kCtrStride words apart; then (words 2 and 3 x kCtrStride)
-  int pend_nlists = 0;                   // the pending (carried) verify's list count: its screen's grid here
-  int pend_nlists_next = 0;              // (the block being enqueued)
   uint64_t* shard_keys = nullptr;        // [32][k_cap] this shard's top-k (all-gather send buffer)
   uint64_t* gathered = nullptr;          // [world][32][k_cap] (all-gather receive buffer)
   // pipelined exchange (k <= RR_FUSED_KMAX, world > 1): the exchange of search i (all-gather + final
@@ -169,13 +167,11 @@ struct Shard {
 
 // One in-flight rr_search_async batch: a pinned buffer that carries its queries to the device and,
 // stream-ordered after the search, its results back.
-// A screened block whose verify is not launched yet: it runs in the next screened block's screen launch (rr_sk.hip
-// carry_verify) or alone when something needs the block's results first (flush_verify). Its lists are in candidate half
-// p, its queries in query buffer qpar; results in place (no exchange) or its keys + flag word in px_keys[x].
-struct PendVerify {
-  bool on = false;
-  int q0 = 0, bb = 0, k = 0, kt = 0, slots = 0, x = 0, p = 0, seq = 0, qpar = 0;
-  bool force = false;   // RR_KERNEL_SCREEN_FALLBACK when the block was enqueued (test hook: report it incomplete)
+// A screened block, as its verify sees it: its lists are in candidate half p; results in place (no exchange) or its
+// keys + flag word in px_keys[x] (verify_args).
+struct VerifyBlock {
+  int q0 = 0, bb = 0, k = 0, kt = 0, slots = 0, x = 0, p = 0, seq = 0;
+  bool force = false;   // RR_KERNEL_SCREEN_FALLBACK (test hook: report the block incomplete)
 };
 
 struct AsyncSlot {
@@ -239,6 +235,7 @@ struct rr_handle {
   int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy)
   int screen_i8 = 1;            // ... and an int8 copy, screened first (rr_screen_int8; RR_SCREEN_I8=0 at creation: off)
   int ct8 = 0;                  // the int8 screen's tiles per chunk (0: by shard size; A/B: RR_SCREEN_CT8)
+  int guided = 1;               // split-K chunks: 2-tile chunks at the end of a launch (A/B: RR_SCREEN_GUIDED=0)
   int64_t i8_min_rows = 65536;  // ... for shards of at least this many rows (RR_SCREEN_I8_MIN_ROWS): below, a search is
                                 // launch-bound and lists holding a large share of the shard's rows leave the looser
                                 // bound little to prove with (a 1000-row corpus of real embeddings re-ran blocks)
@@ -260,10 +257,6 @@ struct rr_handle {
   int wide_verify = 1;          // the verify's wide phase (A/B: RR_WIDE_VERIFY=0)
   bool host_prof = false;       // RR_HOST_PROF=1 (diagnostics)
   HostProf hp;
-  // Carried verify (rr_set_carry_verify; RR_CARRY_VERIFY=0 at creation: off): screened blocks run on one compute stream
-  // and each block's verify rides in the next block's screen launch (rr_sk.hip carry_verify)
-  int carry = 1;
-  PendVerify pend;
   bool ab_no_verify = false;    // A/B only (RR_AB_NO_VERIFY=1): skip the screened search's verify launch — results
                                 // invalid; measures what the verify's launch costs the step
   // adaptive screen (observe_settled): the screen's per-lane lists grow from 4 keys to KT once blocks flag, and
@@ -695,7 +688,6 @@ int drop_work_buffers(rr_handle* h) {
   h->screen_pause = h->pauses = 0;
   h->last_screened = false;
   h->last_settled = true;
-  h->pend.on = false;   // (its buffers are gone: the search it belonged to is discarded with them)
   h->qpar = 0;
   h->loaded = false;
   return RR_OK;
@@ -978,8 +970,7 @@ int collect_timing(rr_handle* h) {
 // Measured against one stream and every CU screening (profiles/r02/ab/ab_screen_grid*.txt): +23-45 % per step at
 // 125k-250k rows, +2-5 % at 1M-2M.
 constexpr int kVerifyCUs = 32;
-// (carry mode: one compute stream — the next block's launch carries this block's verify, so blocks cannot overlap)
-bool two_streams(const rr_handle* h, const Shard&) { return h->streams == 2 && !h->carry; }
+bool two_streams(const rr_handle* h, const Shard&) { return h->streams == 2; }
 // Screen workgroups on shard s; `alone`: no screened block is in flight on the other stream (its last verify has
 // completed: a single search, or the first of a burst), so nothing overlaps this one and every CU screens.
 int screen_grid(const rr_handle* h, const Shard& s, bool alone) {
@@ -1142,13 +1133,14 @@ rr::SkArgs sk_base(const rr_handle* h, const Shard& s, const float* qb, int bb) 
   a.idx_base = (uint32_t)s.row_begin;
   a.ctr = s.ctr;
   a.dyn = h->dyn_sched;
+  a.no_guided = h->guided ? 0 : 1;
   return a;
 }
 
-// The verify's arguments (MODE 1, or a carried verify's fields of a screen launch) for screened block v on shard s:
-// its screen's nlists lists in candidate half v.p; results in place, or (exchange) this shard's exact keys and the
-// block's flag word in px_keys[v.x] (else the flag is the result buffer's head).
-void verify_args(const rr_handle* h, const Shard& s, const PendVerify& v, int nlists, rr::SkArgs* a) {
+// The verify's arguments (MODE 1) for screened block v on shard s: its screen's nlists lists in candidate half v.p;
+// results in place, or (exchange) this shard's exact keys and the block's flag word in px_keys[v.x] (else the flag is
+// the result buffer's head).
+void verify_args(const rr_handle* h, const Shard& s, const VerifyBlock& v, int nlists, rr::SkArgs* a) {
   const bool multi = h->world > 1 || h->dist;
   a->vin = s.cand + (size_t)v.p * cand_half(s);
   a->nlists = nlists;
@@ -1163,27 +1155,6 @@ void verify_args(const rr_handle* h, const Shard& s, const PendVerify& v, int nl
   a->wide_count = s.wcount;
 }
 
-int enqueue_exchange_px(rr_handle* h, int p, int x, int q0, int bb, int k, int kt, int slots, bool scr);
-
-// Launch the pending carried verify on its own (MODE 1, 32 workgroups, on `stream` after its screen) and, with an
-// exchange step, the block's exchange: whenever something needs that block's results, flag or candidate lists before
-// the next screened launch would carry it.
-int flush_verify(rr_handle* h) {
-  if (!h->pend.on) return RR_OK;
-  const PendVerify v = h->pend;
-  h->pend.on = false;
-  for (Shard& s : h->shards) {
-    HIP_TRY(hipSetDevice(s.dev));
-    rr::SkArgs a = sk_base(h, s, s.qbuf[v.qpar] + (size_t)v.q0 * h->d, v.bb);
-    verify_args(h, s, v, s.pend_nlists, &a);
-    a.seq = v.seq;
-    HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, v.kt, 1, rr::kQSlots, rr::kQSlots, a, s.stream));
-  }
-  if (h->world > 1 || h->dist)
-    if (int rc = enqueue_exchange_px(h, v.p, v.x, v.q0, v.bb, v.k, v.kt, v.slots, true)) return rc;
-  return RR_OK;
-}
-
 // Enqueue the device pipeline for query block [q0, q0 + bb) (bb <= slots) on every local shard.
 int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
   const int d = h->d;
@@ -1194,14 +1165,6 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
   const bool local_multi = multi && !h->dist;
   const int p = h->parity;
   const int x = h->xslot;   // pipelined-exchange buffer set of this block
-  // Carried verify (rr_sk.hip carry_verify): a screened block on the dynamic schedule over the f16 / int8 copy (every
-  // shard) defers its verify into the next such launch; a pending verify of another list width is flushed first, and
-  // every other kind of block flushes it (enqueue_block).
-  bool cm = scr && h->carry && h->dyn_sched && kt <= 16 && !h->ab_no_verify;
-  for (const Shard& s : h->shards) cm = cm && s.rows() > 0 && s.scr16 && h->screen_copy && rr::sk_slabs(rr::KDT_SCREEN16, d);
-  if (h->pend.on && (!cm || h->pend.kt != kt))
-    if (int rc = flush_verify(h)) return rc;
-  const bool carrying = cm && h->pend.on;
   if (scr || wk) {
     ++h->screen_seq;
     ++h->screen_blocks;
@@ -1264,11 +1227,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       const bool s8 = s16 && s.scr8 && i8_active(h);
       const bool alone = !two || s.last_vsi < 0 || s.last_vsi == bsi ||
                          hipEventQuery(s.ev_q[s.last_vq][s.last_vsi]) == hipSuccess;
-      // Carried verify (rr_sk.hip carry_verify): this block's verify is deferred into the next screened block's launch
-      // (or a flush); when the previous block's is pending, 32 more workgroups verify it first and then join this
-      // screen. The launch takes every CU.
-      int sgrid = screen_grid(h, s, alone);
-      if (cm) sgrid = carrying ? std::max(1, sgrid - rr::kQSlots) + rr::kQSlots : sgrid;
+      const int sgrid = screen_grid(h, s, alone);
       const int64_t tl = h->host_prof ? now_ns() : 0;
       if (timed) HIP_TRY(hipEventRecord(e0, cs));
       if (s.rows() > 0) {
@@ -1294,37 +1253,24 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
           a.eps_a = kScreen8EpsA;
           a.eps_b = kScreen8EpsB;
         }
-        if (carrying) {   // the previous screened block's verify in workgroups [0, 32)
-          const PendVerify& pv = h->pend;
-          verify_args(h, s, pv, s.pend_nlists, &a);
-          a.carry = 1;
-          a.vcorpus = (const char*)s.corpus;
-          a.vqueries = s.qbuf[pv.qpar] + (size_t)pv.q0 * d;
-          a.vb = pv.bb;
-          a.vseq = pv.seq;
-        }
         HIP_TRY(rr::launch_sk_args(s8 ? rr::KDT_SCREEN8 : s16 ? rr::KDT_SCREEN16 : rr::KDT_SCREEN, h->metric, kt, 0,
                                    sgrid, rr::kQSlots, a, cs));
       }
       if (timed) HIP_TRY(hipEventRecord(e1, cs));
-      if (cm) {
-        s.pend_nlists_next = sgrid;   // this block's lists, verified by the next screened launch or a flush
-      } else {
-        // results written in place (no exchange): this verify follows the previous one when that ran on the other
-        // stream (the same rows of the result buffer)
-        if (two && !multi && s.last_vsi >= 0 && s.last_vsi != bsi)
-          HIP_TRY(hipStreamWaitEvent(vs, s.ev_q[s.last_vq][s.last_vsi], 0));
-        if (s.rows() > 0 && !h->ab_no_verify) {
-          rr::SkArgs v = sk_base(h, s, qb, bb);
-          PendVerify me;
-          me.q0 = q0, me.bb = bb, me.k = k, me.kt = kt, me.slots = slots, me.x = x, me.p = p, me.seq = seq;
-          me.force = h->kernel == RR_KERNEL_SCREEN_FALLBACK;
-          verify_args(h, s, me, sgrid, &v);
-          v.seq = seq;
-          HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 1, rr::kQSlots, rr::kQSlots, v, vs));
-        } else if (!h->ab_no_verify) {   // a shard without rows contributes empty lists and no flag
-          HIP_TRY(hipMemsetAsync(s.px_keys[x], 0, ((size_t)slots * kt + 1) * 8, vs));
-        }
+      // results written in place (no exchange): this verify follows the previous one when that ran on the other
+      // stream (the same rows of the result buffer)
+      if (two && !multi && s.last_vsi >= 0 && s.last_vsi != bsi)
+        HIP_TRY(hipStreamWaitEvent(vs, s.ev_q[s.last_vq][s.last_vsi], 0));
+      if (s.rows() > 0 && !h->ab_no_verify) {
+        rr::SkArgs v = sk_base(h, s, qb, bb);
+        VerifyBlock me;
+        me.q0 = q0, me.bb = bb, me.k = k, me.kt = kt, me.slots = slots, me.x = x, me.p = p, me.seq = seq;
+        me.force = h->kernel == RR_KERNEL_SCREEN_FALLBACK;
+        verify_args(h, s, me, sgrid, &v);
+        v.seq = seq;
+        HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 1, rr::kQSlots, rr::kQSlots, v, vs));
+      } else if (!h->ab_no_verify) {   // a shard without rows contributes empty lists and no flag
+        HIP_TRY(hipMemsetAsync(s.px_keys[x], 0, ((size_t)slots * kt + 1) * 8, vs));
       }
       if (h->host_prof) {
         h->hp.ns[3] += now_ns() - tl;
@@ -1457,21 +1403,6 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       if (!multi) HIP_TRY(rr::launch_decode(s.shard_keys, bb, k, osc, oix, s.stream));
     }
   }
-  if (cm) {   // the carried block's exchange (its keys are written by this launch), then this block is pending
-    if (carrying && multi) {
-      const PendVerify& pv = h->pend;
-      if (int rc = enqueue_exchange_px(h, pv.p, pv.x, pv.q0, pv.bb, pv.k, pv.kt, pv.slots, true)) return rc;
-    }
-    PendVerify& me = h->pend;
-    me.on = true;
-    me.q0 = q0, me.bb = bb, me.k = k, me.kt = kt, me.slots = slots, me.x = x, me.p = p, me.seq = seq;
-    me.qpar = h->qpar;
-    me.force = h->kernel == RR_KERNEL_SCREEN_FALLBACK;
-    for (Shard& s : h->shards) s.pend_nlists = s.pend_nlists_next;
-    h->parity ^= 1;
-    if (multi) h->xslot = (x + 1) % h->xslots;
-    return RR_OK;
-  }
   if (!multi) {
     if (scr) h->parity ^= 1;
     return RR_OK;
@@ -1541,8 +1472,6 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
 // after everything on cstream2, and later cstream2 blocks follow it.
 int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
   const bool scr = screened(h, k, slots);
-  if (!scr)   // a pending carried verify reads the candidate lists and writes results this block may rewrite
-    if (int rc = flush_verify(h)) return rc;
   if (!scr)
     for (Shard& s : h->shards) {
       HIP_TRY(hipSetDevice(s.dev));
@@ -1665,10 +1594,10 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   if (const char* e = getenv("RR_WIDE_VERIFY")) h->wide_verify = atoi(e) ? 1 : 0;   // (A/B)
   if (const char* e = getenv("RR_AB_NO_VERIFY")) h->ab_no_verify = atoi(e) != 0;    // (A/B only: invalid results)
   if (const char* e = getenv("RR_HOST_PROF")) h->host_prof = atoi(e) != 0;
-  if (const char* e = getenv("RR_CARRY_VERIFY")) h->carry = atoi(e) != 0;   // (A/B: 0 = a verify launch per block)
   if (const char* e = getenv("RR_SCREEN_I8")) h->screen_i8 = atoi(e) != 0;         // (A/B: 0 = the f16 copy only)
   if (const char* e = getenv("RR_SCREEN_I8_MIN_ROWS")) h->i8_min_rows = atoll(e);
   if (const char* e = getenv("RR_SCREEN_CT8")) h->ct8 = atoi(e);
+  if (const char* e = getenv("RR_SCREEN_GUIDED")) h->guided = atoi(e) != 0;
   if (const char* e = getenv("RR_STATIC_SCHEDULE")) h->dyn_sched = atoi(e) == 0;   // (A/B: 1 = rr_set_schedule(0))
   if (const char* e = getenv("RR_SCREEN_FULL_LISTS")) h->full_lists_env = atoi(e) != 0;   // (A/B: start with full lists)
   *out = h;
@@ -2018,7 +1947,6 @@ int rr_last_shape(const rr_handle* h, int32_t* b, int32_t* k) {
 namespace {
 
 int sync_streams(rr_handle* h) {
-  if (int rc = flush_verify(h)) return rc;   // (a carried verify still pending: its block's results are owed)
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
     for (hipStream_t st : {s.stream, s.xstream, s.xstream2, s.cstream2})
@@ -2157,7 +2085,6 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
   h->qpar = nq;
   h->cur_b = b;
   if (int rc = rr_search_staged(h, k)) return rc;
-  if (int rc = flush_verify(h)) return rc;   // (the copy below reads this search's results)
   // results come back on the stream that wrote them last: the exchange stream when there is an exchange
   // (the serial k > 32 exchange also orders it after itself), else the compute stream
   Shard& s0 = h->shards[0];
@@ -2327,19 +2254,6 @@ int rr_set_compute_streams(rr_handle* h, int32_t n, int32_t* in_use) {
     h->streams = n;
   }
   if (in_use) *in_use = h->shards.empty() ? 1 : (two_streams(h, h->shards[0]) ? 2 : 1);
-  return RR_OK;
-}
-
-int rr_set_carry_verify(rr_handle* h, int32_t on, int32_t* in_use) {
-  if (!h) return fail(RR_E_INVALID, "null handle");
-  if (h->failed) return failed_handle();
-  if (on < -1 || on > 1) return fail(RR_E_INVALID, "carry verify %d (-1 = as is, 0, 1)", on);
-  if (on >= 0 && (on != 0) != (h->carry != 0)) {
-    if (int rc = rr_synchronize(h)) return rc;   // (flushes a pending verify)
-    for (Shard& s : h->shards) s.last_vsi = -1;
-    h->carry = on;
-  }
-  if (in_use) *in_use = h->carry ? 1 : 0;
   return RR_OK;
 }
 

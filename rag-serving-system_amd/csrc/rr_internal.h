@@ -84,15 +84,6 @@ struct SkArgs {
   uint64_t* floors;
   // MODE 0, KT 32, 32 slots: every key instead of lists, all_keys[q * n + row] for q < b (full-sort path)
   uint64_t* all_keys;
-  // Carried verify (MODE 0, the f16- or int8-copy screen on the dynamic schedule, KT <= 16; rr_sk.hip carry_verify):
-  // workgroups [0, 32) of the launch first verify one query slot each of the PREVIOUS screened block (the MODE 1 fields
-  // above: vin = that block's lists, nlists = its screen's grid, k_out, out_scores / out_idx / out_keys, flag, count,
-  // force_incomplete, wide_verify, wide_count), over the fp32 rows vcorpus with that block's queries vqueries (vb of
-  // them) and sequence number vseq, then join this screen on the dynamic counter.
-  int carry;
-  const char* vcorpus;
-  const float* vqueries;
-  int vb, vseq;
   // int8 screen (KDT_SCREEN8): corpus = the int8 copy, read as n = ceil(rows8 / 2) kernel rows of two corpus rows each;
   // sx8 / e8 [rows8] the rows' scales and error norms; q8 [2][32][d] the queries' int8 pieces and q8s [4][32] their
   // scalars (launch_q8_prep)
@@ -102,6 +93,7 @@ struct SkArgs {
   const float* e8;
   int64_t rows8;
   int ct8;                 // tiles per chunk of the dynamic schedule (0: the kernel's default)
+  int no_guided;           // A/B (RR_SCREEN_GUIDED=0): every chunk CT tiles, no 2-tile chunks at the end
 };
 
 // Split-K streaming kernel (rr_sk.hip): same output contract as launch_fused. sdt = KDT_* (0..3).

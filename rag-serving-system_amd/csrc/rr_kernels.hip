@@ -844,74 +844,11 @@ __global__ __launch_bounds__(256) void f32_to_i8_kernel(const float* __restrict_
   }
 }
 
-// The int8 screen's query pieces, one wave per query slot: s = max|q| / 127, t = q / s, p1 = clamp(rint(t)), p2 =
-// clamp(rint((t - p1) * 64)) — q ~ s (p1 + p2 / 64), the MFMAs' sum being x8 . (64 p1 + p2) — and eq >= the
-// residual's norm (real arithmetic), in the scale's units as f32_to_i8_kernel: t - p1 - p2 / 64 is exact (each step
-// by Sterbenz), so |q - s (p1 + p2 / 64)|_2 <= s |t - p1 - p2/64|_2 (x 1 + 2^-12) + 2^-21 sqrt(d) max|q| + 2^-140.
-// |q| and sum|q| in fp32 (the bound bumps for their summation order). Slots >= b: zero pieces and scalars. One 64-lane
-// workgroup per slot: it runs beside the other stream's screen. (Quantising in the screen itself instead — every
-// workgroup redoing all 32 queries, two L2 passes — measured 8-13 us longer per launch than this launch:
-// profiles/r04/ab/int8/.)
+// The int8 screen's query pieces: one 64-lane workgroup per query slot (rr_device.h q8_prep_slot), launched in front of
+// a screen when the screen launch does not prep them itself (rr_sk.hip: its joiner workgroups do when they run).
 __global__ __launch_bounds__(64) void q8_prep_kernel(const float* __restrict__ q, int b, int d,
                                                      int8_t* __restrict__ q8, float* __restrict__ q8s) {
-  const int slot = blockIdx.x, lane = threadIdx.x;
-  int8_t* p1 = q8 + (size_t)slot * d;
-  int8_t* p2 = q8 + (size_t)(kQSlots + slot) * d;
-  if (slot >= b) {
-    for (int e = 4 * lane; e < d; e += 256) {
-      *(uint32_t*)(p1 + e) = 0;
-      *(uint32_t*)(p2 + e) = 0;
-    }
-    if (lane < 4) q8s[lane * kQSlots + slot] = 0.f;
-    return;
-  }
-  const f32x4* src = (const f32x4*)(q + (size_t)slot * d);
-  float m = 0.f, s2 = 0.f, s1 = 0.f;
-  for (int c = lane; c < (d >> 2); c += 64) {
-    const f32x4 v = src[c];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      m = fmaxf(m, fabsf(v[j]));
-      s2 = fmaf(v[j], v[j], s2);
-      s1 += fabsf(v[j]);
-    }
-  }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    m = fmaxf(m, __shfl_xor(m, off, 64));
-    s2 += __shfl_xor(s2, off, 64);
-    s1 += __shfl_xor(s1, off, 64);
-  }
-  const float s = m > 0.f ? m / 127.0f : 0.f;
-  float se = 0.f;
-  for (int c = lane; c < (d >> 2); c += 64) {
-    const f32x4 v = src[c];
-    uint32_t w1 = 0, w2 = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float a = 0.f, cc = 0.f, r = 0.f;
-      if (s > 0.f) {
-        const float t = v[j] / s;
-        a = fminf(fmaxf(rintf(t), -127.0f), 127.0f);
-        const float ta = t - a;   // exact
-        cc = fminf(fmaxf(rintf(ta * 64.0f), -127.0f), 127.0f);
-        r = ta - cc * 0x1p-6f;    // exact
-      }
-      w1 |= ((uint32_t)(int)a & 0xFFu) << (8 * j);
-      w2 |= ((uint32_t)(int)cc & 0xFFu) << (8 * j);
-      se = fmaf(r, r, se);
-    }
-    *(uint32_t*)(p1 + 4 * c) = w1;
-    *(uint32_t*)(p2 + 4 * c) = w2;
-  }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) se += __shfl_xor(se, off, 64);
-  if (lane == 0) {
-    q8s[slot] = sqrtf(s2);
-    q8s[kQSlots + slot] = s1 * (1.0f + 0x1p-18f);
-    q8s[2 * kQSlots + slot] = s * 0x1p-6f;
-    q8s[3 * kQSlots + slot] = fmaf(s * sqrtf(se), 1.0f + 0x1p-12f, fmaf(m, sqrtf((float)d) * 0x1p-21f, 0x1p-140f));
-  }
+  q8_prep_slot(q, b, d, q8, q8s, (int)blockIdx.x, (int)threadIdx.x);
 }
 
 __global__ void unsplit_f32_kernel(const u32x4* __restrict__ in, const float* __restrict__ rscale, int64_t n,

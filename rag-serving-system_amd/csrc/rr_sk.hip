@@ -410,234 +410,6 @@ __device__ __forceinline__ uint32_t wide_bar(uint64_t ek, uint64_t tb) {
   return ek != 0 && e > t ? e : t + 1;
 }
 
-// ---- Carried verify ------------------------------------------------------------------------------------------
-// A screen on the dynamic schedule (DT 7 / DT 8, SCHED 1, KT <= 16) can carry the PREVIOUS screened block's verify
-// (SkArgs::carry): workgroups [0, 32) verify one query slot each of that block — whose screen ended with the previous
-// launch, so its lists are complete — and then join this block's screen, taking chunks from the dynamic counter; the
-// other workgroups screen from the start. One launch per search block instead of a screen and a separate verify, and
-// the 32 verifying CUs stream corpus rows as soon as they are done. The verify is exactly MODE 1's (same candidates,
-// same exact DT 3 arithmetic: K split over the 8 waves, MFMA order, wave order of the partial sums, the cosine
-// quotient and clip; the same completeness proof and wide phase), so results are bit-identical. Registers: the
-// 9-wave screen's budget (168 VGPRs), so this verify keeps no per-lane lists — a tile's 32 exact keys go through LDS
-// and the top-KT is kept by rank selection — and splits the query from LDS per tile. The 9th wave (the screen's
-// scheduler) passes every barrier and does no work here.
-// LDS (free before the screen starts): [0, 16 KiB) the list merge's scratch, [16, 20 KiB) the query, [20 KiB, ring
-// end) the wide phase's rows; the screen's partial block (red) for the K-partials; the MODE 1 scalars block.
-constexpr int kCvQueryOff = 16384;
-constexpr int kCvWideOff = 20480;
-constexpr int kCvWideCap = (int)((ring_bytes(2) - kCvWideOff) / 4);
-
-template <int NSV, int KT, bool COS>
-__device__ __forceinline__ void carry_verify(const SkArgs& a, const int vq, char* smem, float* red, float* qinfo,
-                                             uint64_t* akeys, int* grow, float* gnorm, int* gvalid, uint64_t* xk,
-                                             uint64_t* vfloor, uint64_t* vtail, int* vstate, uint64_t* tkeys) {
-  constexpr int QS = 32;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
-  const bool sw = w < kWaves;   // a streaming wave (not the scheduler)
-  const int d = a.d;
-  const uint32_t idx_base = a.idx_base;
-  const char* __restrict__ vcorpus = a.vcorpus;
-  const int row_bytes = d * 4;
-  constexpr int KSV = NSV * kSlabRowBytes;   // bytes of a row per wave (fp32 rows)
-  const int p0 = w * (KSV / 16);
-  float* qv = (float*)(smem + kCvQueryOff);
-  int* wl = (int*)(smem + kCvWideOff);
-  if (vq >= a.vb) {   // padding slot: keep the exchange buffer uniform
-    if (a.out_keys && tid < KT) a.out_keys[(size_t)vq * KT + tid] = 0;
-    return;
-  }
-  // the query into LDS; |q| and max |q| by wave 0 exactly as the exact pass computes them
-  const float* __restrict__ vqs = a.vqueries;
-  for (int e = 4 * tid; e < d; e += 4 * kThreads) *(f32x4*)(qv + e) = *(const f32x4*)(vqs + (size_t)vq * d + e);
-  if (w == 0) {
-    const int nc = d >> 2;
-    f32x4 v[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int cc = lane + 64 * c;
-      v[c] = zero_unless(((const f32x4*)vqs)[(size_t)vq * nc + (cc < nc ? cc : 0)], opaque_mask(cc < nc));
-    }
-    float ss = 0.f, m = 0.f;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (lane + 64 * c < nc) {
-        const f32x4 x = v[c];
-        ss = fmaf(x.x, x.x, ss); ss = fmaf(x.y, x.y, ss); ss = fmaf(x.z, x.z, ss); ss = fmaf(x.w, x.w, ss);
-        m = fmaxf(m, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
-      }
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      ss += __shfl_xor(ss, off, 64);
-      m = fmaxf(m, __shfl_xor(m, off, 64));
-    }
-    if (lane == 0) {
-      qinfo[vq] = sqrtf(ss);
-      qinfo[QS + vq] = m;
-    }
-  }
-  __syncthreads();
-  const float qn = qinfo[vq];
-  merge_lists_for_query<KT>(a.vin, a.nlists, QS, vq, (uint64_t*)smem, akeys, vfloor, vtail);
-  if (tid < 32) {
-    const uint64_t k0 = akeys[0];
-    const uint64_t key = tid < KT ? akeys[tid] : 0;
-    const int64_t first = k0 ? (int64_t)(0xFFFFFFFFu - (uint32_t)k0) - idx_base : 0;
-    const int64_t row = key ? (int64_t)(0xFFFFFFFFu - (uint32_t)key) - idx_base : first;
-    grow[tid] = (int)row;
-    gvalid[tid] = key != 0;
-    gnorm[tid] = COS ? a.norms[row] : 0.f;
-  }
-  if (tid < KT) xk[tid] = 0;
-  __syncthreads();
-
-  // exact keys of the 32 rows grow[] (gvalid: 0 -> key 0) into tkeys[]: the DT 3 tile of the full pass with query vq
-  auto score_tile = [&]() {
-    if (sw) {
-      const char* src = vcorpus + (int64_t)grow[r] * row_bytes + (size_t)w * KSV;
-      f32x4 vr[NSV][4];
-#pragma unroll
-      for (int j = 0; j < NSV; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          vr[j][i] = *(const f32x4*)(src + j * kSlabRowBytes + ((4 * (i >> 1) + 2 * h + (i & 1)) << 4));
-      f32x16 acc;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-#pragma unroll
-      for (int j = 0; j < NSV; ++j)
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const float x[8] = {vr[j][2 * t].x, vr[j][2 * t].y, vr[j][2 * t].z, vr[j][2 * t].w,
-                              vr[j][2 * t + 1].x, vr[j][2 * t + 1].y, vr[j][2 * t + 1].z, vr[j][2 * t + 1].w};
-          bf16x8 b0, b1, b2, c0, c1, c2;
-          split3(x, b0, b1, b2);
-          const f32x4 qa = *(const f32x4*)(qv + 4 * inv_pair(p0 + 8 * j + 4 * t + 2 * h));
-          const f32x4 qb = *(const f32x4*)(qv + 4 * inv_pair(p0 + 8 * j + 4 * t + 2 * h + 1));
-          const float qx[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
-          split3(qx, c0, c1, c2);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c0, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c1, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c0, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, c1, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, c2, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, c0, acc, 0, 0, 0);
-        }
-      // every column holds query vq: column 0's partials (lanes 0 and 32: docs 8a + 4h + i), summed in wave order
-      if (r == 0) {
-#pragma unroll
-        for (int a4 = 0; a4 < 4; ++a4)
-          *(f32x4*)(red + w * 32 + 8 * a4 + 4 * h) = (f32x4){acc[4 * a4], acc[4 * a4 + 1], acc[4 * a4 + 2], acc[4 * a4 + 3]};
-      }
-    }
-    __syncthreads();
-    if (tid < 32) {
-      float sv = red[tid];
-#pragma unroll
-      for (int ww = 1; ww < kWaves; ++ww) sv = sv + red[ww * 32 + tid];
-      uint64_t key = 0;
-      if (gvalid[tid]) {
-        float c = sv;
-        if constexpr (COS) {
-          c = c / cos_den(qn, gnorm[tid]);   // IEEE division then clip, as every exact path (retriever.py:605-609)
-          c = fminf(fmaxf(c, -1.0f), 1.0f);
-        }
-        key = make_key(c, idx_base + (uint32_t)grow[tid]);
-      }
-      tkeys[tid] = key;
-    }
-    __syncthreads();
-  };
-  // the running top-KT (xk, descending) and the tile's keys -> the new top-KT, by rank (keys are unique but for 0)
-  auto merge_tile = [&]() {
-    uint64_t me = 0;
-    if (tid < KT + 32) me = tid < KT ? xk[tid] : tkeys[tid - KT];
-    int rank = 0;
-    if (me != 0) {
-      for (int i = 0; i < KT; ++i) rank += xk[i] > me ? 1 : 0;
-      for (int i = 0; i < 32; ++i) rank += tkeys[i] > me ? 1 : 0;
-    }
-    __syncthreads();
-    if (tid < KT) xk[tid] = 0;
-    __syncthreads();
-    if (me != 0 && rank < KT) xk[rank] = me;
-    __syncthreads();
-  };
-  auto finish = [&](bool complete) {   // (thread 0)
-    complete = complete && qinfo[QS + vq] < 32768.0f && !a.force_incomplete;
-    if (!complete)
-      if (__hip_atomic_fetch_max(a.flag, (uint64_t)a.vseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint64_t)a.vseq)
-        __hip_atomic_fetch_add(a.count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (vq == 0) __hip_atomic_fetch_add(a.count + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (a.out_keys)
-      for (int i = 0; i < KT; ++i) a.out_keys[(size_t)vq * KT + i] = xk[i];
-    if (a.out_scores)
-      for (int i = 0; i < a.k_out; ++i) {
-        const uint64_t key = xk[i];
-        a.out_scores[(size_t)vq * a.k_out + i] = key ? float_of_ord((uint32_t)(key >> 32)) : -INFINITY;
-        a.out_idx[(size_t)vq * a.k_out + i] = key ? (int64_t)(0xFFFFFFFFu - (uint32_t)key) : -1;
-      }
-  };
-
-  score_tile();
-  merge_tile();
-  if (tid == 0) {
-    const uint64_t ukt = umax64(akeys[KT - 1], *vfloor);
-    const uint64_t ek = xk[a.k_out - 1];
-    const bool complete = ukt == 0 || (ek != 0 && (uint32_t)(ek >> 32) > (uint32_t)(ukt >> 32));
-    const uint64_t tb = *vtail;
-    const bool wide = !complete && a.wide_verify && !a.force_incomplete && qinfo[QS + vq] < 32768.0f &&
-                      ((uint32_t)(ek >> 32) > (uint32_t)(tb >> 32) ||
-                       (uint32_t)(akeys[a.k_out - 1] >> 32) > (uint32_t)(tb >> 32));
-    vstate[0] = wide ? 1 : 0;
-    vstate[1] = 0;
-    vstate[4] = (int)wide_bar(ek, tb);
-    if (!wide) finish(complete);
-  }
-  __syncthreads();
-  if (vstate[0] != 1) return;
-
-  // wide phase (MODE 1's): every list entry whose bound reaches wide_bar, rescored exactly
-  const uint32_t tb_ord = (uint32_t)(*vtail >> 32);
-  const uint32_t rbar = (uint32_t)vstate[4];
-  for (int l = tid; l < a.nlists; l += kThreads) {
-    const uint64_t* src = a.vin + ((size_t)vq * a.nlists + l) * (KT + 1);
-    int c = 0;
-    while (c < KT && (uint32_t)(src[c] >> 32) >= rbar) ++c;   // a prefix of the sorted list
-    if (c) {
-      const int pos = atomicAdd(&vstate[1], c);
-      for (int i = 0; i < c; ++i)
-        if (pos + i < kCvWideCap) wl[pos + i] = (int)((int64_t)(0xFFFFFFFFu - (uint32_t)src[i]) - idx_base);
-    }
-  }
-  __syncthreads();
-  const int nr = vstate[1];
-  if (nr > kCvWideCap) {
-    if (tid == 0) finish(false);
-    return;
-  }
-  if (tid < KT) xk[tid] = 0;
-  __syncthreads();
-  for (int t = 0; t < (nr + 31) / 32; ++t) {
-    if (tid < 32) {
-      const int i = 32 * t + tid;
-      const int row = wl[i < nr ? i : 0];
-      grow[tid] = row;
-      gvalid[tid] = i < nr;
-      gnorm[tid] = COS ? a.norms[row] : 0.f;
-    }
-    __syncthreads();
-    score_tile();
-    merge_tile();
-  }
-  if (tid == 0) {
-    const uint64_t ek = xk[a.k_out - 1];
-    const bool complete = tb_ord == 0 || (ek != 0 && (uint32_t)(ek >> 32) > tb_ord);
-    if (complete && a.wide_count) __hip_atomic_fetch_add(a.wide_count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    finish(complete);
-  }
-}
-
 // QH = query halves: 32 * QH query slots per pass (64 for the batch-64 configs: one corpus pass serves
 // them all; each A fragment then feeds the MFMAs of both halves).
 // MODE 0: top-KT per query over this workgroup's rows (DT 6: by upper bound).
@@ -704,18 +476,6 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   uint64_t* vfloor = xk + KT;   // MODE 1: the largest floor of the screen's lists (see KL)
   uint64_t* vtail = vfloor + 1; // MODE 1: the largest bound of any single list, max(KT-th key, floor) (wide verify)
   int* vstate = (int*)(vtail + 1);   // MODE 1: [0] what the leader decided after the first check, [1] |R|, [4] R's bar
-  // ---- carried verify (see carry_verify): workgroups [0, 32) verify the previous block's query slots first, then
-  // join this screen on the dynamic counter (NJ of them: no static first chunk)
-  constexpr bool CARRY = MODE == 0 && SCHED == 1 && QH == 1 && (DT == 7 || DT == 8) && KT <= 16;
-  const int NJ = CARRY && a.carry ? kQSlots : 0;   // joiners
-  const bool joiner = (int)blockIdx.x < NJ;
-  if constexpr (CARRY) {
-    if (joiner) {
-      carry_verify<2 * NS, KT, COS>(a, (int)blockIdx.x, smem, red, qinfo, akeys, grow, gnorm, gvalid, xk, vfloor, vtail,
-                                    vstate, vW);
-      __syncthreads();   // (the verify's LDS is the screen's from here)
-    }
-  }
   // MODE 1 reads its 32 gathered rows straight into registers (all loads issued at once: one latency), the
   // exact fragments the LDS image would give: lane (r, h) takes 16-byte units 4(i>>1) + 2h + (i&1) of slab j
   f32x4 vrow[MODE == 1 ? NS : 1][4];
@@ -734,9 +494,17 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // the int8 screen: a.ct8 tiles (of 64 corpus rows) per chunk — 2 on small shards, where a 4-tile chunk is a large
   // share of a workgroup's work and the last ones leave a tail (profiles/r04/ab/ab_ct8.txt), else 4
   const int CT = DT == 8 && a.ct8 > 0 ? a.ct8 : CT0;
-  // the statically scheduled workgroups: G of them, workgroup g's first chunk is chunk g (joiners: g < 0)
-  const int64_t G = (int64_t)gridDim.x - NJ, g = (int64_t)blockIdx.x - NJ;
-  const int64_t T = (n + 31) / 32, C = (T + CT - 1) / CT;
+  const int64_t G = gridDim.x, g = blockIdx.x;
+  // Guided tail: chunks of CT tiles, then (CT > 2) the last ~2 G tiles in 2-tile chunks, so the launch's last chunks —
+  // the tail where workgroups finish at different times — are short (tools/probe_screen.hip: the 1M-row int8 screen's
+  // workgroups ended over 9 us with 4-tile chunks throughout). Chunk c: first tile cbase(c), ctiles(c) tiles; every
+  // chunk but the last has >= 2 tiles (the scheduler wave's next-chunk word is read at a chunk's last tile).
+  const int64_t T = (n + 31) / 32;
+  const int CT2 = CT > 2 ? 2 : CT;
+  const int64_t T1 = CT > 2 && T > 2 * G && !a.no_guided ? (T - 2 * G) / CT * CT : 0;   // tiles in CT-tile chunks
+  const int64_t C1 = T1 / CT, C = C1 + (T - T1 + CT2 - 1) / CT2;
+  auto cbase = [&](int64_t c) -> int64_t { return c < C1 ? c * CT : T1 + (c - C1) * CT2; };
+  auto ctiles = [&](int64_t c) -> int { return c < C1 ? CT : (int)(T - cbase(c) < CT2 ? T - cbase(c) : CT2); };
 
   // LDS-DMA lane mapping: instruction i of a slab covers tile rows 8i + lane/8, 16-byte column
   // (lane % 8) ^ (lane / 8) of the slab — so the image holds column c of row r at c ^ (r & 7)
@@ -797,30 +565,18 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       // The scheduler wave (a 9th wave: no corpus, no query, no inline-asm loads, so hipcc's own waits around
       // its atomic drain nothing else). Per chunk it takes the next free chunk from the counter and publishes
       // it in nxt[] before the chunk's first reduction barrier; the streaming waves read it at the chunk's last
-      // step. It passes exactly the barriers the streaming waves pass: (a joiner's first-chunk barrier,) one after the
-      // query scalars, one per tile.
-      int64_t ck = g;
-      if (joiner) {   // a joiner's first chunk from the counter, published to the streaming waves (nxt[2])
-        if (lane == 0) {
-          const uint32_t old = __hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const int64_t nc = G + (int64_t)old;
-          nxt[2] = (int)(nc < C ? nc : C);
-          if ((int64_t)old == C - 2 + NJ) __hip_atomic_store(a.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        ck = nxt[2];
-      }
+      // step. It passes exactly the barriers the streaming waves pass: one after the query scalars, one per tile.
       __syncthreads();
+      int64_t ck = g;
       int cp = 0;
       while (ck < C) {
-        const int tic = (int)(C - ck == 1 ? T - ck * CT : CT);
+        const int tic = ctiles(ck);
         if (ck != C - 1 && lane == 0) {   // every chunk but the last asks once: C - 1 dequeues per launch
           const uint32_t old = __hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           const int64_t nc = G + (int64_t)old;
           nxt[cp] = (int)(nc < C ? nc : C);
-          // the launch's last dequeue resets the counter for the next launch on this stream: every chunk but the last
-          // asks once, and so does every joiner for its first chunk — C - 1 + NJ dequeues per launch
-          if ((int64_t)old == C - 2 + NJ) __hip_atomic_store(a.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // the launch's last dequeue resets the counter for the next launch on this stream
+          if ((int64_t)old == C - 2) __hip_atomic_store(a.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         for (int t = 0; t < tic; ++t) lds_barrier();
         if (ck == C - 1) break;
@@ -842,14 +598,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #endif
   constexpr int LA = NS >= 2 ? (QH == 1 ? RR_SK_LOOKAHEAD : RR_SK_LA64) : 1;   // (64 slots: measured faster with 1)
   int pend = 0;   // LA 2: vector-memory ops this wave issued after the slab it waits for next
-  int64_t chunk = g;
-  if constexpr (CARRY) {
-    if (joiner) {   // (the scheduler wave published this joiner's first chunk)
-      __syncthreads();
-      chunk = nxt[2];
-    }
-  }
-  int64_t base = chunk * CT * 32;
+  int64_t chunk = g, base = cbase(chunk) * 32;
   if constexpr (MODE == 0) {
     if (chunk < C) {   // prologue: the first tile's factors and slab 0 (and 1)
       if (FX && w == 0) issue_factors(base, 0);
@@ -1002,10 +751,20 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         }
       }
   };
+  // the int8 screen's per-query scalars of this lane's epilogue query (qe below), loaded with the fragments: one
+  // latency before the first barrier instead of a second one after it
+  float q8pre[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (DT == 8) {
+    const int qe0 = 4 * w + lane / 16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q8pre[i] = a.q8s[i * 32 + qe0];
+  }
+  if constexpr (MODE == 0) SK_PROBE(6);   // (diagnostic builds: prologue issued, before the fragments)
   if constexpr (DT != 2) {
     build_frags();
     pin_frags();
   }
+  if constexpr (MODE == 0) SK_PROBE(7);   // (fragments in registers)
   // ---- per-query scalars: |q| (cosine, fp32 as cp.linalg.norm, retriever.py:602), split exponents (DT 2),
   // sum |q| (DT 6 bound), max |q| (MODE 1: the screen's f16 range). All loads of a group of 4 queries are
   // issued before any is used (one L2/HBM latency per group, not one per query); the sums are the same
@@ -1146,12 +905,12 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   const float qs = DT == 2 ? qinfo[QS + qe] : 1.f;
   float qsa = 0.f, q8sc = 0.f, q8e1 = 0.f, q8e2 = 0.f, q8e3 = 0.f;
   if constexpr (DT == 8) {
-    qn = a.q8s[qe];
-    qsa = a.q8s[QS + qe];
-    q8sc = a.q8s[2 * QS + qe];
+    qn = q8pre[0];   // (a.q8s[i * QS + qe], loaded before the first barrier)
+    qsa = q8pre[1];
+    q8sc = q8pre[2];
     // the bound's slack e Q1 + |x| Q2 + Q3 (see the epilogue), its per-query factors once: all terms are positive and
     // each is rounded a few times, which the 1.001 margin covers
-    const float eq = a.q8s[3 * QS + qe];
+    const float eq = q8pre[3];
     q8e1 = (qn + eq) * 1.001f;
     q8e2 = (eq + fmaf(a.eps_a, qn, a.eps_b * a.sqrt_d)) * 1.001f;
     // + 2^-110 absolute: the exact DT 3 score's products that fall below fp32's normal range, and every rounding of
@@ -1481,7 +1240,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   int64_t tcount = 0;                       // tiles done (reduction buffer parity)
   bool run = MODE == 1 || chunk < C;
   while (run) {
-    const int tic = MODE == 1 ? 1 : (int)(C - chunk == 1 ? T - chunk * CT : CT);   // tiles in this chunk
+    const int tic = MODE == 1 ? 1 : ctiles(chunk);   // tiles in this chunk
     const bool last_in_chunk = ti + 1 == tic;
     int64_t next_chunk = C, next_base = -1;
     f32x16 accs[QH];
@@ -1507,7 +1266,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         } else {   // (SCHED: nxt[] was published before this chunk's first tile barrier; a chunk with a
                    // successor has >= 2 tiles, so that barrier is behind us)
           next_chunk = !SCHED ? chunk + G : chunk == C - 1 ? C : (int64_t)nxt[cpar];
-          next_base = next_chunk < C ? next_chunk * CT * 32 : -1;
+          next_base = next_chunk < C ? cbase(next_chunk) * 32 : -1;
         }
         if (next_base >= 0) {
           if (FX && w == 0) {
@@ -1544,7 +1303,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
             next_base = base + 32;
           } else {
             next_chunk = !SCHED ? chunk + G : chunk == C - 1 ? C : (int64_t)nxt[cpar];
-            next_base = next_chunk < C ? next_chunk * CT * 32 : -1;
+            next_base = next_chunk < C ? cbase(next_chunk) * 32 : -1;
           }
           if (next_base >= 0) {
             if (FX && w == 0) {
@@ -1672,7 +1431,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       chunk = next_chunk;
       ti = 0;
       cpar ^= 1;
-      base = chunk * CT * 32;
+      base = cbase(chunk) * 32;
       continue;
     }
 #endif
@@ -1722,7 +1481,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       chunk = next_chunk;
       ti = 0;
       cpar ^= 1;
-      base = chunk * CT * 32;
+      base = cbase(chunk) * 32;
     }
   }
   if (defer && bsd >= 0) epilogue(svd, bsd, tsd);   // the last tile's deferred epilogue
@@ -1768,7 +1527,6 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     // the screen's lists go query-major, [QS][grid][KT + 1] — KT keys, then the workgroup's floor (see KL): each
     // verify workgroup then reads its query's lists as one contiguous block (the other paths' merge_kernel reads
     // [grid][QS][KT])
-    // (one list per workgroup of the launch, joiners included: list slot = blockIdx.x of gridDim.x)
     uint64_t* dst = a.out + (SCR ? ((size_t)qe * gridDim.x + blockIdx.x) * (KT + 1)
                                  : ((size_t)blockIdx.x * QS + qe) * KT);
     if constexpr (SCR) {   // before any pop: a full lane's last entry bounds every key it dropped
@@ -2034,6 +1792,7 @@ int sk_slabs(int sdt, int d) {
   return (ns >= 1 && ns <= (eb == 2 ? 2 : 4)) ? ns : 0;
 }
 
+#ifndef RR_SK_NO_DISPATCH   // (diagnostic tools that instantiate one kernel directly: tools/probe_screen.hip)
 hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int qslots, const SkArgs& a,
                           hipStream_t s, int ring) {
   const int ns = sk_slabs(sdt == KDT_SCREEN ? KDT_F32_X3 : sdt, a.d);
@@ -2045,10 +1804,6 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
   }
   // the screen: dynamic schedule (9-wave form) when asked for and the lists fit its registers; short or full
   // per-lane lists (a.full_lists)
-  // a carried verify (a.carry): the f16 / int8 copy's screen on the dynamic schedule, KT <= 16, more than 32 workgroups
-  if (a.carry && (sdt == KDT_SCREEN || !(a.dyn && a.ctr && kt <= 16) || grid <= kQSlots || !a.vin || !a.vqueries ||
-                  !a.vcorpus || a.vb < 1 || a.vb > kQSlots))
-    return hipErrorInvalidValue;
   if (sdt == KDT_SCREEN) {
     if (qslots != 32 || ring != 2) return hipErrorInvalidValue;
     const bool dyn = a.dyn && a.ctr && kt <= 16;
@@ -2117,6 +1872,8 @@ hipError_t launch_sk(int sdt, int metric, int kt, int grid, const void* c, const
   a.out = cand;
   return launch_sk_args(sdt, metric, kt, 0, grid, qslots, a, s, ring);
 }
+
+#endif   // RR_SK_NO_DISPATCH
 
 }  // namespace rr
 

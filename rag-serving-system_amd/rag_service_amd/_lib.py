@@ -80,7 +80,6 @@ SIGNATURES = {
     "rr_screen_copy": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_i32)]),
     "rr_screen_int8": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_i32)]),
     "rr_set_compute_streams": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_i32)]),
-    "rr_set_carry_verify": (_c_int, [_vp, _c_i32, ctypes.POINTER(_c_i32)]),
     "rr_last_shape": (_c_int, [_vp, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i32)]),
     "rr_dist_info": (_c_int, [_vp, _ip, _ip]),
     "rr_screen_counts": (_c_int, [_vp, _i64p, _i64p, _i64p, _i64p]),
@@ -332,13 +331,6 @@ class Index:
         u = _c_i32()
         _check(self._lib.rr_set_compute_streams(self._h, -1 if n is None else int(n), ctypes.byref(u)))
         return u.value
-
-    def carry_verify(self, on: Optional[bool] = None) -> bool:
-        """Carried verify (the default): each screened block's exact verify rides in the next screened block's launch
-        (one compute stream; results identical); None leaves the setting. Returns the setting."""
-        u = _c_i32()
-        _check(self._lib.rr_set_carry_verify(self._h, -1 if on is None else int(bool(on)), ctypes.byref(u)))
-        return bool(u.value)
 
     def screen_copy(self, use: Optional[bool] = None) -> bool:
         """The screened search's f16 copy of fp32 rows (half the bytes per screen pass; results unchanged):

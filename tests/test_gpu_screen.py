@@ -501,23 +501,20 @@ def test_narrow_lists_switch_to_wide(Index):
 
 
 @pytest.mark.parametrize("devices", [[0], [0, 0]])
-def test_carry_and_two_streams_match_one(Index, devices, monkeypatch):
-    """The screened search's three enqueue forms give, step by step, exactly the same results: the carried verify
-    (the default: each block's verify rides in the next screened block's launch, flushed when results are needed),
-    two alternating compute streams (carry off), and one stream with a verify launch per block. A mixed sequence of
-    staged searches (several back to back, then fetched), multi-block batches, list widths that change between
-    searches (a pending verify of another width is flushed), another kind of search in between (k = 40), and four
-    asynchronous searches in flight, forced re-runs included."""
+def test_two_compute_streams_match_one(Index, devices):
+    """Screened blocks alternate between two compute streams (the default): a mixed sequence of staged searches
+    (several back to back, then fetched), multi-block batches, list widths that change between searches, another kind
+    of search in between (k = 40), and four asynchronous searches in flight, forced re-runs included, gives, step by
+    step, exactly the one-stream results."""
     corpus = synth.unit_norm_gaussian(31, 40000, 1024)
     qa = synth.unit_norm_gaussian(32, 32, 1024)
     qb = synth.unit_norm_gaussian(33, 77, 1024)
     qs = [synth.unit_norm_gaussian(34 + i, 1 + 19 * i, 1024) for i in range(6)]
 
-    def run(mode):
+    def run(streams):
         ix = Index(devices=devices, dtype="fp32", metric="cosine")
         ix.load(corpus)
-        assert ix.carry_verify(mode == "carry") == (mode == "carry")
-        assert ix.compute_streams(2 if mode == "two" else 1) == (2 if mode == "two" else 1)
+        assert ix.compute_streams(streams) == streams
         out = []
         ix.set_queries(qa)
         for k in (5, 5, 7):
@@ -528,7 +525,7 @@ def test_carry_and_two_streams_match_one(Index, devices, monkeypatch):
         ix.search_staged(3)
         out.append(ix.fetch())
         ix.set_queries(qa)
-        for k in (5, 2, 2, 5):                     # list widths 16, 8, 8, 16: carried, flushed, carried, flushed
+        for k in (5, 2, 2, 5):                     # list widths 16, 8, 8, 16
             ix.search_staged(k)
         out.append(ix.fetch())
         out.append(ix.search(qa, 40))            # large k: another kind of search between screened ones
@@ -556,56 +553,5 @@ def test_carry_and_two_streams_match_one(Index, devices, monkeypatch):
         ix.close()
         return out
 
-    ref = run("one")
-    for mode in ("carry", "two"):
-        for (s1, i1), (s2, i2) in zip(ref, run(mode)):
-            assert np.array_equal(i1, i2) and np.array_equal(s1, s2), mode
-
-
-@pytest.mark.parametrize("i8", [False, True])
-@pytest.mark.parametrize("exchange", [False, True])
-@pytest.mark.parametrize("layout", ["interleaved", "contiguous"])
-def test_carried_verify_matches_separate_verify(Index, layout, exchange, i8, monkeypatch):
-    """The carried verify (rr_sk.hip carry_verify: 32 workgroups of block i + 1's screen launch verify block i, then
-    join the screen) against a verify launch per block (RR_CARRY_VERIFY=0), through the f16 copy and the int8 copy
-    (i8: RR_SCREEN_I8_MIN_ROWS=0), with and without an exchange step (a 1-rank RCCL communicator: the carried block's
-    keys are exchanged after the launch that verified them). On near-duplicate clusters — interleaved: the wide phase
-    proves the query slots; contiguous: blocks flag and re-run exactly — both handles return the exact kernel's
-    results bit for bit, for single searches and back-to-back staged ones, and count the same screened blocks."""
-    from rag_service_amd import get_unique_id
-    corpus, q = _clustered(60000, 0.01, layout)
-    ex = Index(dtype="fp32", metric="cosine")
-    ex.load(corpus)
-    ex.set_kernel("exact")
-    counts = {}
-    for carry in (True, False):
-        monkeypatch.setenv("RR_CARRY_VERIFY", "1" if carry else "0")
-        if i8:
-            monkeypatch.setenv("RR_SCREEN_I8_MIN_ROWS", "0")
-        ix = Index(dtype="fp32", metric="cosine")
-        monkeypatch.delenv("RR_CARRY_VERIFY")
-        monkeypatch.delenv("RR_SCREEN_I8_MIN_ROWS", raising=False)
-        if exchange:
-            ix.init_dist(1, 0, get_unique_id())
-        ix.load(corpus)
-        assert ix.carry_verify() == carry and ix.screen_int8() == i8
-        for k in (5, 10):
-            want = ex.search(q, k)
-            got = ix.search(q, k)
-            assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), (carry, k)
-            ix.set_queries(q)
-            for _ in range(6):
-                ix.search_staged(k)
-            got = ix.fetch()
-            assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), (carry, k, "staged")
-        counts[carry] = ix.screen_counts_all()
-        ix.close()
-    print(layout, exchange, i8, counts)
-    blocks, flagged, reruns, wide = counts[True]
-    assert blocks == counts[False][0] == 14
-    assert reruns <= flagged          # (a flagged staged search that nobody fetched is superseded, not re-run)
-    if layout == "contiguous":
-        assert flagged >= 1 and reruns >= 1 and counts[False][1] >= 1
-    elif not i8:                      # the f16 copy's wide phase proves every interleaved block either way
-        assert flagged == counts[False][1] == 0 and wide >= 32 and counts[False][3] >= 32
-    ex.close()
+    for (s1, i1), (s2, i2) in zip(run(1), run(2)):
+        assert np.array_equal(i1, i2) and np.array_equal(s1, s2)
