@@ -235,6 +235,12 @@ int rr_screen_copy(rr_handle* h, int32_t use, int32_t* present);
  * the next search screens the int8 copy on every local shard. */
 int rr_screen_int8(rr_handle* h, int32_t use, int32_t* active);
 
+/* Repair mode (the adaptive screen's answer to corpora whose near-duplicate clusters defeat the screen's lists; see
+ * rr_screen_state): query slots, summed over local shards since the corpus was (re)loaded, that the verify could not
+ * prove and the in-stream repair pass completed instead — the rows of every chunk whose screen bound reaches the
+ * slot's exact k-th score rescored exactly, no host re-run. Synchronises the handle's streams. */
+int rr_screen_repairs(rr_handle* h, int64_t* repaired_slots);
+
 /* Screened-search counters since the corpus was (re)loaded: search blocks screened (summed over local
  * shards) and how many of them needed the exact fallback pass. Synchronises the handle's streams. */
 int rr_screen_stats(rr_handle* h, int64_t* blocks, int64_t* fallbacks);
@@ -246,8 +252,10 @@ int rr_screen_stats(rr_handle* h, int64_t* blocks, int64_t* fallbacks);
  * settles the last search. Any pointer may be null. */
 int rr_screen_counts(rr_handle* h, int64_t* blocks, int64_t* flagged, int64_t* reruns, int64_t* wide_slots);
 
-/* The screen's adaptive state (fp32 storage): *full_lists = 1 once re-run blocks made the handle switch the screen's
- * per-lane lists from 4 keys (+ a floor) to the full list width; *pause_left = search blocks still to run with the
+/* The screen's adaptive state (fp32 storage): *full_lists = 1 once re-run blocks made the handle switch to REPAIR
+ * MODE — the screen keeps full per-lane lists (instead of 4 keys + a floor) and records per chunk of rows the largest
+ * bound, and a query slot the verify cannot prove is completed in-stream by rescoring exactly the rows of the chunks
+ * whose bound reaches its exact k-th score (rr_screen_repairs), not by a host re-run; *pause_left = search blocks still to run with the
  * one-pass exact kernel because the screen could not prune this corpus; *pauses = how often that happened. Decided
  * from the searches whose results were collected (rr_fetch_results, rr_synchronize, rr_search, rr_wait), whose
  * completeness flag is exchanged between shards: every rank of a world decides identically. Reset at every load.

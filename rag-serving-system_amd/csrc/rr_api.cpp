@@ -111,7 +111,16 @@ struct Shard {
   int cand_grid = 0;                     // alternates the halves by parity; the other paths use half 0)
   int* scount = nullptr;                 // screened search: [0] blocks this shard flagged for the exact pass,
                                          // [1] blocks its verify completed
-  int* wcount = nullptr;                 // ... query slots its verify proved in the wide phase
+  int* wcount = nullptr;                 // ... [0] query slots its verify proved in the wide phase, [1] query slots
+                                         // the repair pass completed (repair mode)
+  // Repair mode (rr_sk.hip "Repair"; observe_settled), per candidate half (block parity): per-chunk maxima of the
+  // bound [chunks][32], the verify's chunk marks, their compacted list and its count; made at the first repair-mode
+  // block for up to rcap chunks (every chunk geometry of this shard)
+  uint32_t* rcmax[2] = {nullptr, nullptr};
+  uint32_t* rbits[2] = {nullptr, nullptr};
+  int* rlist[2] = {nullptr, nullptr};
+  int* rcnt[2] = {nullptr, nullptr};
+  int64_t rcap = 0;
   int* pin_scount = nullptr;             // pinned staging of scount / wcount reads (rr_screen_counts)
   uint32_t* ctr = nullptr;               // split-K chunk counters (dynamic schedule), 0 between launches: one per
                                          // compute stream, kCtrStride words apart; then (words 2 and 3 x kCtrStride)
@@ -391,7 +400,8 @@ int dmalloc(T** p, size_t bytes) {
 int free_shard(Shard& s) {
   hipSetDevice(s.dev);
   void* ptrs[] = {s.corpus, s.scr16, s.scr8, s.sx8, s.e8, s.q8[0], s.q8[1], s.q8s[0], s.q8s[1], s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.wcount, s.ctr, s.shard_keys, s.gathered, s.out_base,
-                  s.full_keys, s.sort_temp, s.wcand, s.wfloor, s.wsel};
+                  s.full_keys, s.sort_temp, s.wcand, s.wfloor, s.wsel, s.rcmax[0], s.rcmax[1], s.rbits[0], s.rbits[1],
+                  s.rlist[0], s.rlist[1], s.rcnt[0], s.rcnt[1]};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (int x = 0; x < kXSlots; ++x) {
@@ -657,7 +667,9 @@ int drop_work_buffers(rr_handle* h) {
     s.last_vsi = -1;
     void** ptrs[] = {(void**)&s.qbuf[0], (void**)&s.qbuf[1], (void**)&s.cand, (void**)&s.scount, (void**)&s.wcount, (void**)&s.ctr, (void**)&s.shard_keys, (void**)&s.gathered,
                      (void**)&s.out_base, (void**)&s.full_keys, &s.sort_temp,
-                     (void**)&s.wcand, (void**)&s.wfloor, (void**)&s.wsel};
+                     (void**)&s.wcand, (void**)&s.wfloor, (void**)&s.wsel, (void**)&s.rcmax[0], (void**)&s.rcmax[1],
+                     (void**)&s.rbits[0], (void**)&s.rbits[1], (void**)&s.rlist[0], (void**)&s.rlist[1],
+                     (void**)&s.rcnt[0], (void**)&s.rcnt[1]};
     for (void** p : ptrs) {
       if (*p) HIP_TRY(hipFree(*p));
       *p = nullptr;
@@ -668,6 +680,7 @@ int drop_work_buffers(rr_handle* h) {
         *p = nullptr;
       }
     s.q_cap = s.k_cap = s.cand_grid = 0;
+    s.rcap = 0;
     s.full_cap = s.sort_temp_bytes = 0;
     s.out_scores = nullptr;
     s.out_idx = nullptr;
@@ -759,8 +772,8 @@ int ensure_buffers(rr_handle* h, int b, int k) {
       if (int rc = dmalloc(&s.cand, 2 * cand_half(s) * 8)) return rc;
       if (int rc = dmalloc(&s.scount, 2 * sizeof(int))) return rc;
       HIP_TRY(hipMemset(s.scount, 0, 2 * sizeof(int)));
-      if (int rc = dmalloc(&s.wcount, sizeof(int))) return rc;
-      HIP_TRY(hipMemset(s.wcount, 0, sizeof(int)));
+      if (int rc = dmalloc(&s.wcount, 2 * sizeof(int))) return rc;
+      HIP_TRY(hipMemset(s.wcount, 0, 2 * sizeof(int)));
       if (!s.pin_scount) HIP_TRY(hipHostMalloc((void**)&s.pin_scount, 2 * sizeof(int), hipHostMallocDefault));
       ((volatile int*)s.pin_scount)[0] = ((volatile int*)s.pin_scount)[1] = 0;
       if (int rc = dmalloc(&s.ctr, 4 * kCtrStride * sizeof(uint32_t))) return rc;
@@ -871,16 +884,15 @@ bool screened(const rr_handle* h, int k, int slots) {
 // narrow -> wide switch under rr_init_dist. A staged search nobody collects is not observed (its outcome is never
 // read; the bench pays its re-run itself).
 //   * narrow (16-entry) lists -> 32-entry ones when more than 1 in 32 settled narrow blocks re-ran (over >= 64);
-//   * the int8 copy's screen -> the f16 copy's when more than 1 in 32 blocks of a window re-ran (its bound is ~8x
-//     looser: corpora whose top scores crowd within it), with full lists at once when more than 1 in 2 re-ran;
-//   * windows of >= 32 settled screened blocks of the current configuration (list width, per-lane list form):
-//     short per-lane lists (4 keys + the workgroup's floor, rr_sk.hip KL) -> full lists (KT keys) when more than
-//     1 in 32 re-ran (each costs an exact pass, twice a screen: 3 % re-run cost more than the full lists do):
-//     crowded near-duplicates (a few lanes holding many of them) raise the floors above what the verify can prove;
-//   * full lists, and still more than 1 in 2 re-ran: the screen cannot prune this corpus (near-duplicate clusters
-//     stored together fill a few workgroups' lists) and each such block pays the screen AND the exact pass — pause
-//     screening for 1024 blocks (the one-pass exact kernel alone), then probe again. Not while this k screens with
-//     the narrow lists (the 32-entry ones are tried first).
+//   * windows of >= 32 settled screened blocks of the current configuration: more than 1 in 32 re-ran -> REPAIR MODE
+//     (r5; h->full_lists): the screen keeps full per-lane lists (KT keys) and records, per chunk of rows and query, the
+//     largest bound; a query slot the verify cannot prove is then not flagged — its exact k-th score bars the chunks
+//     to rescore exactly, in-stream (mark / compact / repair pass / merge: rr_sk.hip "Repair"), so a corpus whose
+//     near-duplicate clusters defeat the lists (contiguous clusters fill a few workgroups' lists) costs the screen plus
+//     the rows of those chunks instead of a whole exact pass per block (the int8 copy keeps screening);
+//   * repair mode, and still more than 1 in 2 re-ran (only the f16-range guard or the test hook flag there): pause
+//     screening for 1024 blocks (the one-pass exact kernel alone), then probe again. Not while this k screens with the
+//     narrow lists (the 32-entry ones are tried first).
 // A block counts as re-run when its search was (a flagged search re-runs all its blocks). Reset at every load.
 void observe_settled(rr_handle* h, int blocks, bool narrow, bool full, bool wide, bool i8, bool rerun) {
   if (blocks <= 0) return;
@@ -901,16 +913,12 @@ void observe_settled(rr_handle* h, int blocks, bool narrow, bool full, bool wide
   h->win_nb += blocks;
   h->win_nf += nre;
   if (h->win_nb < 32) return;
-  if (i8) {   // the int8 screen's looser bound first gives way to the f16 copy's
+  (void)i8;
+  if (!h->full_lists) {
     if (h->win_nf * 32 > h->win_nb) {
-      h->i8_off = true;
-      // most blocks re-ran: crowded near-duplicates that the f16 copy's short lists will not prove either — its full
-      // lists come with it, so a corpus the screen cannot prune still reaches the pause one window later, as before
-      // the int8 copy (profiles/r04/final/clustered.jsonl: contiguous clusters otherwise paid screen + re-run)
-      if (h->win_nf * 2 > h->win_nb) h->full_lists = true;
+      h->full_lists = true;   // repair mode; the narrow lists are judged afresh in it (they no longer re-run)
+      h->narrow_settled = h->narrow_reruns = 0;
     }
-  } else if (!h->full_lists) {
-    if (h->win_nf * 32 > h->win_nb) h->full_lists = true;
   } else if (h->win_nf * 2 > h->win_nb && !narrow) {
     h->screen_pause = 1024;
     ++h->pauses;
@@ -1155,6 +1163,21 @@ void verify_args(const rr_handle* h, const Shard& s, const VerifyBlock& v, int n
   a->wide_count = s.wcount;
 }
 
+// Repair mode's buffers on shard s for up to `chunks` chunks (allocated once per load: any screen geometry of the shard
+// has at most one chunk per 32 rows; current device = s.dev, no repair pass of this shard in flight: the first use).
+int ensure_repair(Shard& s, int64_t chunks) {
+  if (chunks <= s.rcap) return RR_OK;
+  const int64_t cap = std::max<int64_t>(chunks, (s.rows() + 31) / 32 + 8);
+  for (int i = 0; i < 2; ++i) {
+    if (int rc = dmalloc(&s.rcmax[i], (size_t)cap * rr::kQSlots * 4)) return rc;
+    if (int rc = dmalloc(&s.rbits[i], (size_t)((cap + 31) / 32) * 4)) return rc;
+    if (int rc = dmalloc(&s.rlist[i], (size_t)cap * 4)) return rc;
+    if (int rc = dmalloc(&s.rcnt[i], 16)) return rc;
+  }
+  s.rcap = cap;
+  return RR_OK;
+}
+
 // Enqueue the device pipeline for query block [q0, q0 + bb) (bb <= slots) on every local shard.
 int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
   const int d = h->d;
@@ -1228,6 +1251,16 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       const bool alone = !two || s.last_vsi < 0 || s.last_vsi == bsi ||
                          hipEventQuery(s.ev_q[s.last_vq][s.last_vsi]) == hipSuccess;
       const int sgrid = screen_grid(h, s, alone);
+      const int ct8 = h->ct8 > 0 ? h->ct8 : s.rows() < 500000 ? 2 : 4;   // the int8 screen's tiles per chunk (A/B: RR_SCREEN_CT8)
+      // repair mode (rr_sk.hip "Repair"): the screen's chunk geometry, which its per-chunk maxima are indexed by
+      const bool rmode = h->full_lists && s.rows() > 0 && !h->ab_no_verify;
+      rr::ChunkGeo geo{};
+      if (rmode) {
+        const int sdt = s8 ? rr::KDT_SCREEN8 : s16 ? rr::KDT_SCREEN16 : rr::KDT_SCREEN;
+        const int64_t kn = s8 ? (s.rows() + 1) / 2 : s.rows();
+        geo = rr::chunk_geo((kn + 31) / 32, rr::sk_chunk_tiles(sdt, d, ct8), sgrid, h->guided != 0);
+        if (int rc = ensure_repair(s, geo.C)) return rc;
+      }
       const int64_t tl = h->host_prof ? now_ns() : 0;
       if (timed) HIP_TRY(hipEventRecord(e0, cs));
       if (s.rows() > 0) {
@@ -1236,7 +1269,12 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         a.clear_word = multi ? s.px_keys[x] + (size_t)slots * kt : nullptr;   // the verify of this block may raise it
         a.ctr = s.ctr + (cs == s.stream ? 0 : kCtrStride);
         a.sqrt_d = sqrtf((float)d) * (1.0f + 0x1p-20f);
-        a.full_lists = h->full_lists ? 1 : 0;
+        a.full_lists = rmode ? 2 : 0;   // (repair mode: full lists + per-chunk maxima)
+        if (rmode) {
+          a.cmax = s.rcmax[p];
+          a.rbits = s.rbits[p];
+          a.rbits_words = (int)((geo.C + 31) / 32);
+        }
         a.eps_a = s16 ? kScreen16EpsA : kScreenEpsA;
         a.eps_b = s16 ? kScreen16EpsB : kScreenEpsB;
         if (s16) a.corpus = (const char*)s.scr16;
@@ -1249,7 +1287,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
           a.q8s = s.q8s[bsi];
           a.sx8 = s.sx8;
           a.e8 = s.e8;
-          a.ct8 = h->ct8 > 0 ? h->ct8 : s.rows() < 500000 ? 2 : 4;   // (A/B: RR_SCREEN_CT8)
+          a.ct8 = ct8;
           a.eps_a = kScreen8EpsA;
           a.eps_b = kScreen8EpsB;
         }
@@ -1268,7 +1306,36 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         me.force = h->kernel == RR_KERNEL_SCREEN_FALLBACK;
         verify_args(h, s, me, sgrid, &v);
         v.seq = seq;
+        // repair mode: the verify's exact keys go after the repair pass's lists in this block's candidate half (past the
+        // screen's lists, which the verify reads), slots it cannot prove mark chunks; the repair pass rescores the
+        // marked chunks' rows exactly and merge_kernel joins both into the results (or this shard's exchanged keys)
+        const size_t half = cand_half(s);
+        const size_t roff = ((size_t)rr::kQSlots * sgrid * (kt + 1) + 63) / 64 * 64;
+        const size_t lkeys = (size_t)rr::kQSlots * kt;
+        const int rgrid = (int)std::min<int64_t>({255, (int64_t)s.cand_grid, (int64_t)((half - roff) / lkeys) - 1});
+        uint64_t* rbase = s.cand + (size_t)p * half + roff;
+        if (rmode) {
+          v.out_keys = rbase + (size_t)rgrid * lkeys;
+          v.out_scores = nullptr;
+          v.out_idx = nullptr;
+          v.cmax = s.rcmax[p];
+          v.rbits = s.rbits[p];
+          v.nchunks = geo.C;
+          v.repair_count = s.wcount + 1;
+        }
         HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 1, rr::kQSlots, rr::kQSlots, v, vs));
+        if (rmode) {
+          HIP_TRY(rr::launch_compact_bits(s.rbits[p], (int)((geo.C + 31) / 32), s.rlist[p], s.rcnt[p], vs));
+          rr::SkArgs r = sk_base(h, s, qb, bb);
+          r.out = rbase;
+          r.rlist = s.rlist[p];
+          r.rcount = s.rcnt[p];
+          r.rs = geo;
+          r.rs_rows = s8 ? 64 : 32;
+          HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 0, rgrid, rr::kQSlots, r, vs));
+          HIP_TRY(rr::launch_merge(kt, rbase, rgrid + 1, kt, bb, k, multi ? s.px_keys[x] : nullptr,
+                                   multi ? nullptr : osc, multi ? nullptr : oix, vs));
+        }
       } else if (!h->ab_no_verify) {   // a shard without rows contributes empty lists and no flag
         HIP_TRY(hipMemsetAsync(s.px_keys[x], 0, ((size_t)slots * kt + 1) * 8, vs));
       }
@@ -2194,6 +2261,22 @@ int rr_screen_counts(rr_handle* h, int64_t* blocks, int64_t* flagged, int64_t* r
   if (flagged) *flagged = fb;
   if (reruns) *reruns = h->screen_reruns;
   if (wide_slots) *wide_slots = ws;
+  return RR_OK;
+}
+
+int rr_screen_repairs(rr_handle* h, int64_t* repaired_slots) {
+  if (!h || !repaired_slots) return fail(RR_E_INVALID, "null argument");
+  if (h->failed) return failed_handle();
+  if (int rc = rr_synchronize(h)) return rc;
+  int64_t n = 0;
+  for (Shard& s : h->shards) {
+    if (!s.wcount) continue;
+    HIP_TRY(hipSetDevice(s.dev));
+    HIP_TRY(hipMemcpyAsync(s.pin_scount, s.wcount + 1, sizeof(int), hipMemcpyDeviceToHost, s.stream));
+    if (int rc = wait_stream(h, s, s.stream, "the repaired-slot count")) return rc;
+    n += *(volatile int*)s.pin_scount;
+  }
+  *repaired_slots = n;
   return RR_OK;
 }
 

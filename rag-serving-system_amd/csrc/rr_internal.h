@@ -48,6 +48,32 @@ hipError_t launch_fused(int kdt, int metric, int kt, int grid, const void* corpu
                         const float* rscale, const float* queries, int64_t n, int d, int b, uint32_t idx_base,
                         uint64_t* cand, hipStream_t s);
 
+// Chunk geometry of a split-K launch over T tiles (32 kernel rows each) and `grid` statically scheduled workgroups:
+// chunks of ct tiles, then (ct > 2, guided) the last ~2 grid tiles in 2-tile chunks, so the launch's last chunks are
+// short (rr_sk.hip "Guided tail"). Shared by the kernel and the host (the repair pass maps the screen's chunks to rows).
+struct ChunkGeo {
+  int64_t T, T1, C1, C;
+  int ct, ct2;
+};
+__host__ __device__ inline ChunkGeo chunk_geo(int64_t T, int ct, int64_t grid, bool guided) {
+  ChunkGeo g;
+  g.T = T;
+  g.ct = ct;
+  g.ct2 = ct > 2 ? 2 : ct;
+  g.T1 = ct > 2 && T > 2 * grid && guided ? (T - 2 * grid) / ct * ct : 0;   // tiles in ct-tile chunks
+  g.C1 = g.T1 / ct;
+  g.C = g.C1 + (T - g.T1 + g.ct2 - 1) / g.ct2;
+  return g;
+}
+__host__ __device__ inline int64_t chunk_tile0(const ChunkGeo& g, int64_t c) {
+  return c < g.C1 ? c * g.ct : g.T1 + (c - g.C1) * g.ct2;
+}
+__host__ __device__ inline int chunk_ntiles(const ChunkGeo& g, int64_t c) {
+  if (c < g.C1) return g.ct;
+  const int64_t left = g.T - chunk_tile0(g, c);
+  return (int)(left < g.ct2 ? left : g.ct2);
+}
+
 // Arguments of the split-K kernel (rr_sk.hip), all modes.
 struct SkArgs {
   const char* corpus;      // this shard's rows in the storage layout
@@ -94,6 +120,22 @@ struct SkArgs {
   int64_t rows8;
   int ct8;                 // tiles per chunk of the dynamic schedule (0: the kernel's default)
   int no_guided;           // A/B (RR_SCREEN_GUIDED=0): every chunk CT tiles, no 2-tile chunks at the end
+  // Repair mode (the screen's full_lists == 2; rr_sk.hip "Repair"): the screen writes, per chunk and query, the largest
+  // upper bound of the chunk's rows (cmax [nchunks][32], order-preserving ords) and zeroes rbits (rbits_words words);
+  // the verify (MODE 1, cmax / rbits / nchunks of its block) marks in rbits every chunk whose bound reaches the exact
+  // k-th score of a query slot it could not prove (instead of flagging the block) and writes its exact keys to
+  // out_keys; repair_count counts those slots. The repair pass (MODE 0 over the fp32 rows) then rescores the listed
+  // chunks (rlist, *rcount entries: screen chunk ids, rs = the screen's chunk geometry, rs_rows corpus rows per
+  // screen tile) and merge_kernel joins its lists with the verify's keys.
+  uint32_t* cmax;
+  uint32_t* rbits;
+  int rbits_words;
+  int64_t nchunks;
+  int* repair_count;
+  const int* rlist;
+  const int* rcount;
+  ChunkGeo rs;
+  int rs_rows;
 };
 
 // Split-K streaming kernel (rr_sk.hip): same output contract as launch_fused. sdt = KDT_* (0..3).
@@ -143,6 +185,11 @@ struct SelArgs {
   int seq, force_incomplete;
 };
 hipError_t launch_select(const SelArgs& a, hipStream_t s);
+
+// Repair pass: the set bits of rbits (words words) -> their indices, ascending, in list, and their count in *count.
+hipError_t launch_compact_bits(const uint32_t* rbits, int words, int* list, int* count, hipStream_t s);
+// Split-K chunk size (tiles) the kernel uses for screen dtype sdt at dimension d (ct8: the int8 screen's setting).
+int sk_chunk_tiles(int sdt, int d, int ct8);
 
 // A/B only: a one-workgroup kernel that holds a CU for `us` microseconds (a stand-in for a slower exchange).
 hipError_t launch_delay(int us, hipStream_t s);

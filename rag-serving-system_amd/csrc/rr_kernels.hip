@@ -484,7 +484,10 @@ __global__ __launch_bounds__(256) void merge_kernel(const uint64_t* __restrict__
     for (int i = 0; i < KT; ++i) {
       const uint64_t key = src[i];
       if (key <= tk.last()) break;            // sorted input: nothing further can enter
-      tk.insert(key);
+      bool dup = false;                       // (the same key in two lists: a repaired row the verify also scored)
+#pragma unroll
+      for (int j = 0; j < KT; ++j) dup = dup || tk.v[j] == key;
+      if (!dup) tk.insert(key);
     }
   }
 #pragma unroll
@@ -494,7 +497,7 @@ __global__ __launch_bounds__(256) void merge_kernel(const uint64_t* __restrict__
   for (int rnd = 0; rnd < KT; ++rnd) {
     const uint64_t m = wave_max_u64(head);
     if (lane == 0) W[wid * KT + rnd] = m;
-    if (m != 0 && head == m) {                 // keys are unique: exactly one owner advances
+    if (m != 0 && head == m) {                 // every owner of m advances (a key in two lists is emitted once)
       ++p;
       head = p < KT ? L[tid][p] : 0;
     }
@@ -505,9 +508,9 @@ __global__ __launch_bounds__(256) void merge_kernel(const uint64_t* __restrict__
   uint64_t mine = 0;
   for (int rnd = 0; rnd < KT; ++rnd) {
     const uint64_t m = wave_max_u64(umax64(a, c));
-    if (m != 0) {
+    if (m != 0) {   // every copy of m leaves (equal keys from different lists: one result)
       if (a == m) a = 0;
-      else if (c == m) c = 0;
+      if (c == m) c = 0;
     }
     if (lane == rnd) mine = m;
   }
@@ -851,6 +854,34 @@ __global__ __launch_bounds__(64) void q8_prep_kernel(const float* __restrict__ q
   q8_prep_slot(q, b, d, q8, q8s, (int)blockIdx.x, (int)threadIdx.x);
 }
 
+// Repair pass (rr_sk.hip "Repair"): the set bits of `bits` -> their indices in ascending order (list) and their count,
+// one 1024-thread workgroup: per pass of 1024 words, a block-wide scan of the words' popcounts gives each thread its
+// output position.
+__global__ __launch_bounds__(1024) void compact_bits_kernel(const uint32_t* __restrict__ bits, int words,
+                                                            int* __restrict__ list, int* __restrict__ count) {
+  __shared__ int pre[1024];
+  const int t = threadIdx.x;
+  int total = 0;
+  for (int w0 = 0; w0 < words; w0 += 1024) {
+    const int w = w0 + t;
+    const uint32_t v = w < words ? bits[w] : 0u;
+    const int c = __popc(v);
+    pre[t] = c;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {   // inclusive scan
+      const int x = t >= off ? pre[t - off] : 0;
+      __syncthreads();
+      pre[t] += x;
+      __syncthreads();
+    }
+    int pos = total + pre[t] - c;
+    for (uint32_t x = v; x; x &= x - 1) list[pos++] = (w << 5) + (__ffs(x) - 1);
+    total += pre[1023];
+    __syncthreads();
+  }
+  if (t == 0) *count = total;
+}
+
 __global__ void unsplit_f32_kernel(const u32x4* __restrict__ in, const float* __restrict__ rscale, int64_t n,
                                    int d, float* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // one 8-element group
@@ -1036,6 +1067,11 @@ hipError_t launch_merge(int kt, const uint64_t* in, int nlists, int in_kt, int b
     case 32: hipLaunchKernelGGL(merge_kernel<32>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out, clear_word); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_compact_bits(const uint32_t* rbits, int words, int* list, int* count, hipStream_t s) {
+  hipLaunchKernelGGL(compact_bits_kernel, dim3(1), dim3(1024), 0, s, rbits, words, list, count);
   return hipGetLastError();
 }
 

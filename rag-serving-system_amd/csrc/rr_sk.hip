@@ -426,6 +426,10 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   if constexpr (MODE == 0) {   // the exchanged flag word this block's verify may raise starts at 0
     if (a.clear_word && blockIdx.x == 0 && threadIdx.x == 0) *a.clear_word = 0;
   }
+  if constexpr (MODE == 0 && FL == 2) {   // repair mode: this block's chunk marks start empty (the verify sets them)
+    for (int i = (int)(blockIdx.x * blockDim.x + threadIdx.x); i < a.rbits_words; i += (int)(gridDim.x * blockDim.x))
+      a.rbits[i] = 0u;
+  }
   const char* __restrict__ corpus = a.corpus;
   const float* __restrict__ norms = a.norms;
   const float* __restrict__ rscale = a.rscale;
@@ -475,7 +479,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   uint64_t* xk = (uint64_t*)(gvalid + 32);
   uint64_t* vfloor = xk + KT;   // MODE 1: the largest floor of the screen's lists (see KL)
   uint64_t* vtail = vfloor + 1; // MODE 1: the largest bound of any single list, max(KT-th key, floor) (wide verify)
-  int* vstate = (int*)(vtail + 1);   // MODE 1: [0] what the leader decided after the first check, [1] |R|, [4] R's bar
+  int* vstate = (int*)(vtail + 1);   // MODE 1: [0] what the leader decided after the first check, [1] |R|, [4] R's bar,
+                                     // [5] the slot needs the repair pass, [6] its bar (an ord)
   // MODE 1 reads its 32 gathered rows straight into registers (all loads issued at once: one latency), the
   // exact fragments the LDS image would give: lane (r, h) takes 16-byte units 4(i>>1) + 2h + (i&1) of slab j
   f32x4 vrow[MODE == 1 ? NS : 1][4];
@@ -497,14 +502,37 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   const int64_t G = gridDim.x, g = blockIdx.x;
   // Guided tail: chunks of CT tiles, then (CT > 2) the last ~2 G tiles in 2-tile chunks, so the launch's last chunks —
   // the tail where workgroups finish at different times — are short (tools/probe_screen.hip: the 1M-row int8 screen's
-  // workgroups ended over 9 us with 4-tile chunks throughout). Chunk c: first tile cbase(c), ctiles(c) tiles; every
-  // chunk but the last has >= 2 tiles (the scheduler wave's next-chunk word is read at a chunk's last tile).
-  const int64_t T = (n + 31) / 32;
-  const int CT2 = CT > 2 ? 2 : CT;
-  const int64_t T1 = CT > 2 && T > 2 * G && !a.no_guided ? (T - 2 * G) / CT * CT : 0;   // tiles in CT-tile chunks
-  const int64_t C1 = T1 / CT, C = C1 + (T - T1 + CT2 - 1) / CT2;
-  auto cbase = [&](int64_t c) -> int64_t { return c < C1 ? c * CT : T1 + (c - C1) * CT2; };
-  auto ctiles = [&](int64_t c) -> int { return c < C1 ? CT : (int)(T - cbase(c) < CT2 ? T - cbase(c) : CT2); };
+  // workgroups ended over 9 us with 4-tile chunks throughout; +4-5 % for the screen alone at 1M rows,
+  // profiles/r05/ab_guided.txt). Chunk c: first tile cbase(c), ctiles(c) tiles; every chunk but the last has >= 2 tiles
+  // (the scheduler wave's next-chunk word is read at a chunk's last tile).
+  // The repair pass (a.rlist: MODE 0 over the fp32 rows, static schedule) instead walks the screen chunks listed in
+  // rlist: chunk j = the corpus rows of screen chunk rlist[j] (rs: the screen's geometry, rs_rows rows per screen tile).
+  const bool REP = MODE == 0 && !SCR && SCHED == 0 && a.rlist != nullptr;
+  const ChunkGeo geo = chunk_geo((n + 31) / 32, CT, G, !a.no_guided);
+  const int64_t T = geo.T;
+  const int64_t C = REP ? (int64_t)*a.rcount : geo.C;
+  auto rep_rows = [&](int64_t j, int64_t* r0, int64_t* r1) {
+    const int64_t sc = a.rlist[j];
+    *r0 = chunk_tile0(a.rs, sc) * a.rs_rows;
+    const int64_t e = *r0 + (int64_t)chunk_ntiles(a.rs, sc) * a.rs_rows;
+    *r1 = e < n ? e : n;
+  };
+  auto cbase = [&](int64_t c) -> int64_t {
+    if (REP) {
+      int64_t r0, r1;
+      rep_rows(c, &r0, &r1);
+      return r0 / 32;
+    }
+    return chunk_tile0(geo, c);
+  };
+  auto ctiles = [&](int64_t c) -> int {
+    if (REP) {
+      int64_t r0, r1;
+      rep_rows(c, &r0, &r1);
+      return (int)((r1 - r0 + 31) / 32);
+    }
+    return chunk_ntiles(geo, c);
+  };
 
   // LDS-DMA lane mapping: instruction i of a slab covers tile rows 8i + lane/8, 16-byte column
   // (lane % 8) ^ (lane / 8) of the slab — so the image holds column c of row r at c ^ (r & 7)
@@ -933,6 +961,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 
   TopK<KL> tk;
   tk.init();
+  float umax = -INFINITY;   // repair mode (FL 2): this lane's largest bound in the current chunk
 #if defined(RR_SK_DIAG) && (RR_SK_DIAG & 4)
   unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // phase cycles; [7] = insert executions (wave-wide)
 #endif
@@ -1086,6 +1115,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
             u = v;
           }
           if (valid && u >= thr) tk.insert(make_key(u, key_base + (uint32_t)(ero + e)));   // (NaN: never)
+          if constexpr (FL == 2) {   // repair mode: the largest bound of the chunk's rows (NaN-free: u is clipped)
+            if (valid) umax = fmaxf(umax, u);
+          }
         } else if constexpr (COS) {
           // dot / (|q|*|d| + 1e-8), then clip to [-1, 1]   (retriever.py:605-609)
           if (DUMP && a.all_keys) {
@@ -1155,7 +1187,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #endif
   // (Rejected and removed: exchanging a tile's K-partials one tile late behind the next tile's MFMAs, -2 % on the
   // 64-slot pass, profiles/r03/b/ab_pipelined_exchange_rejected.txt; deferring the odd waves instead of 4-7.)
-  constexpr bool STG = MODE == 0 && !(QH == 2 && DT == 2) && DT != 6 && (DT != 8 || RR_SK_STAGGER8) &&
+  constexpr bool STG = MODE == 0 && FL != 2 && !(QH == 2 && DT == 2) && DT != 6 && (DT != 8 || RR_SK_STAGGER8) &&
                        KT <= 16 &&   // (measured)
                        (RR_SK_STAGGER == 2 || (RR_SK_STAGGER == 1 && QH == 2));
   const bool defer = STG && w >= 4;
@@ -1460,6 +1492,13 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       } else {
         epilogue(sv, base, ts);
       }
+      if constexpr (SCR && FL == 2) {   // repair mode: the chunk's largest bound per query, at its last tile
+        if (last_in_chunk) {
+          const uint32_t m = group_max_u32<LPQ>(ord_of(umax));
+          if (lane % LPQ == 0) a.cmax[(size_t)chunk * QS + qe] = m;
+          umax = -INFINITY;
+        }
+      }
       const unsigned long long pt5 = PH_NOW();
       PH_ADD(2, pt2 - pt1);
       PH_ADD(3, pt3 - pt2);
@@ -1554,14 +1593,21 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         }
       }
     };
-    // the leader's verdict and the results (xk); an incomplete block raises the flag word (the host re-runs it)
-    auto finish = [&](bool complete) {
-      complete = complete && qinfo[QS + vq] < 32768.0f && !a.force_incomplete;   // f16 range of the screen
-      if (!complete) {   // the first query slot to flag the block also counts it
+    // The leader's verdict and the results (xk); an incomplete block raises the flag word (the host re-runs it).
+    // Repair mode (a.rbits: the block's screen recorded per-chunk maxima of the bound): a slot the bound cannot prove
+    // is not flagged — its exact k-th key ek bars the chunks to rescore, since every row that can be in its top-k has
+    // bound >= its exact score >= the true k-th score >= ek's; they are marked in rbits (mark, every thread, below) and
+    // the repair pass merges their exact keys with xk (written to out_keys). Returns whether the slot needs it.
+    auto finish = [&](bool complete) -> bool {
+      const bool range = qinfo[QS + vq] < 32768.0f && !a.force_incomplete;   // f16 range of the screen
+      const bool repair = a.rbits != nullptr && !complete && range;
+      complete = complete && range;
+      if (!complete && !repair) {   // the first query slot to flag the block also counts it
         if (__hip_atomic_fetch_max(a.flag, (uint64_t)a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
             (uint64_t)a.seq)
           __hip_atomic_fetch_add(a.count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      if (repair && a.repair_count) __hip_atomic_fetch_add(a.repair_count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (vq == 0) __hip_atomic_fetch_add(a.count + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // done
       if (a.out_keys)
         for (int i = 0; i < KT; ++i) a.out_keys[(size_t)vq * KT + i] = xk[i];
@@ -1571,6 +1617,12 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           a.out_scores[(size_t)vq * a.k_out + i] = key ? float_of_ord((uint32_t)(key >> 32)) : -INFINITY;
           a.out_idx[(size_t)vq * a.k_out + i] = key ? (int64_t)(0xFFFFFFFFu - (uint32_t)key) : -1;
         }
+      return repair;
+    };
+    // repair mode: every chunk whose largest bound for this slot reaches bar (an ord), marked for the repair pass
+    auto mark = [&](uint32_t bar) {
+      for (int64_t c = tid; c < a.nchunks; c += kThreads)
+        if (a.cmax[(size_t)c * QS + vq] >= bar) atomicOr(&a.rbits[c >> 5], 1u << (c & 31));
     };
     lane_merge();
     if (leader) {
@@ -1595,9 +1647,14 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       VDIAG(4, 0);
       VDIAG(5, complete ? 0 : wide ? 1 : 2);
       VDIAG(6, complete);
-      if (!wide) finish(complete);
+      vstate[5] = !wide && finish(complete) ? 1 : 0;
+      vstate[6] = (int)(uint32_t)(ek >> 32);   // (0 with fewer than k candidates: every chunk)
     }
     __syncthreads();
+    if (vstate[5]) {
+      mark((uint32_t)vstate[6]);
+      return;
+    }
     if (vstate[0] != 1) return;
 
     // ---- wide phase: R = every list entry whose bound reaches R's bar (wide_bar; every key left out of the lists is
@@ -1622,7 +1679,12 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     __syncthreads();
     const int nr = vstate[1];
     if (nr > kWideCap) {   // (cannot happen while lists x KT <= kWideCap; kept as a guard)
-      if (leader) finish(false);
+      if (leader) {
+        vstate[5] = finish(false) ? 1 : 0;
+        vstate[6] = (int)(uint32_t)(xk[a.k_out - 1] >> 32);
+      }
+      __syncthreads();
+      if (vstate[5]) mark((uint32_t)vstate[6]);
       return;
     }
     tk.init();
@@ -1717,8 +1779,11 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       VDIAG(4, nr);
       VDIAG(6, complete);
       if (complete && a.wide_count) __hip_atomic_fetch_add(a.wide_count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      finish(complete);
+      vstate[5] = finish(complete) ? 1 : 0;
+      vstate[6] = (int)(uint32_t)(ek >> 32);
     }
+    __syncthreads();
+    if (vstate[5]) mark((uint32_t)vstate[6]);
   }
   SK_PROBE(5);
 }
@@ -1777,12 +1842,17 @@ size_t sk_lds_bytes(int sdt, bool cos, int ring, int qslots) {
   // + per-row factors [4][64] (the int8 screen: [4][192]), next-chunk words [4], query scalars [3][qslots], MODE 1
   // scratch: W [8][32] + akeys [32] keys, grow / gnorm / gvalid [32], xk [32] keys, the floors' and the list bounds'
   // maxima, 6 ints
-  const size_t verify = (size_t)(kWaves * 32 + 32 + 32 + 5) * 8 + 3 * 32 * 4;
+  const size_t verify = (size_t)(kWaves * 32 + 32 + 32 + 8) * 8 + 3 * 32 * 4;
   const size_t factors = (size_t)4 * (sdt == KDT_SCREEN8 ? 192 : 64) * 4;
   return sk::ring_bytes(ring) + sk::red_bytes(ring, qslots / 32) + factors + 4 * 4 + 3 * qslots * 4 + verify;
 }
 
 bool sk_supports_64(int sdt) { return sdt == KDT_BF16 || sdt == KDT_F32_SPLIT; }
+int sk_chunk_tiles(int sdt, int d, int ct8) {   // (the kernel's CT: CT0 by slabs per wave, or the int8 screen's ct8)
+  const int ns = sk_slabs(sdt == KDT_SCREEN ? KDT_F32_X3 : sdt, d);
+  if (sdt == KDT_SCREEN8 && ct8 > 0) return ct8;
+  return ns >= 4 ? 2 : ns == 3 ? 3 : ns == 2 ? 4 : 8;
+}
 int sk_slabs(int sdt, int d) {
   // (the int8 screen: kernel rows of two corpus rows, 2 d bytes)
   const int eb = sdt == KDT_BF16 || sdt == KDT_SCREEN16 || sdt == KDT_SCREEN8 ? 2 : 4;
@@ -1807,6 +1877,9 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
   if (sdt == KDT_SCREEN) {
     if (qslots != 32 || ring != 2) return hipErrorInvalidValue;
     const bool dyn = a.dyn && a.ctr && kt <= 16;
+    if (a.full_lists == 2)   // repair mode: full lists + per-chunk maxima of the bound
+      return dyn ? sk::launch_metric<6, 2, 1, 0, 1, 2>(metric, ns, kt, grid, a, s)
+                 : sk::launch_metric<6, 2, 1, 0, 0, 2>(metric, ns, kt, grid, a, s);
     if (a.full_lists)
       return dyn ? sk::launch_metric<6, 2, 1, 0, 1, 1>(metric, ns, kt, grid, a, s)
                  : sk::launch_metric<6, 2, 1, 0, 0, 1>(metric, ns, kt, grid, a, s);
@@ -1818,6 +1891,9 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
     if (qslots != 32 || ring != 2 || !ns8 || !a.q8 || !a.q8s || !a.sx8 || !a.e8 || a.n != (a.rows8 + 1) / 2)
       return hipErrorInvalidValue;
     const bool dyn = a.dyn && a.ctr && kt <= 16;
+    if (a.full_lists == 2)   // repair mode: full lists + per-chunk maxima of the bound
+      return dyn ? sk::launch_metric<8, 2, 1, 0, 1, 2>(metric, ns8, kt, grid, a, s)
+                 : sk::launch_metric<8, 2, 1, 0, 0, 2>(metric, ns8, kt, grid, a, s);
     if (a.full_lists)
       return dyn ? sk::launch_metric<8, 2, 1, 0, 1, 1>(metric, ns8, kt, grid, a, s)
                  : sk::launch_metric<8, 2, 1, 0, 0, 1>(metric, ns8, kt, grid, a, s);
@@ -1828,6 +1904,9 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
     const int ns16 = sk_slabs(KDT_SCREEN16, a.d);
     if (qslots != 32 || ring != 2 || !ns16) return hipErrorInvalidValue;
     const bool dyn = a.dyn && a.ctr && kt <= 16;
+    if (a.full_lists == 2)   // repair mode: full lists + per-chunk maxima of the bound
+      return dyn ? sk::launch_metric<7, 2, 1, 0, 1, 2>(metric, ns16, kt, grid, a, s)
+                 : sk::launch_metric<7, 2, 1, 0, 0, 2>(metric, ns16, kt, grid, a, s);
     if (a.full_lists)
       return dyn ? sk::launch_metric<7, 2, 1, 0, 1, 1>(metric, ns16, kt, grid, a, s)
                  : sk::launch_metric<7, 2, 1, 0, 0, 1>(metric, ns16, kt, grid, a, s);

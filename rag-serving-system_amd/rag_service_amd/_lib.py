@@ -87,6 +87,7 @@ SIGNATURES = {
     "rr_stream_queues": (_c_int, [_vp, _c_int, ctypes.POINTER(ctypes.c_uint64)]),
     "rr_update_rows": (_c_int, [_vp, _fp, _i64p, _c_i64, _c_i32]),
     "rr_screen_state": (_c_int, [_vp, ctypes.POINTER(_c_i32), _i64p, _i64p]),
+    "rr_screen_repairs": (_c_int, [_vp, _i64p]),
 }
 
 
@@ -346,6 +347,12 @@ class Index:
         p = _c_i32()
         _check(self._lib.rr_screen_int8(self._h, -1 if use is None else int(bool(use)), ctypes.byref(p)))
         return bool(p.value)
+
+    def screen_repairs(self) -> int:
+        """Query slots the repair pass completed (repair mode) since the corpus was loaded, over local shards."""
+        n = _c_i64()
+        _check(self._lib.rr_screen_repairs(self._h, ctypes.byref(n)))
+        return n.value
 
     def screen_stats(self) -> Tuple[int, int]:
         """(screened search blocks, blocks that needed the exact fallback pass)."""

@@ -92,3 +92,77 @@ def test_host_merge_equals_single_shard():
             ids.append(np.where(i >= 0, i + b0, -1))
         mv, mi = merge_shard_topk(np.stack(vs), np.stack(ids), 12)
         assert np.array_equal(mi, want_i)
+
+
+class _FakeIndex:
+    """Stands in for rag_service_amd.Index in bench.timed_steps (no GPU): every screened search block flags with the
+    rank's own rate, the library re-runs some of them itself, and each search issued under kernel "exact" is counted
+    (the re-runs timed_steps pays)."""
+
+    def __init__(self, flag_every, lib_rerun_every):
+        self.kernel = "auto"
+        self.blocks = self.flagged = self.reruns = 0
+        self.exact_searches = 0
+        self.flag_every, self.lib_rerun_every = flag_every, lib_rerun_every
+
+    def search_staged(self, k):
+        if self.kernel == "exact":
+            self.exact_searches += 1
+            return
+        self.blocks += 1
+        if self.flag_every and self.blocks % self.flag_every == 0:
+            self.flagged += 1
+            if self.lib_rerun_every and self.flagged % self.lib_rerun_every == 0:
+                self.reruns += 1
+
+    def synchronize(self):
+        pass
+
+    def screen_counts_all(self):
+        return self.blocks, self.flagged, self.reruns, 0
+
+    def set_timing(self, on):
+        pass
+
+    def kernel_time(self, reset=True):
+        return 0.0, 0
+
+    def set_kernel(self, k):
+        self.kernel = k
+
+
+def _timed_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from rag_service_amd.dist import init_control_plane
+    dist = init_control_plane(world, rank)
+    # rank 0: every 4th block flags, the library re-runs every 2nd flagged one; rank 1: every 5th, none re-run
+    ix = _FakeIndex(4, 2) if rank == 0 else _FakeIndex(5, 0)
+    acct = {}
+    bench.timed_steps(ix, 5, 40, 3, dist, lambda: None, 1, acct)
+    q.put((rank, acct, ix.exact_searches))
+    dist.destroy_process_group()
+
+
+def test_timed_steps_pays_summed_reruns_on_every_rank():
+    """bench.timed_steps at world 2 (gloo, a fake index per rank): the blocks each rank flagged inside the window and
+    the library did not re-run itself are summed over the ranks, and EVERY rank issues that many exact searches
+    before the closing sync — so their all-gathers pair up. Rank 0: 40 window blocks, 10 flagged (every
+    4th), 5 re-run by the library -> owes 5; rank 1: 8 flagged, none re-run -> owes 8; both pay 13."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_timed_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, a0, e0), (r1, a1, e1) = out
+    assert (a0["blocks"], a0["flagged"], a0["reruns_library"]) == (40, 10, 5)
+    assert (a1["blocks"], a1["flagged"], a1["reruns_library"]) == (40, 8, 0)
+    assert a0["reruns_paid"] == a1["reruns_paid"] == 13 and e0 == e1 == 13

@@ -80,10 +80,10 @@ def test_int8_screen_proves_unit_norm_blocks_in_the_wide_phase(Index):
     ix.close()
 
 
-def test_int8_screen_gives_way_to_the_f16_copy(Index):
-    """Adaptive: a window of settled blocks that re-ran (forced here) switches the handle to the f16 copy — with its
-    full per-lane lists, since every block re-ran — not yet to the pause; results stay exact throughout; a reload
-    re-arms the int8 screen."""
+def test_int8_screen_forced_reruns_then_pause(Index):
+    """Adaptive (r5): a window of settled blocks that re-ran (forced here: RR_KERNEL_SCREEN_FALLBACK flags every block)
+    switches the handle to repair mode, keeping the int8 copy; forced flags go on (the test hook bypasses the repair),
+    so the next window pauses screening; results stay exact throughout; a reload re-arms everything."""
     rng = np.random.default_rng(3)
     corpus = rng.standard_normal((20000, 1024)).astype(np.float32)
     q = rng.standard_normal((32, 1024)).astype(np.float32)
@@ -96,14 +96,16 @@ def test_int8_screen_gives_way_to_the_f16_copy(Index):
     for _ in range(32):
         got = ix.search(q, 5)
         assert np.array_equal(got[1], want[1])
-    assert not ix.screen_int8()
-    # every block re-ran (more than 1 in 2): the f16 copy takes over with its full per-lane lists at once
-    assert ix.screen_state() == (True, 0, 0)
+    assert ix.screen_int8() and ix.screen_state() == (True, 0, 0)     # repair mode, the int8 copy still screening
+    for _ in range(32):
+        got = ix.search(q, 5)
+        assert np.array_equal(got[1], want[1])
+    assert ix.screen_state() == (True, 1024, 1)                       # still flagging in repair mode: paused
     ix.set_kernel("auto")
     got = ix.search(q, 5)
     assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
     ix.load(corpus)
-    assert ix.screen_int8()
+    assert ix.screen_int8() and ix.screen_state() == (False, 0, 0)
     ix.close()
 
 

@@ -311,11 +311,11 @@ def test_screen_adapts_to_clustered_corpora(Index, layout):
     """The adaptive screen (rr_api.cpp observe_settled) on 1000 noisy copies of each of 100 SQuAD rows (sigma 0.01):
     interleaved, every cluster's copies fall on a few lanes of each workgroup (a stride of 100 rows) and the wide
     phase, barred at the exact k-th score, proves every block with the short lists and the int8 copy (no flags, no
-    switch). Contiguous, a cluster fills a few workgroups' lists: after a window of re-run blocks the handle gives
-    the int8 copy up for the f16 one (with full per-lane lists, since most blocks re-ran), and after the next pauses
-    screening (the exact kernel alone) for 1024 blocks. Decided from settled searches only, so a handle in multi-process mode (1-rank RCCL
-    communicator) switches at exactly the same searches as a plain one. Results bit-identical to the exact kernel
-    at every step."""
+    switch). Contiguous, a cluster fills a few workgroups' lists: after a window of re-run blocks the handle switches
+    to repair mode (r5: full lists + per-chunk maxima, the unproven slots' chunks rescored exactly in-stream) and no
+    block flags after that, the int8 copy screening throughout. Decided from settled searches only, so a handle in
+    multi-process mode (1-rank RCCL communicator) switches at exactly the same searches as a plain one. Results
+    bit-identical to the exact kernel at every step."""
     corpus, q = _clustered(100000, 0.01, layout, clusters=100)
     ex = Index(dtype="fp32", metric="cosine")
     ex.load(corpus)
@@ -326,7 +326,7 @@ def test_screen_adapts_to_clustered_corpora(Index, layout):
     for ix in handles:
         assert ix.screen_state() == (False, 0, 0)
         hist = []
-        for step in range(140):
+        for step in range(100):
             got = ix.search(q, 5)
             assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), step
             hist.append(ix.screen_counts_all() + ix.screen_state() + (ix.screen_int8(),))
@@ -337,20 +337,16 @@ def test_screen_adapts_to_clustered_corpora(Index, layout):
     assert [h[:3] for h in hist] == [h[:3] for h in hist_dist]          # the same blocks, flags and re-runs
     blocks, flagged, reruns, wide_slots, full, pause_left, pauses, i8 = hist[-1]
     print(layout, hist[40], hist[-1])
+    assert all(h[7] for h in hist)                                      # the int8 copy screens throughout
     if layout == "interleaved":
         # r4: the wide phase bars at the exact k-th score once that clears the lists' tail, so the short lists prove
         # every block of the interleaved clusters (r3 needed a window of re-runs and the full lists first)
-        assert flagged == 0 and pauses == 0 and not full and blocks == 140 and wide_slots >= 32 * 100
-        assert all(h[7] for h in hist)                                  # the int8 copy screens throughout
+        assert flagged == 0 and pauses == 0 and not full and blocks == 100 and wide_slots >= 32 * 100
     else:
-        # the int8 copy gives way first (every block re-ran: with the f16 copy's full lists at once), then screening
-        # pauses — each at a window's end
-        i8_off = next(i for i, h in enumerate(hist) if not h[7])
+        # repair mode at the end of the first window; no flag, re-run or pause after it
         full_at = next(i for i, h in enumerate(hist) if h[4])
-        assert i8_off % 32 == 31 and full_at % 32 == 31 and i8_off <= full_at
-        pause_at = next(i for i, h in enumerate(hist) if h[6])
-        assert pause_at % 32 == 31 and pauses == 1 and blocks == pause_at + 1   # then the exact kernel alone
-        assert pause_left == 1024 - (139 - pause_at)
+        assert full_at == 31 and pauses == 0 and blocks == 100
+        assert flagged == hist[full_at][1] and reruns == hist[full_at][2]
     ex.close()
 
 
@@ -469,12 +465,13 @@ def test_screen_copy_equals_fp32_screen_and_exact(Index, metric):
     ex.close()
 
 
-def test_narrow_lists_switch_to_wide(Index):
-    """k = 10 screens with 16-entry lists (k + 3 spare). Twenty near-copies of each query make the 16th upper
-    bound exceed the exact 10th score: every block is re-run exactly — until, after 64 settled narrow blocks, the
-    handle switches to 32-entry lists, which prove these blocks complete. The same switch, at the same search, in
-    multi-process mode (1-rank RCCL communicator: the decision comes from the exchanged flag words). Results are
-    exact throughout."""
+def test_narrow_lists_then_repair_mode(Index):
+    """k = 10 screens with 16-entry lists (k + 3 spare). Twenty near-copies of each query make the 16th upper bound
+    exceed the exact 10th score: every block flags and is re-run exactly — until the first window of 32 settled blocks
+    switches the handle to repair mode (r5; before it, the narrow lists switched to 32-entry ones after 64), whose
+    repair pass completes these blocks in-stream: no flag after it, and the narrow lists stay. The same switch, at the
+    same search, in multi-process mode (1-rank RCCL communicator: the decision comes from the exchanged flag words).
+    Results are exact throughout."""
     rng = np.random.default_rng(5)
     corpus = synth.unit_norm_gaussian(91, 65536, 1024)
     q = synth.unit_norm_gaussian(92, 32, 1024)
@@ -493,7 +490,8 @@ def test_narrow_lists_switch_to_wide(Index):
             assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]), step
             flags.append(ix.screen_stats()[1])
         blocks, flagged = ix.screen_stats()
-        assert blocks == 80 and flagged == 64 and flags[63] == 64 and flags[62] == 63   # none after the switch
+        assert blocks == 80 and flagged == 32 and flags[31] == 32 and flags[30] == 31   # none after the switch
+        assert ix.screen_state() == (True, 0, 0) and ix.screen_repairs() >= 48
         per_mode.append(flags)
         ix.close()
     assert per_mode[0] == per_mode[1]

@@ -53,6 +53,8 @@ def main() -> None:
                     help="untimed steps first, each awaited: the adaptive screen settles (short -> full lists, pause)")
     ap.add_argument("--sigmas", default="0.01,0.03,0.1,0.3")
     ap.add_argument("--layouts", default="interleaved,contiguous")
+    ap.add_argument("--int8", default="auto", choices=["auto", "off"],
+                    help="off: screen the f16 copy (rr_screen_int8(0)) instead of the int8 one")
     args = ap.parse_args()
 
     import bench
@@ -81,6 +83,8 @@ def main() -> None:
             q /= np.linalg.norm(q, axis=1, keepdims=True)
             ix.set_kernel("auto")
             ix.load(corpus)
+            if args.int8 == "off":
+                ix.screen_int8(False)
             del corpus
             ix.set_queries(q)
             # warm-up paced like a serving loop (each batch's results awaited): the adaptive screen decides from the
@@ -113,7 +117,8 @@ def main() -> None:
                    "reruns_paid": acct["reruns_paid"], "reruns_library": acct["reruns_library"],
                    "flag_rate": round(acct["flagged"] / max(1, acct["blocks"]), 4),
                    "wide_verified_slots": acct["wide_slots"],
-                   "screen_state_after": dict(zip(("full_lists", "pause_left", "pauses"), state), int8=i8),
+                   "screen_state_after": dict(zip(("repair_mode", "pause_left", "pauses"), state), int8=i8),
+                   "repaired_slots": ix.screen_repairs(),
                    "bit_identical_to_exact": same,
                    "median_score_gap_k_to_16": round(gap16, 6), "median_score_gap_k_to_32": round(gap32, 6),
                    "top1_median": round(float(np.median(s32[:, 0])), 5)}
