@@ -37,7 +37,8 @@ METRIC = "retrieval queries/sec + p99 latency, batch=32, 1M docs d=1024, 1/2/4/8
 SCORE_KERNEL_DOC = ("the corpus-streaming kernel: sk_score_kernel MODE 0 (split-K, LDS-DMA; for fp32 storage the "
                     "screened search's screen — DT 8 over the int8 screening copy (d a multiple of 512 up to 1024), "
                     "DT 7 over the f16 copy, else DT 6 over the fp32 rows — whose exact fp32 verify of the candidates "
-                    "runs on the other compute stream), else fused_score_kernel")
+                    "runs on the other compute stream; for bf16 storage's 64-slot blocks DT 9 over the int8 copy of the "
+                    "bf16 rows, verified by the bf16 pass's own arithmetic), else fused_score_kernel")
 
 
 def is_score_kernel(name: str) -> bool:
@@ -111,9 +112,10 @@ def algorithmic_bytes(rows: int, d: int, batch: int, dtype: str, metric: str, sc
     """HBM bytes one corpus-streaming launch must move: the rows once (4 B/element fp32 and fp32-split, 2 B bf16,
     2 B when the fp32 screen streams the f16 screening copy, 1 B the int8 copy), the per-row factors it reads (norm
     for cosine, row scale for fp32-split; the int8 copy's norm, scale and error norm), the queries once (fp32; the
-    int8 screen's two int8 pieces of 32 slots)."""
+    int8 screen's two int8 pieces of 32 slots, or bf16 storage's one piece of 64 slots) and their 4 scalars."""
     if screen8:
-        return rows * (d + 12) + 2 * 32 * d + 4 * 32 * 4
+        slots = 64 if dtype == "bf16" else 32
+        return rows * (d + 12) + 64 * d + 4 * slots * 4
     elem = 2 if dtype == "bf16" or screen16 else 4
     # per-row factors: the norm (cosine; and the fp32 screen's error bound for either metric), the split scale
     per_row = (4 if metric == "cosine" or dtype == "fp32" else 0) + (4 if dtype == "fp32-split" else 0)
@@ -171,6 +173,61 @@ def timed_steps(ix, k, steps, warmup, dist, cuda_sync, every=1, acct=None):
     return elapsed, kern_ms, launches
 
 
+def clustered_field(args, local: int, cuda_sync, steps: int = 60, warmup: int = 80, sigma: float = 0.03) -> dict:
+    """Data dependence of the screened search: the headline's search (k, cosine) over 1M-row corpora
+    built from the reference's only real embeddings (data/squad_embeddings.npy, 1000 e5 rows, a committed fixture):
+    row i = SQuAD row c(i) + seeded Gaussian noise of relative size sigma, L2-normalised — "interleaved" (c(i) = i mod
+    1000) and "contiguous" (c(i) = i div (n / 1000): clusters stored in topic order, the normal case for an ingested
+    corpus). Per layout, after `warmup` awaited searches (the adaptive screen settles): screened q/s over `steps` staged
+    steps with every flagged block's exact re-run paid inside the window, the exact one-pass kernel's q/s, which copy
+    screened, repair mode and the slots it completed, and whether a fetched result equals the exact kernel's bit for
+    bit (tools/clustered_bench.py has the sigma sweep)."""
+    from rag_service_amd import Index
+    squad = np.load(os.path.join(REPO, "tests", "golden", "data", "squad_embeddings.npy")).astype(np.float32)
+    squad /= np.linalg.norm(squad, axis=1, keepdims=True)
+    n, d = args.docs, squad.shape[1]
+    rng = np.random.default_rng(20260)
+    noise = rng.standard_normal((n, d), dtype=np.float32) / np.float32(np.sqrt(d))
+    qrng = np.random.default_rng(777)
+    qc = qrng.integers(0, squad.shape[0], args.batch)
+    q = squad[qc] + np.float32(sigma) * qrng.standard_normal((args.batch, d), dtype=np.float32) / np.float32(np.sqrt(d))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    out = {"sigma": sigma, "docs": n, "k": args.k, "steps": steps, "warmup_awaited": warmup,
+           "source": "tests/golden/data/squad_embeddings.npy (the reference's data/squad_embeddings.npy)"}
+    ix = Index(devices=[local], dtype="fp32", metric=args.metric)
+    for layout in ("interleaved", "contiguous"):
+        c = np.arange(n) % squad.shape[0] if layout == "interleaved" else np.minimum(np.arange(n) // (n // squad.shape[0]),
+                                                                                       squad.shape[0] - 1)
+        corpus = squad[c]
+        corpus += np.float32(sigma) * noise
+        corpus /= np.linalg.norm(corpus, axis=1, keepdims=True)
+        ix.set_kernel("auto")
+        ix.load(corpus)
+        del corpus
+        ix.set_queries(q)
+        for _ in range(warmup):
+            ix.search_staged(args.k)
+            ix.synchronize()
+        acct = {}
+        s_el, _, _ = timed_steps(ix, args.k, steps, 0, None, cuda_sync, 10, acct)
+        state = ix.screen_state()
+        i8, repaired = ix.screen_int8(), ix.screen_repairs()
+        got = ix.search(q, args.k)
+        ix.set_kernel("exact")
+        ix.set_queries(q)
+        e_el, _, _ = timed_steps(ix, args.k, steps, 5, None, cuda_sync, 10)
+        want = ix.search(q, args.k)
+        out[layout] = {"screened_qps": round(args.batch * steps / s_el, 1),
+                       "exact_qps": round(args.batch * steps / e_el, 1), "speedup_vs_exact": round(e_el / s_el, 3),
+                       "screen_copy": "int8" if i8 else "f16", "repair_mode": bool(state[0]), "pauses": state[2],
+                       "repaired_slots_since_load": repaired, "flagged_timed": acct["flagged"],
+                       "reruns_paid_timed": acct["reruns_paid"],
+                       "bit_identical_to_exact": bool(np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0]))}
+    ix.close()
+    del noise
+    return out
+
+
 def spawn_ranks(n: int) -> int:
     """Run this script under torch.distributed.run with one rank per GPU, as a child process (this process
     has not touched the GPU). Returns the child's exit status."""
@@ -214,6 +271,8 @@ def main() -> None:
                     help="similarity kernel of the timed loops (rr_set_kernel; A/B and counter passes: `exact` = the "
                          "one-pass exact fp32 kernel without the screen)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-clustered", action="store_true",
+                    help="skip the clustered-corpus field (two SQuAD-derived 1M-row corpora; N=1 only)")
     ap.add_argument("--exchange-1rank", action="store_true",
                     help="N=1: run the multi-GPU data path anyway (a 1-rank RCCL communicator: per-block all-gather "
                          "of the candidates and the device merge), for measuring the exchange's cost on one GPU")
@@ -354,8 +413,11 @@ def run(args, stage: dict) -> None:
     # ---- roofline of the fused kernel (rank 0's shard) ---------------------------------------------
     n_local = se - sb
     # the fp32 screened search (k <= 29) streams the f16 screening copy when the handle keeps one
-    screen16 = args.dtype == "fp32" and args.k <= 29 and ix.screen_copy()
-    screen8 = screen16 and ix.screen_int8()   # ... and the int8 copy, unless the adaptive screen gave it up
+    screen16 = args.dtype == "fp32" and args.k <= 29 and args.kernel == "auto" and ix.screen_copy()
+    # bf16 storage: 64-slot blocks (batch > 32) with 16-entry lists (k <= 13) screen its int8 copy (DT 9)
+    screen_bf = (args.dtype == "bf16" and args.batch > 32 and args.k <= 13 and args.kernel == "auto" and
+                 ix.screen_int8())
+    screen8 = (screen16 and ix.screen_int8()) or screen_bf   # the int8 copy, unless the adaptive screen gave it up
     alg_bytes = algorithmic_bytes(n_local, args.dim, args.batch, args.dtype, args.metric, screen16, screen8)
     fp32_floor = n_local * args.dim * 4 + args.batch * args.dim * 4
     avg_kernel_s = (kern_ms / max(launches, 1)) / 1e3
@@ -364,7 +426,7 @@ def run(args, stage: dict) -> None:
     # drains and its verify runs, so each launch's event span covers about two steps and is no duration of its
     # own. One launch per step: the launch's time is then the step time, and `achieved` = its algorithmic bytes /
     # ms_per_step (the sustained HBM rate of the path). The kernel alone (one stream, every CU) is measured below.
-    streams = ix.compute_streams() if args.dtype == "fp32" else 1
+    streams = ix.compute_streams() if args.dtype == "fp32" or screen_bf else 1
     overlap = streams == 2
     launch_s = step_s if overlap else avg_kernel_s
     achieved = alg_bytes / launch_s / 1e9 if launches else None
@@ -404,7 +466,7 @@ def run(args, stage: dict) -> None:
         del host
 
     variants = {}
-    if world == 1 and args.dtype == "fp32" and args.variant_steps > 0 and args.kernel == "auto":
+    if world == 1 and (args.dtype == "fp32" or screen_bf) and args.variant_steps > 0 and args.kernel == "auto":
         # the one-pass exact fp32 kernel (RR_KERNEL_EXACT, DT 3) on the same handle: it streams the fp32 rows the
         # reference streams (retriever.py:600), and it is what a flagged block's re-run and any corpus the screen
         # cannot prune cost
@@ -413,15 +475,18 @@ def run(args, stage: dict) -> None:
         _, e_idx = ix.search(q, args.k)
         ix.set_kernel("auto")
         e_kern = e_ms / max(e_n, 1) / 1e3
-        e_ach = algorithmic_bytes(n_local, args.dim, args.batch, "fp32", args.metric) / e_kern / 1e9
-        variants["exact_fp32"] = {
+        e_ach = algorithmic_bytes(n_local, args.dim, args.batch, args.dtype, args.metric) / e_kern / 1e9
+        variants["exact_" + args.dtype] = {
             "value": round(args.batch * args.variant_steps / e_el, 2), "unit": "queries/s",
             "ms_per_step": round(e_el / args.variant_steps * 1e3, 4), "kernel_avg_us": round(e_kern * 1e6, 2),
             "achieved_GBps": round(e_ach, 1), "frac": round(e_ach / HBM_PEAK_GBS, 4), "steps": args.variant_steps,
-            "alg_bytes_per_launch": algorithmic_bytes(n_local, args.dim, args.batch, "fp32", args.metric),
+            "alg_bytes_per_launch": algorithmic_bytes(n_local, args.dim, args.batch, args.dtype, args.metric),
             "index_agreement_with_headline": round(float(np.mean(e_idx == head_idx)), 4),
-            "note": "RR_KERNEL_EXACT: sk_score_kernel DT 3 (fp32 rows, each value split exactly into 3 bf16, 6 bf16 "
-                    "MFMAs) over the fp32 rows, one pass, no screen; HIP events on every 10th launch"}
+            "note": ("RR_KERNEL_EXACT: sk_score_kernel DT 3 (fp32 rows, each value split exactly into 3 bf16, 6 bf16 "
+                     "MFMAs) over the fp32 rows, one pass, no screen; HIP events on every 10th launch"
+                     if args.dtype == "fp32" else
+                     "RR_KERNEL_EXACT: sk_score_kernel DT 1 over the bf16 rows (64 query slots, bf16 hi + lo query "
+                     "pieces), one pass, no screen; HIP events on every 10th launch")}
     if world == 1 and args.variants:
         for vd in [v for v in args.variants.split(",") if v and v != args.dtype]:
             vx = Index(devices=[local], dtype=vd, metric=args.metric)
@@ -438,6 +503,13 @@ def run(args, stage: dict) -> None:
                             "frac": round(v_ach / HBM_PEAK_GBS, 4), "steps": args.variant_steps,
                             "index_agreement_with_headline": round(float(np.mean(v_idx == head_idx)), 4)}
 
+    clustered = None
+    if world == 1 and args.dtype == "fp32" and not args.no_clustered and args.variants:
+        stage["stage"] = "clustered corpora"
+        try:
+            clustered = clustered_field(args, local, cuda_sync)
+        except Exception as e:   # reported, never fatal to the headline line
+            clustered = {"error": f"{type(e).__name__}: {e}"[:300]}
     traffic, traffic_note, mfma = None, "not measured", None
     if rank == 0 and world == 1 and not args.no_pmc:
         ix.close()                 # free HBM for the child pass
@@ -535,6 +607,7 @@ def run(args, stage: dict) -> None:
                                           "the window (bench.py timed_steps)",
                          "screened_blocks": scr_blocks, "screen_fallbacks": scr_fallbacks},
             "cpu_baseline": cpu,
+            "clustered": clustered,
             "other_dtypes": variants or None,
             "ingest": ingest,
             "dtype_note": {"fp32": "fp32 rows stored exactly; split-K kernel splits corpus and query values exactly "

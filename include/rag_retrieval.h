@@ -193,9 +193,13 @@ int rr_set_queries_device(rr_handle* h, const float* dev_q, int32_t b, int32_t d
                                fp32-split at k <= 16), else the register-streaming kernel. fp32 storage at
                                k <= 29: the screened search (an f16 screening pass of upper bounds, exact
                                rescoring of the candidates, an exact full pass when the bound cannot prove
-                               completeness) — results identical to RR_KERNEL_EXACT */
+                               completeness) — results identical to RR_KERNEL_EXACT; bf16 storage in
+                               64-query blocks (33..64 queries) at k <= 13: the screened search over its
+                               int8 copy (rr_screen_int8), verified by the bf16 pass's own arithmetic —
+                               results identical to RR_KERNEL_EXACT */
 #define RR_KERNEL_FUSED 1   /* always the register-streaming kernel (fp32: f32 MFMA) */
-#define RR_KERNEL_EXACT 2   /* split-K kernel, fp32 storage scored exactly in one pass (no screening) */
+#define RR_KERNEL_EXACT 2   /* split-K kernel, every row scored by the storage's exact arithmetic in one pass
+                               (no screening) */
 #define RR_KERNEL_SCREEN_FALLBACK 3   /* test hook: screened search whose verify always reports the block
                                          incomplete, so the exact fallback pass produces the results */
 
@@ -208,7 +212,7 @@ int rr_set_kernel(rr_handle* h, int kernel);
  * (chunks dealt round-robin). Results are identical; for A/B measurements. */
 int rr_set_schedule(rr_handle* h, int dynamic);
 
-/* Compute streams of the screened search (fp32 storage): 2 (default) = consecutive search blocks alternate
+/* Compute streams of the screened search (fp32 and bf16 storage): 2 (default) = consecutive search blocks alternate
  * between two streams, so one block's screen starts while the previous block's screen drains its last chunks
  * and its exact verify runs (the screen then leaves 32 CUs to the verify; verifies that write the same results
  * still follow each other); 1 = every block on one stream, every CU screening; -1 = leave as is. Results are
@@ -221,7 +225,7 @@ int rr_set_compute_streams(rr_handle* h, int32_t n, int32_t* in_use);
  * result still come from the fp32 rows (bit-identical results either way). The copy costs 2 bytes per element
  * of HBM and is made at load time when it fits (default). use = 1: keep one (from the next load), 0: free it
  * and screen from the fp32 rows, -1: leave as is. *present (may be null): the copy is in use on every local
- * shard. */
+ * shard. bf16 storage: the same switch for its int8 copy (rr_screen_int8), *present = that copy on every shard. */
 int rr_screen_copy(rr_handle* h, int32_t use, int32_t* present);
 
 /* The screened search's int8 copy (fp32 storage, d a multiple of 512 up to 1024, beside the f16 copy): per row a
@@ -232,7 +236,11 @@ int rr_screen_copy(rr_handle* h, int32_t use, int32_t* present);
  * at every load). Made at load time for shards of at least 65536 rows when it fits (default; RR_SCREEN_I8=0 at
  * creation: not made; RR_SCREEN_I8_MIN_ROWS: another row minimum). use = 1: screen it
  * (re-armed; from the next load if none was made), 0: screen the f16 copy, -1: leave as is. *active (may be null):
- * the next search screens the int8 copy on every local shard. */
+ * the next search screens the int8 copy on every local shard.
+ * bf16 storage: an int8 copy of the bf16 rows (half their bytes), screened against ONE int8 piece per query so that
+ * 64 query slots fit a pass, and verified by the bf16 pass's own arithmetic (DT 9 / DT 1 in rr_sk.hip); it is bf16's
+ * only screen (no f16 copy), so use = 0 (or the adaptive pause) leaves bf16 on the exact pass. Made for shards of at
+ * least 65536 rows (as above) when every row is finite. */
 int rr_screen_int8(rr_handle* h, int32_t use, int32_t* active);
 
 /* Repair mode (the adaptive screen's answer to corpora whose near-duplicate clusters defeat the screen's lists; see

@@ -241,7 +241,7 @@ struct rr_handle {
   int verify_cus = 32;           // (kVerifyCUs) CUs an overlapping screen leaves to the other stream's verify (A/B: RR_VERIFY_CUS)
   int xslots = kXSlots;         // pipelined-exchange buffer sets in use (A/B: RR_X_SLOTS, 2..kXSlots)
   int x_delay_us = 0;           // A/B: RR_X_EXCHANGE_DELAY_US, a stand-in for a slower exchange
-  int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy)
+  int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy); bf16: the int8 one
   int screen_i8 = 1;            // ... and an int8 copy, screened first (rr_screen_int8; RR_SCREEN_I8=0 at creation: off)
   int ct8 = 0;                  // the int8 screen's tiles per chunk (0: by shard size; A/B: RR_SCREEN_CT8)
   int guided = 1;               // split-K chunks: 2-tile chunks at the end of a launch (A/B: RR_SCREEN_GUIDED=0)
@@ -459,9 +459,11 @@ int alloc_corpus(rr_handle* h, Shard& s) {
       (void)hipGetLastError();
     }
   }
-  // the int8 copy (a quarter of the fp32 bytes; d a multiple of 512 up to 1024), next to the f16 one it falls back to
-  if (s.scr16 && h->screen_i8 && rows >= h->i8_min_rows && rr::sk_slabs(rr::KDT_SCREEN8, h->d) &&
-      hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+  // the int8 copy (a quarter of the fp32 bytes; d a multiple of 512 up to 1024), next to the f16 one it falls back to;
+  // bf16 storage: the int8 copy of the bf16 rows (half their bytes), its only screen (rr_sk.hip DT 9)
+  const bool bf = h->dtype == RR_DTYPE_BF16;
+  if ((s.scr16 || (bf && h->screen_copy && rows > 0)) && h->screen_i8 && rows >= h->i8_min_rows &&
+      rr::sk_slabs(bf ? rr::KDT_SCREEN9 : rr::KDT_SCREEN8, h->d) && hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
     const int64_t r2 = (rows + 1) / 2 * 2;
     const size_t need8 = (size_t)r2 * h->d + 2 * (size_t)r2 * 4;
     if (free_b > need8 + (4ull << 30)) {
@@ -469,8 +471,9 @@ int alloc_corpus(rr_handle* h, Shard& s) {
       ok = ok && hipMalloc((void**)&s.sx8, (size_t)r2 * 4) == hipSuccess;
       ok = ok && hipMalloc((void**)&s.e8, (size_t)r2 * 4) == hipSuccess;
       for (int i = 0; i < 2 && ok; ++i) {
+        // (two pieces x 32 slots, or DT 9's one piece x 64; scalars [4][64] at most)
         ok = hipMalloc((void**)&s.q8[i], (size_t)2 * rr::kQSlots * h->d) == hipSuccess;
-        ok = ok && hipMalloc((void**)&s.q8s[i], (size_t)4 * rr::kQSlots * 4) == hipSuccess;
+        ok = ok && hipMalloc((void**)&s.q8s[i], (size_t)4 * kMaxSlots * 4) == hipSuccess;
       }
       // the padding row (odd row counts) is read as the second half of the last kernel row: zeros, scale 0
       if (ok && r2 > rows) {
@@ -516,6 +519,25 @@ int finish_corpus(rr_handle* h, Shard& s, bool* screen_ok) {
     if (int rc = wait_stream(h, s, s.stream, "the corpus range check")) return rc;
     hipFree(dmax);
     *screen_ok = m < 32768.0f;   // also false for NaN
+  } else if (h->dtype == RR_DTYPE_BF16) {
+    // the bf16 screen's bound holds for finite rows: every error norm finite (a NaN or infinite value makes its row's
+    // NaN or infinite)
+    *screen_ok = true;
+    if (s.scr8 && s.rows() > 0) {
+      float* dmax = nullptr;
+      HIP_TRY(hipMalloc((void**)&dmax, sizeof(float)));
+      hipError_t e = hipMemsetAsync(dmax, 0, sizeof(float), s.stream);
+      if (e == hipSuccess) e = rr::launch_absmax(s.e8, s.rows(), dmax, s.stream);
+      float m = 0.f;
+      if (e == hipSuccess) e = hipMemcpyAsync(&m, dmax, sizeof(float), hipMemcpyDeviceToHost, s.stream);
+      if (e != hipSuccess) {
+        hipFree(dmax);
+        return fail(RR_E_HIP, "corpus range check failed: %s", hipGetErrorString(e));
+      }
+      if (int rc = wait_stream(h, s, s.stream, "the corpus range check")) return rc;
+      hipFree(dmax);
+      *screen_ok = m <= 3.0e38f;   // (false for NaN and infinity)
+    }
   }
   return wait_stream(h, s, s.stream, "the corpus norms");
 }
@@ -569,6 +591,10 @@ hipError_t store_rows(rr_handle* h, Shard& s, const float* tmp, int64_t dst_row,
   const int d = h->d;
   switch (kdt_of(h->dtype)) {
     case rr::KDT_BF16:
+      if (s.scr8)   // the int8 copy of the rows' bf16 roundings
+        if (hipError_t e = rr::launch_f32_to_i8(tmp, nr, d, s.scr8 + dst_row * d, s.sx8 + dst_row, s.e8 + dst_row,
+                                                s.stream, 1))
+          return e;
       return rr::launch_f32_to_bf16(tmp, (uint16_t*)s.corpus + dst_row * d, nr, d, s.stream);
     case rr::KDT_F32_SPLIT:
       return rr::launch_split_f32(tmp, nr, d, (float*)s.corpus + dst_row * d, s.norms + dst_row,
@@ -869,10 +895,15 @@ constexpr float kScreen8EpsB = 4.0e-8f;
 // The int8 copy screens (shards that hold one) unless turned off or given way to the f16 copy (observe_settled).
 bool i8_active(const rr_handle* h) { return h->screen_i8 && !h->i8_off && h->screen_copy; }
 
+// fp32 storage: 32-slot blocks (the int8, f16-copy or fp32-reading screen, DT 3 verify); bf16 storage: 64-slot blocks
+// over the int8 copy on every shard (DT 9 screen, DT 1 verify: the bf16 pass's own arithmetic), 16-entry lists at most.
+bool screened_bf16(const rr_handle* h, int k, int slots) {
+  return h->dtype == RR_DTYPE_BF16 && slots == kMaxSlots && i8_active(h) && h->i8_all && screen_kt(h, k) <= 16;
+}
 bool screened(const rr_handle* h, int k, int slots) {
-  return (h->kernel == RR_KERNEL_AUTO || h->kernel == RR_KERNEL_SCREEN_FALLBACK) && h->dtype == RR_DTYPE_F32 &&
-         h->screen_ok && slots == rr::kQSlots && screen_kt(h, k) != 0 && use_sk(h) &&
-         (h->screen_pause == 0 || h->kernel == RR_KERNEL_SCREEN_FALLBACK);
+  return (h->kernel == RR_KERNEL_AUTO || h->kernel == RR_KERNEL_SCREEN_FALLBACK) &&
+         ((h->dtype == RR_DTYPE_F32 && slots == rr::kQSlots) || screened_bf16(h, k, slots)) && h->screen_ok &&
+         screen_kt(h, k) != 0 && use_sk(h) && (h->screen_pause == 0 || h->kernel == RR_KERNEL_SCREEN_FALLBACK);
 }
 
 // Adaptive screen (r4): decided from SETTLED searches only — a search whose completeness the host checked when it
@@ -1169,7 +1200,7 @@ int ensure_repair(Shard& s, int64_t chunks) {
   if (chunks <= s.rcap) return RR_OK;
   const int64_t cap = std::max<int64_t>(chunks, (s.rows() + 31) / 32 + 8);
   for (int i = 0; i < 2; ++i) {
-    if (int rc = dmalloc(&s.rcmax[i], (size_t)cap * rr::kQSlots * 4)) return rc;
+    if (int rc = dmalloc(&s.rcmax[i], (size_t)cap * kMaxSlots * 4)) return rc;
     if (int rc = dmalloc(&s.rbits[i], (size_t)((cap + 31) / 32) * 4)) return rc;
     if (int rc = dmalloc(&s.rlist[i], (size_t)cap * 4)) return rc;
     if (int rc = dmalloc(&s.rcnt[i], 16)) return rc;
@@ -1245,9 +1276,11 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       if (multi) HIP_TRY(wait_px(x, cs));
       uint64_t* candp = s.cand + (size_t)p * cand_half(s);
       // the f16 copy holds exactly the values the fp32-reading screen rounds to: half the bytes
-      const bool s16 = s.scr16 && h->screen_copy && rr::sk_slabs(rr::KDT_SCREEN16, d);
+      const bool bf = h->dtype == RR_DTYPE_BF16;   // (bf16: the int8 copy, DT 9, 64 slots; verified by the bf16 pass)
+      const bool s16 = !bf && s.scr16 && h->screen_copy && rr::sk_slabs(rr::KDT_SCREEN16, d);
       // the int8 copy: a quarter of the fp32 bytes, a bound ~8x looser (more rows reach the verify's wide phase)
-      const bool s8 = s16 && s.scr8 && i8_active(h);
+      const bool s8 = bf || (s16 && s.scr8 && i8_active(h));
+      const int sdt = bf ? rr::KDT_SCREEN9 : s8 ? rr::KDT_SCREEN8 : s16 ? rr::KDT_SCREEN16 : rr::KDT_SCREEN;
       const bool alone = !two || s.last_vsi < 0 || s.last_vsi == bsi ||
                          hipEventQuery(s.ev_q[s.last_vq][s.last_vsi]) == hipSuccess;
       const int sgrid = screen_grid(h, s, alone);
@@ -1256,7 +1289,6 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       const bool rmode = h->full_lists && s.rows() > 0 && !h->ab_no_verify;
       rr::ChunkGeo geo{};
       if (rmode) {
-        const int sdt = s8 ? rr::KDT_SCREEN8 : s16 ? rr::KDT_SCREEN16 : rr::KDT_SCREEN;
         const int64_t kn = s8 ? (s.rows() + 1) / 2 : s.rows();
         geo = rr::chunk_geo((kn + 31) / 32, rr::sk_chunk_tiles(sdt, d, ct8), sgrid, h->guided != 0);
         if (int rc = ensure_repair(s, geo.C)) return rc;
@@ -1279,7 +1311,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         a.eps_b = s16 ? kScreen16EpsB : kScreenEpsB;
         if (s16) a.corpus = (const char*)s.scr16;
         if (s8) {   // the queries' int8 pieces on this stream first (the previous block's screen here is done with them)
-          HIP_TRY(rr::launch_q8_prep(qb, bb, d, s.q8[bsi], s.q8s[bsi], cs));
+          HIP_TRY(bf ? rr::launch_q8_prep(qb, bb, d, s.q8[bsi], s.q8s[bsi], cs, 1, slots)
+                     : rr::launch_q8_prep(qb, bb, d, s.q8[bsi], s.q8s[bsi], cs));
           a.corpus = (const char*)s.scr8;
           a.n = (s.rows() + 1) / 2;
           a.rows8 = s.rows();
@@ -1291,8 +1324,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
           a.eps_a = kScreen8EpsA;
           a.eps_b = kScreen8EpsB;
         }
-        HIP_TRY(rr::launch_sk_args(s8 ? rr::KDT_SCREEN8 : s16 ? rr::KDT_SCREEN16 : rr::KDT_SCREEN, h->metric, kt, 0,
-                                   sgrid, rr::kQSlots, a, cs));
+        HIP_TRY(rr::launch_sk_args(sdt, h->metric, kt, 0, sgrid, slots, a, cs));
       }
       if (timed) HIP_TRY(hipEventRecord(e1, cs));
       // results written in place (no exchange): this verify follows the previous one when that ran on the other
@@ -1310,8 +1342,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         // screen's lists, which the verify reads), slots it cannot prove mark chunks; the repair pass rescores the
         // marked chunks' rows exactly and merge_kernel joins both into the results (or this shard's exchanged keys)
         const size_t half = cand_half(s);
-        const size_t roff = ((size_t)rr::kQSlots * sgrid * (kt + 1) + 63) / 64 * 64;
-        const size_t lkeys = (size_t)rr::kQSlots * kt;
+        const size_t roff = ((size_t)slots * sgrid * (kt + 1) + 63) / 64 * 64;
+        const size_t lkeys = (size_t)slots * kt;
         const int rgrid = (int)std::min<int64_t>({255, (int64_t)s.cand_grid, (int64_t)((half - roff) / lkeys) - 1});
         uint64_t* rbase = s.cand + (size_t)p * half + roff;
         if (rmode) {
@@ -1321,9 +1353,11 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
           v.cmax = s.rcmax[p];
           v.rbits = s.rbits[p];
           v.nchunks = geo.C;
+          v.cslots = slots;
           v.repair_count = s.wcount + 1;
         }
-        HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 1, rr::kQSlots, rr::kQSlots, v, vs));
+        const int xdt = bf ? rr::KDT_BF16 : rr::KDT_F32_X3;   // the storage's exact arithmetic
+        HIP_TRY(rr::launch_sk_args(xdt, h->metric, kt, 1, slots, slots, v, vs));
         if (rmode) {
           HIP_TRY(rr::launch_compact_bits(s.rbits[p], (int)((geo.C + 31) / 32), s.rlist[p], s.rcnt[p], vs));
           rr::SkArgs r = sk_base(h, s, qb, bb);
@@ -1332,9 +1366,9 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
           r.rcount = s.rcnt[p];
           r.rs = geo;
           r.rs_rows = s8 ? 64 : 32;
-          HIP_TRY(rr::launch_sk_args(rr::KDT_F32_X3, h->metric, kt, 0, rgrid, rr::kQSlots, r, vs));
+          HIP_TRY(rr::launch_sk_args(xdt, h->metric, kt, 0, rgrid, slots, r, vs));
           HIP_TRY(rr::launch_merge(kt, rbase, rgrid + 1, kt, bb, k, multi ? s.px_keys[x] : nullptr,
-                                   multi ? nullptr : osc, multi ? nullptr : oix, vs));
+                                   multi ? nullptr : osc, multi ? nullptr : oix, vs, slots));
         }
       } else if (!h->ab_no_verify) {   // a shard without rows contributes empty lists and no flag
         HIP_TRY(hipMemsetAsync(s.px_keys[x], 0, ((size_t)slots * kt + 1) * 8, vs));
@@ -1832,8 +1866,10 @@ int rr_update_rows(rr_handle* h, const float* host_rows, const int64_t* row_idx,
   // the screen reads fp32 rows as f16 (|x| < 2^15): decided over every given row, on the host, then agreed across the
   // ranks (an RCCL min: a rank given other rows than its peers must not keep screening while they stop — the list
   // width sizes the all-gather)
+  // (bf16 storage's int8 screen: finite rows, |x| < 2^100 here)
+  const float lim = h->dtype == RR_DTYPE_BF16 ? 0x1p100f : 32768.0f;
   bool in_range = true;
-  for (int64_t e = 0; e < n_rows * (int64_t)d && in_range; ++e) in_range = fabsf(host_rows[e]) < 32768.0f;   // NaN: no
+  for (int64_t e = 0; e < n_rows * (int64_t)d && in_range; ++e) in_range = fabsf(host_rows[e]) < lim;   // NaN: no
   // the last search may still be re-run from the rows about to change: settle it, and let every stream drain
   if (int rc = rr_synchronize(h)) return rc;
   int agreed = in_range ? 1 : 0;
@@ -2359,7 +2395,8 @@ int rr_screen_copy(rr_handle* h, int32_t use, int32_t* present) {
   }
   if (present) {
     bool all = !h->shards.empty();
-    for (const Shard& s : h->shards) all = all && (s.scr16 != nullptr || s.rows() == 0);
+    const bool bf = h->dtype == RR_DTYPE_BF16;   // (bf16 storage: its int8 copy)
+    for (const Shard& s : h->shards) all = all && ((bf ? s.scr8 != nullptr : s.scr16 != nullptr) || s.rows() == 0);
     *present = all && h->screen_copy && h->loaded ? 1 : 0;
   }
   return RR_OK;
@@ -2374,7 +2411,9 @@ int rr_screen_int8(rr_handle* h, int32_t use, int32_t* active) {
   }
   if (active) {
     bool all = !h->shards.empty();
-    for (const Shard& s : h->shards) all = all && ((s.scr8 != nullptr && s.scr16 != nullptr) || s.rows() == 0);
+    const bool bf = h->dtype == RR_DTYPE_BF16;   // (bf16 storage: no f16 copy)
+    for (const Shard& s : h->shards)
+      all = all && ((s.scr8 != nullptr && (bf || s.scr16 != nullptr)) || s.rows() == 0);
     *active = all && i8_active(h) && h->loaded ? 1 : 0;
   }
   return RR_OK;

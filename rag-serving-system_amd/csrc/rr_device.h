@@ -143,19 +143,22 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
 // slots >= b get zero pieces and scalars. Run by the screen launch's joiner workgroups (rr_sk.hip, one slot each) or
 // by q8_prep_kernel (rr_kernels.hip). (Quantising in every screen workgroup instead — each redoing all 32 queries,
 // two L2 passes — measured 8-13 us longer per launch: profiles/r04/ab/int8/.)
+// PIECES = 1 (the bf16-storage screen, DT 9: q ~ s p1, pieces [QS][d], scalars [4][QS] with the scale s itself; up to 64
+// slots) or 2 (DT 8: q ~ s (p1 + p2 / 64), pieces [2][32][d], scale s / 64).
+template <int PIECES = 2, int kQS = 32>
 __device__ __forceinline__ void q8_prep_slot(const float* __restrict__ q, int b, int d, int8_t* __restrict__ q8,
                                              float* __restrict__ q8s, int slot, int lane) {
-  constexpr int kQS = 32;
   int8_t* p1 = q8 + (size_t)slot * d;
   int8_t* p2 = q8 + (size_t)(kQS + slot) * d;
   if (slot >= b) {
     for (int e = 4 * lane; e < d; e += 256) {
       *(uint32_t*)(p1 + e) = 0;
-      *(uint32_t*)(p2 + e) = 0;
+      if constexpr (PIECES == 2) *(uint32_t*)(p2 + e) = 0;
     }
     if (lane < 4) q8s[lane * kQS + slot] = 0.f;
     return;
   }
+  (void)p2;
   const f32x4* src = (const f32x4*)(q + (size_t)slot * d);
   float m = 0.f, s2 = 0.f, s1 = 0.f;
   for (int c = lane; c < (d >> 2); c += 64) {
@@ -185,22 +188,26 @@ __device__ __forceinline__ void q8_prep_slot(const float* __restrict__ q, int b,
         const float t = v[j] / s;
         a = fminf(fmaxf(rintf(t), -127.0f), 127.0f);
         const float ta = t - a;   // exact
-        cc = fminf(fmaxf(rintf(ta * 64.0f), -127.0f), 127.0f);
-        r = ta - cc * 0x1p-6f;    // exact
+        if constexpr (PIECES == 2) {
+          cc = fminf(fmaxf(rintf(ta * 64.0f), -127.0f), 127.0f);
+          r = ta - cc * 0x1p-6f;    // exact
+        } else {
+          r = ta;
+        }
       }
       w1 |= ((uint32_t)(int)a & 0xFFu) << (8 * j);
       w2 |= ((uint32_t)(int)cc & 0xFFu) << (8 * j);
       se = fmaf(r, r, se);
     }
     *(uint32_t*)(p1 + 4 * c) = w1;
-    *(uint32_t*)(p2 + 4 * c) = w2;
+    if constexpr (PIECES == 2) *(uint32_t*)(p2 + 4 * c) = w2;
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) se += __shfl_xor(se, off, 64);
   if (lane == 0) {
     q8s[slot] = sqrtf(s2);
     q8s[kQS + slot] = s1 * (1.0f + 0x1p-18f);
-    q8s[2 * kQS + slot] = s * 0x1p-6f;
+    q8s[2 * kQS + slot] = PIECES == 2 ? s * 0x1p-6f : s;
     q8s[3 * kQS + slot] = fmaf(s * sqrtf(se), 1.0f + 0x1p-12f, fmaf(m, sqrtf((float)d) * 0x1p-21f, 0x1p-140f));
   }
 }

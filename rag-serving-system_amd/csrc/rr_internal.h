@@ -34,6 +34,9 @@ constexpr int KDT_SCREEN16 = 7;
 //   KDT_SCREEN8  : the screen over an int8 copy (per-row scale, per-row error norm; a quarter of the fp32 bytes)
 //                  against the query's two int8 pieces, v_mfma_i32_32x32x32_i8 (rr_sk.hip DT 8)
 constexpr int KDT_SCREEN8 = 8;
+//   KDT_SCREEN9  : the int8 screen for bf16 storage: an int8 copy of the bf16 rows against ONE int8 piece per query, so
+//                  64 query slots fit one pass (rr_sk.hip DT 9); verified with the bf16 kernel's own arithmetic
+constexpr int KDT_SCREEN9 = 9;
 
 // Smallest fused-kernel list width KT >= k (4, 8, 16, 32); 0 if k > RR_FUSED_KMAX.
 int fused_kt(int k);
@@ -130,6 +133,7 @@ struct SkArgs {
   uint32_t* cmax;
   uint32_t* rbits;
   int rbits_words;
+  int cslots;              // MODE 1: query slots of the screen's cmax rows (32, or the bf16 screen's 64)
   int64_t nchunks;
   int* repair_count;
   const int* rlist;
@@ -152,7 +156,8 @@ size_t sk_lds_bytes(int sdt, bool cos, int ring, int qslots);
 hipError_t launch_sk(int sdt, int metric, int kt, int grid, const void* corpus, const float* norms,
                      const float* rscale, const float* queries, int64_t n, int d, int b, uint32_t idx_base,
                      uint64_t* cand, hipStream_t s, int ring = 0, int qslots = 32, uint32_t* ctr = nullptr);
-// Any mode: mode 0 (top-KT per workgroup; sdt KDT_SCREEN = the screen), mode 1 (verify, grid = 32).
+// Any mode: mode 0 (top-KT per workgroup; sdt KDT_SCREEN* = the screens), mode 1 (verify, grid = qslots: KDT_F32_X3
+// with 32 slots, or KDT_BF16 — the bf16 screen's verify — with 32 or 64).
 hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int qslots, const SkArgs& a,
                           hipStream_t s, int ring = 0);
 
@@ -224,10 +229,14 @@ hipError_t launch_f32_to_bf16(const float* in, uint16_t* out, int64_t nrows, int
 hipError_t launch_f32_to_f16(const float* in, uint16_t* out, int64_t nrows, int d, hipStream_t s);
 // fp32 rows (natural order) -> the int8 screen copy: per row sx = max|x| / 127, x8 = clamp(rint(x / sx), +-127),
 // e = an upper bound of |x - sx * x8| (rr_kernels.hip f32_to_i8_kernel)
-hipError_t launch_f32_to_i8(const float* in, int64_t nrows, int d, int8_t* out, float* sx, float* e, hipStream_t s);
+// (bf16 = 1: the rows' bf16 roundings, for bf16 storage's int8 copy)
+hipError_t launch_f32_to_i8(const float* in, int64_t nrows, int d, int8_t* out, float* sx, float* e, hipStream_t s,
+                            int bf16 = 0);
 // The int8 screen's query pieces for a block of b <= 32 queries (slots b..31 zeroed): q8 [2][32][d], q8s [4][32] =
 // |q|, sum|q|, the pieces' scale / 64, an upper bound of |q - scale * (p1 + p2 / 64)|
-hipError_t launch_q8_prep(const float* q, int b, int d, int8_t* q8, float* q8s, hipStream_t s);
+// pieces = 1 (the bf16 screen, DT 9): q ~ s p1, q8 [64][d], q8s [4][64] (scale s), for `slots` (32 or 64) slots.
+hipError_t launch_q8_prep(const float* q, int b, int d, int8_t* q8, float* q8s, hipStream_t s, int pieces = 2,
+                          int slots = 32);
 hipError_t launch_row_norms(int dtype, const void* corpus, int64_t n, int d, float* norms, hipStream_t s);
 hipError_t launch_synth(int kind, uint64_t seed, int64_t row_begin, int64_t n_rows, int d, float* out,
                         hipStream_t s);

@@ -809,16 +809,22 @@ __global__ __launch_bounds__(256) void split_f32_kernel(const float* __restrict_
 //   squares of t - x8 (in [-1/2, 1/2]: <= d / 4 + 6 roundings a chain, squares below 2^-126 add <= 2^-116 in all) and
 //   the sqrt and product within 2^-14, covered by the 2^-12 relative bump; 2^-22 sqrt(d) max|x| covers the division
 //   term 4x over, and 2^-140 what the products round away when max|x| is itself near fp32's underflow.
+// bf16: quantise the rows' bf16 roundings (RNE) — the values bf16 storage holds — instead of the fp32 values.
+__device__ __forceinline__ f32x4 bf16_round4(f32x4 v) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = (float)(__bf16)v[j];
+  return v;
+}
 __global__ __launch_bounds__(256) void f32_to_i8_kernel(const float* __restrict__ in, int64_t n, int d,
                                                         uint32_t* __restrict__ out, float* __restrict__ sx,
-                                                        float* __restrict__ e8) {
+                                                        float* __restrict__ e8, int bf16) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n) return;
   const f32x4* src = (const f32x4*)(in + row * d);
   float m = 0.f;
   for (int c = lane; c < (d >> 2); c += 64) {
-    const f32x4 v = src[c];
+    const f32x4 v = bf16 ? bf16_round4(src[c]) : src[c];
     m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
   }
 #pragma unroll
@@ -827,7 +833,7 @@ __global__ __launch_bounds__(256) void f32_to_i8_kernel(const float* __restrict_
   float ss = 0.f;
   uint32_t* dst = out + row * (d >> 2);
   for (int c = lane; c < (d >> 2); c += 64) {
-    const f32x4 v = src[c];
+    const f32x4 v = bf16 ? bf16_round4(src[c]) : src[c];
     uint32_t packed = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -851,7 +857,12 @@ __global__ __launch_bounds__(256) void f32_to_i8_kernel(const float* __restrict_
 // a screen when the screen launch does not prep them itself (rr_sk.hip: its joiner workgroups do when they run).
 __global__ __launch_bounds__(64) void q8_prep_kernel(const float* __restrict__ q, int b, int d,
                                                      int8_t* __restrict__ q8, float* __restrict__ q8s) {
-  q8_prep_slot(q, b, d, q8, q8s, (int)blockIdx.x, (int)threadIdx.x);
+  q8_prep_slot<2, 32>(q, b, d, q8, q8s, (int)blockIdx.x, (int)threadIdx.x);
+}
+// ... one piece per query, up to 64 slots (the bf16-storage screen, rr_sk.hip DT 9)
+__global__ __launch_bounds__(64) void q9_prep_kernel(const float* __restrict__ q, int b, int d,
+                                                     int8_t* __restrict__ q8, float* __restrict__ q8s) {
+  q8_prep_slot<1, 64>(q, b, d, q8, q8s, (int)blockIdx.x, (int)threadIdx.x);
 }
 
 // Repair pass (rr_sk.hip "Repair"): the set bits of `bits` -> their indices in ascending order (list) and their count,
@@ -1122,17 +1133,24 @@ hipError_t launch_f32_to_f16(const float* in, uint16_t* out, int64_t nrows, int 
   return hipGetLastError();
 }
 
-hipError_t launch_f32_to_i8(const float* in, int64_t nrows, int d, int8_t* out, float* sx, float* e, hipStream_t s) {
+hipError_t launch_f32_to_i8(const float* in, int64_t nrows, int d, int8_t* out, float* sx, float* e, hipStream_t s,
+                            int bf16) {
   if (nrows < 1 || d % 4 != 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(f32_to_i8_kernel, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, s, in, nrows, d,
-                     (uint32_t*)out, sx, e);
+                     (uint32_t*)out, sx, e, bf16);
   return hipGetLastError();
 }
 
-hipError_t launch_q8_prep(const float* q, int b, int d, int8_t* q8, float* q8s, hipStream_t s) {
-  if (b < 1 || b > kQSlots || d < 1) return hipErrorInvalidValue;
-  if (d % 4 != 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(q8_prep_kernel, dim3(kQSlots), dim3(64), 0, s, q, b, d, q8, q8s);
+hipError_t launch_q8_prep(const float* q, int b, int d, int8_t* q8, float* q8s, hipStream_t s, int pieces,
+                          int slots) {
+  if (b < 1 || d < 1 || d % 4 != 0) return hipErrorInvalidValue;
+  if (pieces == 2) {
+    if (b > kQSlots || slots != kQSlots) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(q8_prep_kernel, dim3(kQSlots), dim3(64), 0, s, q, b, d, q8, q8s);
+  } else {   // one piece: [64][d] pieces and [4][64] scalars, `slots` of them written (32 or 64)
+    if (pieces != 1 || b > slots || (slots != 32 && slots != 64)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(q9_prep_kernel, dim3(slots), dim3(64), 0, s, q, b, d, q8, q8s);
+  }
   return hipGetLastError();
 }
 
@@ -1167,7 +1185,10 @@ hipError_t launch_row_norms(int dtype, const void* corpus, int64_t n, int d, flo
 __global__ void absmax_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
   float m = 0.f;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    m = fmaxf(m, fabsf(x[i]));
+  {
+    const float v = fabsf(x[i]);
+    m = fmaxf(m, v != v ? INFINITY : v);   // (fmaxf drops NaN: a NaN counts as infinite here, so range checks fail)
+  }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
   if ((threadIdx.x & 63) == 0) atomicMax((int*)out, __float_as_int(m));   // non-negative: int order = float order

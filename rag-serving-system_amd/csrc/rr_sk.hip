@@ -89,7 +89,7 @@ __device__ unsigned long long probe2[4096 * 8];   // verify list-merge sub-phase
 __device__ unsigned long long vdiag[32 * 8];
 #define VDIAG(i, v)                                        \
   do {                                                     \
-    vdiag[vq * 8 + (i)] = (unsigned long long)(v);         \
+    vdiag[(vq & 31) * 8 + (i)] = (unsigned long long)(v);         \
   } while (0)
 #else
 #define VDIAG(i, v) \
@@ -267,6 +267,8 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 template <int NS>
 struct QFrag<8, NS> { i32x4 c1[NS][4], c2[NS][4]; };   // int8 screen: 4 K-steps of 32 per slab, two int8 pieces
+template <int NS>
+struct QFrag<9, NS> { i32x4 c1[NS][4]; };   // the bf16 storage's int8 screen: one int8 piece (64 slots fit)
 
 
 // LDS byte offset (within a slot) of 16-byte column position cp of tile row r (swizzled image)
@@ -418,7 +420,8 @@ template <int DT, int NS, int KT, bool COS, int RS, int QH, int MODE, int SCHED,
 __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const SkArgs a) {
   static_assert(RS == 2, "two slab slots per wave: one in flight while one is multiplied (the waits assume it)");
   static_assert(QH == 1 || QH == 2, "32 or 64 query slots");
-  static_assert(MODE == 0 || (DT == 3 && QH == 1), "the verify stage runs the exact fp32 arithmetic");
+  static_assert(MODE == 0 || ((DT == 3 || DT == 1) && QH == 1),
+                "the verify stage runs the storage's exact arithmetic: fp32 (DT 3) or bf16 (DT 1)");
   static_assert(SCHED == 0 || (MODE == 0 && QH == 1), "the scheduler wave serves the 32-slot streaming pass");
   constexpr int QS = 32 * QH;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -440,7 +443,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
-  constexpr bool SCR = DT == 6 || DT == 7 || DT == 8;           // the screen (upper bounds, "Screened search")
+  constexpr bool SCR = DT == 6 || DT == 7 || DT == 8 || DT == 9;   // the screen (upper bounds, "Screened search")
+  constexpr bool I8 = DT == 8 || DT == 9;                          // ... over an int8 copy (kernel rows of two rows)
   // The screen's per-lane lists hold KL keys, not KT: a query's LPQ lanes together still hold >= KT, and a lane drops
   // a key only below its own last entry. The workgroup reports the largest last entry of its full lanes as its FLOOR
   // (no key missing from its list is above max(the list's KT-th key, the floor)); the verify adds the floors to its
@@ -448,11 +452,11 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // (FL = 1: full lists, KL = KT — the handle switches to them when the short lists' floors stop the verify's
   // proofs, e.g. near-duplicate clusters whose copies crowd a few lanes; rr_api.cpp observe_settled)
   constexpr int KL = SCR && KT > 4 && !FL ? 4 : KT;
-  constexpr int EB = DT == 1 || DT == 7 ? 2 : DT == 8 ? 1 : 4;   // storage bytes per element
+  constexpr int EB = DT == 1 || DT == 7 ? 2 : I8 ? 1 : 4;   // storage bytes per element
   // the int8 screen reads two corpus rows as one kernel row (waves 0-3 the first, 4-7 the second): its tiles then
   // carry 64 KiB like the f16 copy's, 64 corpus rows each (int8 tiles of 32 rows would halve every per-tile cost's
   // share of the bytes it pays for)
-  constexpr int RPK = DT == 8 ? 2 : 1;
+  constexpr int RPK = I8 ? 2 : 1;
   const int row_bytes = d * EB * RPK;
   constexpr int KS = NS * kSlabRowBytes;                        // bytes of a row per wave
   const int p0 = w * (KS / 16);                                 // first 16-byte storage unit of the slice
@@ -461,8 +465,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   constexpr int SW = (COS || SCR ? 1 : 0) + (DT == 2 ? 1 : 0);   // per-row factors (norm, split scale)
   // LDS-DMA instructions per tile for them: one (64 lanes: 2 factors x 32 rows), or the int8 screen's three (norm,
   // scale, error norm of 64 corpus rows)
-  constexpr int FX = DT == 8 ? 3 : SW > 0 ? 1 : 0;
-  constexpr int TRS = DT == 8 ? 192 : 64;                       // floats per factor slot
+  constexpr int FX = I8 ? 3 : SW > 0 ? 1 : 0;
+  constexpr int TRS = I8 ? 192 : 64;                            // floats per factor slot
   float* trow = (float*)(smem + ring_bytes(RS) + red_bytes(RS, QH));   // [4 tiles][TRS]
   int* nxt = (int*)(trow + 4 * TRS);                            // [2] next chunk (dynamic schedule), + pad
   float* qinfo = (float*)(nxt + 4);                             // [QS] |q|, [QS] 2^-e / sum|q| / max|q|, [QS] int e
@@ -471,6 +475,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // ---- MODE 1: the candidate rows of query slot vq ---------------------------------------------------------
   // (LDS after qexp: merge scratch W [8][KT], akeys [KT], grow [32], gnorm [32], gvalid [32], xk [KT])
   const int vq = MODE == 1 ? (int)blockIdx.x : 0;
+  // (the bf16 screen's verify serves 64 slots: slot vq's data — query row, lists, chunk maxima, results — at vq, its
+  // place in this workgroup's 32-column lane mapping and query scalars at vql)
+  const int vql = vq & 31;
   uint64_t* vW = (uint64_t*)(qexp + QS);
   uint64_t* akeys = vW + kWaves * KT;
   int* grow = (int*)(akeys + KT);
@@ -484,6 +491,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // MODE 1 reads its 32 gathered rows straight into registers (all loads issued at once: one latency), the
   // exact fragments the LDS image would give: lane (r, h) takes 16-byte units 4(i>>1) + 2h + (i&1) of slab j
   f32x4 vrow[MODE == 1 ? NS : 1][4];
+  // (bf16, DT 1: K-step t's unit 2t + h)
+  auto vunit = [&](int i) { return DT == 1 ? 2 * i + h : 4 * (i >> 1) + 2 * h + (i & 1); };
   if constexpr (MODE == 1) {
     if (vq >= b) {   // padding slot: keep the exchange buffer uniform
       if (a.out_keys && tid < KT) a.out_keys[(size_t)vq * KT + tid] = 0;
@@ -498,7 +507,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   constexpr int CT0 = NS >= 4 ? 2 : NS == 3 ? 3 : NS == 2 ? 4 : 8;
   // the int8 screen: a.ct8 tiles (of 64 corpus rows) per chunk — 2 on small shards, where a 4-tile chunk is a large
   // share of a workgroup's work and the last ones leave a tail (profiles/r04/ab/ab_ct8.txt), else 4
-  const int CT = DT == 8 && a.ct8 > 0 ? a.ct8 : CT0;
+  const int CT = I8 && a.ct8 > 0 ? a.ct8 : CT0;
   const int64_t G = gridDim.x, g = blockIdx.x;
   // Guided tail: chunks of CT tiles, then (CT > 2) the last ~2 G tiles in 2-tile chunks, so the launch's last chunks —
   // the tail where workgroups finish at different times — are short (tools/probe_screen.hip: the 1M-row int8 screen's
@@ -574,7 +583,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // wave 0: the per-row factors of the tile at row base into factor slot ts (lanes 0-31: the norm, or the
   // split scale when there is no norm; lanes 32-63: the split scale next to a norm)
   auto issue_factors = [&](int64_t base, int ts) {
-    if constexpr (DT == 8) {   // corpus rows 2 base + lane: norm, scale, error norm
+    if constexpr (I8) {   // corpus rows 2 base + lane: norm, scale, error norm
       int64_t row = 2 * base + lane;
       row = row < a.rows8 ? row : a.rows8 - 1;
       glds4(norms + row, trow_lds + ts * TRS * 4);
@@ -624,7 +633,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #ifndef RR_SK_LA64
 #define RR_SK_LA64 1
 #endif
-  constexpr int LA = NS >= 2 ? (QH == 1 ? RR_SK_LOOKAHEAD : RR_SK_LA64) : 1;   // (64 slots: measured faster with 1)
+  constexpr int LA = NS >= 2 ? (QH == 1 || I8 ? RR_SK_LOOKAHEAD : RR_SK_LA64) : 1;   // (64-slot bf16: measured faster with 1)
   int pend = 0;   // LA 2: vector-memory ops this wave issued after the slab it waits for next
   int64_t chunk = g, base = cbase(chunk) * 32;
   if constexpr (MODE == 0) {
@@ -692,6 +701,12 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
             qf.c1[j][t] = *(const i32x4*)(p1 + e0);
             qf.c2[j][t] = *(const i32x4*)(p2 + e0);
           }
+        } else if constexpr (DT == 9) {
+          // one piece per query, [64][d] (slot rq = r + 32 qh), the same element mapping as DT 8
+          const int8_t* p1 = a.q8 + (size_t)rq * d;
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            qf.c1[j][t] = *(const i32x4*)(p1 + (w & (kWaves / 2 - 1)) * KS + j * kSlabRowBytes + 32 * t + 16 * h);
         } else if constexpr (DT == 7) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) {   // the bf16 layout (position 2t + h, 8 elements), f16 pieces c0 + c1
@@ -773,6 +788,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         } else if constexpr (DT == 8) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) asm volatile("" : "+v"(qfs[qh].c1[j][t]), "+v"(qfs[qh].c2[j][t]));
+        } else if constexpr (DT == 9) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) asm volatile("" : "+v"(qfs[qh].c1[j][t]));
         } else {
 #pragma unroll
           for (int t = 0; t < 2; ++t) asm volatile("" : "+v"(qfs[qh].c0[j][t]), "+v"(qfs[qh].c1[j][t]));
@@ -782,10 +800,11 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // the int8 screen's per-query scalars of this lane's epilogue query (qe below), loaded with the fragments: one
   // latency before the first barrier instead of a second one after it
   float q8pre[4] = {0.f, 0.f, 0.f, 0.f};
-  if constexpr (DT == 8) {
-    const int qe0 = 4 * w + lane / 16;
+  if constexpr (I8) {   // (scalars [4][32], or DT 9's [4][64])
+    constexpr int QSS = DT == 9 ? 64 : 32;
+    const int qe0 = 4 * QH * w + lane / (16 / QH);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) q8pre[i] = a.q8s[i * 32 + qe0];
+    for (int i = 0; i < 4; ++i) q8pre[i] = a.q8s[i * QSS + qe0];
   }
   if constexpr (MODE == 0) SK_PROBE(6);   // (diagnostic builds: prologue issued, before the fragments)
   if constexpr (DT != 2) {
@@ -821,8 +840,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         m = fmaxf(m, __shfl_xor(m, off, 64));
       }
       if (lane == 0) {
-        qinfo[vq] = sqrtf(ss);
-        qinfo[QS + vq] = m;
+        qinfo[vql] = sqrtf(ss);
+        qinfo[QS + vql] = m;
       }
     }
     __syncthreads();
@@ -832,7 +851,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     // summed per query in wave order below. No second read of the query rows: every workgroup re-reading all 32
     // rows from L2 was the larger part of the launch's start-up (8-10 us). The order of these sums differs from
     // the exact path's |q|, so the bound takes a 2^-18 relative bump for it (rr_sk.hip epilogue).
-    if constexpr (DT != 8) {   // (the int8 screen's scalars come from the query prep kernel)
+    if constexpr (!I8) {   // (the int8 screens' scalars come from the query prep kernel)
       const float ss = scr_ss + __shfl_xor(scr_ss, 32, 64), sa = scr_sa + __shfl_xor(scr_sa, 32, 64);
       float* part = (float*)vW;
       if (lane < 32) {
@@ -917,22 +936,23 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     for (int j = 0; j < NS; ++j)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        vrow[j][i] = *(const f32x4*)(src + j * kSlabRowBytes + ((4 * (i >> 1) + 2 * h + (i & 1)) << 4));
+        vrow[j][i] = *(const f32x4*)(src + j * kSlabRowBytes + (vunit(i) << 4));
   }
 
 
   // epilogue lane mapping: wave w owns queries 4·QH·w + [0, 4·QH); LPQ lanes per query, each with DPL
   // consecutive tile rows (QH 1: 16 lanes x 2 rows, QH 2: 8 lanes x 4 rows)
   constexpr int LPQ = 16 / QH, DPL = 2 * QH;
-  constexpr int DPO = DPL * RPK;   // scores per lane and tile (the int8 screen: the two corpus rows of each kernel row)
+  constexpr int DPO = DPL * RPK;
+  constexpr int NIA = DT == 8 ? 2 : DT == 9 ? QH : 1;   // int32 accumulators (DT 8: pieces p1, p2; DT 9: query halves)   // scores per lane and tile (the int8 screen: the two corpus rows of each kernel row)
   constexpr int J = (KT + LPQ - 1) / LPQ;   // (the epilogue's tighter bar: each lane's J-th list entry)
   static_assert(J <= KL, "the tighter bar reads each lane's J-th entry");
   const int qe = 4 * QH * w + lane / LPQ, er = DPL * (lane % LPQ);
-  const bool qev = MODE == 1 ? qe == vq : qe < b;
+  const bool qev = MODE == 1 ? qe == vql : qe < b;
   float qn = COS && !SCR ? qinfo[qe] : 0.f;
   const float qs = DT == 2 ? qinfo[QS + qe] : 1.f;
   float qsa = 0.f, q8sc = 0.f, q8e1 = 0.f, q8e2 = 0.f, q8e3 = 0.f;
-  if constexpr (DT == 8) {
+  if constexpr (I8) {
     qn = q8pre[0];   // (a.q8s[i * QS + qe], loaded before the first barrier)
     qsa = q8pre[1];
     q8sc = q8pre[2];
@@ -1015,7 +1035,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       }
       // rows of this tile (scalar; 32 except in the last tile): the screen's validity test is one 32-bit compare
       // (the int8 screen: corpus rows of this 64-row tile, lane rows 2 er .. 2 er + 3)
-      const int rem = DT == 8 ? (int)(a.rows8 - 2 * bse < 64 ? a.rows8 - 2 * bse : 64)
+      const int rem = I8 ? (int)(a.rows8 - 2 * bse < 64 ? a.rows8 - 2 * bse : 64)
                               : MODE == 0 ? (int)(n - bse < 32 ? n - bse : 32) : 32;
       const uint32_t key_base = MODE == 0 ? idx_base + (uint32_t)(RPK * bse) : 0u;
       const int ero = RPK * er;   // this lane's first tile row
@@ -1031,14 +1051,17 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       const float thf = th != 0 ? float_of_ord(th) : -INFINITY;   // dot: the bar's float (ord order = float order)
       // this lane's per-row factors, one vector LDS read each (factor 0 at [0, 32), factor 1 at [32, 64))
       float fac0[DPO], fac1[DPO], fac2[DPO];
-      if constexpr (DT == 8) {   // norm, scale, error norm of corpus rows 2 er .. 2 er + 3 (16-byte aligned)
+      if constexpr (I8) {   // norm, scale, error norm of corpus rows 2 er .. 2 er + DPO - 1 (16-byte aligned)
         const float* tf = trow + tsl * TRS + ero;
-        const f32x4 v0 = *(const f32x4*)tf, v1 = *(const f32x4*)(tf + 64), v2 = *(const f32x4*)(tf + 128);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          fac0[e] = v0[e];
-          fac1[e] = v1[e];
-          fac2[e] = v2[e];
+        for (int e4 = 0; e4 < DPO; e4 += 4) {
+          const f32x4 v0 = *(const f32x4*)(tf + e4), v1 = *(const f32x4*)(tf + 64 + e4), v2 = *(const f32x4*)(tf + 128 + e4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            fac0[e4 + e] = v0[e];
+            fac1[e4 + e] = v1[e];
+            fac2[e4 + e] = v2[e];
+          }
         }
       } else if constexpr (MODE == 0 && (COS || SCR || DT == 2)) {
         const float* tf = trow + tsl * 64 + er;
@@ -1091,8 +1114,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           // upper bound of the exact (DT 3) score, see "Screened search"; the relative bumps cover the
           // roundings of the bound's own arithmetic and of the reciprocal (<= 1 ulp)
           float v;
-          if constexpr (DT == 8) {
-            // int8 screen: s = x8 . (64 p1 + p2) exactly (int32, rounded once to fp32); x . q = sx s scale + q~ . rx
+          if constexpr (I8) {
+            // int8 screen: s = x8 . (64 p1 + p2) exactly (DT 9: x8 . p1) (int32, rounded once to fp32); x . q = sx s scale + q~ . rx
             // + eq . x with |q~ . rx| <= (|q| + eq) e and |eq . x| <= eq |x|, plus the exact DT 3 score's own error
             // (eps_a |x||q| + eps_b (sqrt(d) |x| + sum|q|), rr_api.cpp kScreen8EpsA/B; eps_b sum|q| also covers
             // residuals whose squares underflow fp32 in e, |r| < 2^-63); x 1.001 for the roundings of
@@ -1187,7 +1210,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #endif
   // (Rejected and removed: exchanging a tile's K-partials one tile late behind the next tile's MFMAs, -2 % on the
   // 64-slot pass, profiles/r03/b/ab_pipelined_exchange_rejected.txt; deferring the odd waves instead of 4-7.)
-  constexpr bool STG = MODE == 0 && FL != 2 && !(QH == 2 && DT == 2) && DT != 6 && (DT != 8 || RR_SK_STAGGER8) &&
+  constexpr bool STG = MODE == 0 && FL != 2 && !(QH == 2 && DT == 2) && DT != 6 && (!I8 || RR_SK_STAGGER8) &&
                        KT <= 16 &&   // (measured)
                        (RR_SK_STAGGER == 2 || (RR_SK_STAGGER == 1 && QH == 2));
   const bool defer = STG && w >= 4;
@@ -1219,22 +1242,35 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       *(i32x4*)(rb + (w * QS + r) * kRedRow + 4 * ((2 * a4 + h) ^ (r & 7))) = v;
     }
   };
+  // DT 9: each query half's accumulator as int32 bits (|.| < 2^23), the 64-slot layout of write_partials
+  auto write_partials9 = [&](float* rb, const i32x16 (&ia)[NIA]) {
+#pragma unroll
+    for (int qh = 0; qh < QH; ++qh)
+#pragma unroll
+      for (int a4 = 0; a4 < 4; ++a4) {
+        const i32x4 v = {ia[qh][4 * a4], ia[qh][4 * a4 + 1], ia[qh][4 * a4 + 2], ia[qh][4 * a4 + 3]};
+        const int rq = 32 * qh + r;
+        *(i32x4*)(rb + (w * QS + rq) * kRedRow + 4 * ((2 * a4 + h) ^ (rq & 7))) = v;
+      }
+  };
   // ... and summed exactly in int32 (|sum| < 2^31): waves 0-3 give the kernel rows' first corpus rows, 4-7 the second;
-  // sv = corpus rows 2 er, 2 er + 1, 2 er + 2, 2 er + 3, each rounded once to fp32
+  // sv = corpus rows 2 er, 2 er + 1, ..., 2 (er + DPL) - 1, each rounded once to fp32
   auto read_partials8 = [&](const float* rb, float (&sv)[DPO]) {
     typedef int i32x2 __attribute__((ext_vector_type(2)));
-    i32x2 ev = {0, 0}, od = {0, 0};
+    typedef int i32xd __attribute__((ext_vector_type(DPL)));
+    i32xd ev, od;
 #pragma unroll
     for (int ww = 0; ww < kWaves; ++ww) {
-      const i32x2 p = *(const i32x2*)(rb + (ww * QS + qe) * kRedRow + 4 * ((er >> 2) ^ (qe & 7)) + (er & 3));
-      if (ww < kWaves / 2) ev += p;
+      const i32xd p = *(const i32xd*)(rb + (ww * QS + qe) * kRedRow + 4 * ((er >> 2) ^ (qe & 7)) + (er & 3));
+      if (ww == 0) ev = p;
+      else if (ww < kWaves / 2) ev += p;
+      else if (ww == kWaves / 2) od = p;
       else od += p;
     }
-    if constexpr (DPO == 4) {
-      sv[0] = (float)ev[0];
-      sv[1] = (float)od[0];
-      sv[2] = (float)ev[1];
-      sv[3] = (float)od[1];
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) {
+      sv[2 * i] = (float)ev[i];
+      sv[2 * i + 1] = (float)od[i];
     }
   };
   // (two-float vectors: packed adds, each element summed in the same wave order)
@@ -1264,7 +1300,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #define RR_SK_PRIO 1
 #endif
   // (not the int8 screen, which runs without the stagger: +1.5-3 % without it, profiles/r04/ab/ab_i8_prio.txt)
-  if (MODE == 0 && DT != 8 && ((RR_SK_PRIO == 1 && w >= 4) || (RR_SK_PRIO == 2 && w < 4))) __builtin_amdgcn_s_setprio(1);
+  if (MODE == 0 && !I8 && ((RR_SK_PRIO == 1 && w >= 4) || (RR_SK_PRIO == 2 && w < 4))) __builtin_amdgcn_s_setprio(1);
   unsigned long long ph_t = PH_NOW();
   (void)ph_t;
   SK_PROBE(1);
@@ -1280,10 +1316,12 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     for (int qh = 0; qh < QH; ++qh)
 #pragma unroll
       for (int i = 0; i < 16; ++i) accs[qh][i] = 0.f;
-    i32x16 iacc[DT == 8 ? 2 : 1];   // the int8 screen's accumulators (pieces p1, p2)
-    if constexpr (DT == 8)
+    i32x16 iacc[NIA];   // the int8 screens' accumulators (DT 8: pieces p1, p2; DT 9: the query halves)
+    if constexpr (I8)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) iacc[0][i] = iacc[1][i] = 0;
+      for (int u = 0; u < NIA; ++u)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) iacc[u][i] = 0;
     // LA 2: after slab j's fragments are read, its slot takes slab j + 2 — of this tile, or slab 0 / 1 of the
     // next tile (found at slab NS - 2; wave 0 issues that tile's factors before its slab 0)
     auto issue_ahead = [&](auto jc) {
@@ -1363,7 +1401,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       } else if constexpr (DT == 1) {
         bf16x8 av[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) av[t] = *(const bf16x8*)(sl + slab_off(r, 2 * t + h));
+        for (int t = 0; t < 4; ++t)
+          av[t] = MODE == 1 ? __builtin_bit_cast(bf16x8, vrow[MODE == 1 ? j : 0][t]) : *(const bf16x8*)(sl + slab_off(r, 2 * t + h));
         if constexpr (MODE == 0 && LA == 2) issue_ahead(jc);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -1389,6 +1428,14 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           iacc[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[t], qfs[0].c1[j][t], iacc[0], 0, 0, 0);
           iacc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[t], qfs[0].c2[j][t], iacc[1], 0, 0, 0);
         }
+      } else if constexpr (DT == 9) {   // bf16 storage's int8 screen: one piece per query, both query halves
+        i32x4 av[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) av[t] = *(const i32x4*)(sl + slab_off(r, 2 * t + h));
+        if constexpr (MODE == 0 && LA == 2) issue_ahead(jc);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          for (int qh = 0; qh < QH; ++qh) iacc[qh] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[t], qfs[qh].c1[j][t], iacc[qh], 0, 0, 0);
       } else if constexpr (DT == 2) {
         f16x8 ah[2], al[2];
 #pragma unroll
@@ -1473,11 +1520,12 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       }
       const unsigned long long pt2 = PH_NOW();
       if constexpr (DT == 8) write_partials8(rb, iacc);
+      else if constexpr (DT == 9) write_partials9(rb, iacc);
       else write_partials(rb, accs);
       lds_barrier();   // (also publishes wave 0's LDS-DMA factors and its next-chunk word)
       const unsigned long long pt3 = PH_NOW();
       float sv[DPO];
-      if constexpr (DT == 8) read_partials8(rb, sv);
+      if constexpr (I8) read_partials8(rb, sv);
       else read_partials(rb, sv);
 #if defined(RR_SK_DIAG) && (RR_SK_DIAG & 4)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1581,15 +1629,15 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   } else if constexpr (MODE == 1) {
     // The wave that owns query slot vq (QH 1: queries 4w..4w+3) merges its lanes' lists into xk; its leader lane
     // checks completeness and writes the results. Every wave stays: a second, wide phase may follow.
-    const bool owner = w == vq / 4;
-    const bool leader = owner && qe == vq && lane % LPQ == 0;
+    const bool owner = w == vql / 4;
+    const bool leader = owner && qe == vql && lane % LPQ == 0;
     auto lane_merge = [&]() {
       if (owner) {
 #pragma unroll 1
         for (int rnd = 0; rnd < KT; ++rnd) {
           const uint64_t m = group_max_u64<LPQ>(tk.v[0]);
           if (m != 0 && tk.v[0] == m) tk.pop();
-          if (qe == vq && lane % LPQ == 0) xk[rnd] = m;
+          if (qe == vql && lane % LPQ == 0) xk[rnd] = m;
         }
       }
     };
@@ -1599,7 +1647,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     // bound >= its exact score >= the true k-th score >= ek's; they are marked in rbits (mark, every thread, below) and
     // the repair pass merges their exact keys with xk (written to out_keys). Returns whether the slot needs it.
     auto finish = [&](bool complete) -> bool {
-      const bool range = qinfo[QS + vq] < 32768.0f && !a.force_incomplete;   // f16 range of the screen
+      const bool range = qinfo[QS + vql] < 32768.0f && !a.force_incomplete;   // f16 range of the screen
       const bool repair = a.rbits != nullptr && !complete && range;
       complete = complete && range;
       if (!complete && !repair) {   // the first query slot to flag the block also counts it
@@ -1622,7 +1670,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     // repair mode: every chunk whose largest bound for this slot reaches bar (an ord), marked for the repair pass
     auto mark = [&](uint32_t bar) {
       for (int64_t c = tid; c < a.nchunks; c += kThreads)
-        if (a.cmax[(size_t)c * QS + vq] >= bar) atomicOr(&a.rbits[c >> 5], 1u << (c & 31));
+        if (a.cmax[(size_t)c * (a.cslots ? a.cslots : 32) + vq] >= bar) atomicOr(&a.rbits[c >> 5], 1u << (c & 31));
     };
     lane_merge();
     if (leader) {
@@ -1635,7 +1683,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       // bound of any single list (vtail): every key left out of every list is below that.
       const uint64_t tb = *vtail;
       const uint32_t rbar = wide_bar(ek, tb);
-      const bool wide = !complete && a.wide_verify && !a.force_incomplete && qinfo[QS + vq] < 32768.0f &&
+      const bool wide = !complete && a.wide_verify && !a.force_incomplete && qinfo[QS + vql] < 32768.0f &&
                         ((uint32_t)(ek >> 32) > (uint32_t)(tb >> 32) ||
                          (uint32_t)(akeys[a.k_out - 1] >> 32) > (uint32_t)(tb >> 32));
       vstate[0] = wide ? 1 : 0;
@@ -1697,7 +1745,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       for (int j = 0; j < NS; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          vrow[j][i] = *(const f32x4*)(src + j * kSlabRowBytes + ((4 * (i >> 1) + 2 * h + (i & 1)) << 4));
+          vrow[j][i] = *(const f32x4*)(src + j * kSlabRowBytes + (vunit(i) << 4));
       int erow[DPL];
       float end[DPL];
 #pragma unroll
@@ -1711,18 +1759,27 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 #pragma unroll
       for (int j = 0; j < NS; ++j) {
+        if constexpr (DT == 1) {   // the bf16 pass's MFMAs: per K-step, hi then lo
 #pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-          const f32x4 v0 = vrow[j][2 * tt], v1 = vrow[j][2 * tt + 1];
-          const float x[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-          bf16x8 b0, b1, b2;
-          split3(x, b0, b1, b2);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[0].c0[j][tt], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[0].c1[j][tt], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qfs[0].c0[j][tt], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qfs[0].c1[j][tt], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[0].c2[j][tt], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, qfs[0].c0[j][tt], acc, 0, 0, 0);
+          for (int tt = 0; tt < 4; ++tt) {
+            const bf16x8 ab = __builtin_bit_cast(bf16x8, vrow[j][tt]);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ab, qfs[0].hi[j][tt], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ab, qfs[0].lo[j][tt], acc, 0, 0, 0);
+          }
+        } else {
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt) {
+            const f32x4 v0 = vrow[j][2 * tt], v1 = vrow[j][2 * tt + 1];
+            const float x[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+            bf16x8 b0, b1, b2;
+            split3(x, b0, b1, b2);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[0].c0[j][tt], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[0].c1[j][tt], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qfs[0].c0[j][tt], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b1, qfs[0].c1[j][tt], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b0, qfs[0].c2[j][tt], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b2, qfs[0].c0[j][tt], acc, 0, 0, 0);
+          }
         }
       }
       // K-partials through LDS in the fixed wave order (the first tile used buffer 0: alternate from 1)
@@ -1821,9 +1878,9 @@ hipError_t launch_ns(int ns, int kt, int grid, const SkArgs& a, hipStream_t s) {
   switch (ns) {
     case 1: return launch_kt<DT, 1, COS, RS, QH, MODE, SCHED, FL>(kt, grid, a, s);
     case 2: return launch_kt<DT, 2, COS, RS, QH, MODE, SCHED, FL>(kt, grid, a, s);
-    case 3: if constexpr (DT != 1 && DT != 7 && DT != 8) return launch_kt<DT, 3, COS, RS, QH, MODE, SCHED, FL>(kt, grid, a, s);
+    case 3: if constexpr (DT != 1 && DT != 7 && DT != 8 && DT != 9) return launch_kt<DT, 3, COS, RS, QH, MODE, SCHED, FL>(kt, grid, a, s);
             else return hipErrorInvalidValue;
-    case 4: if constexpr (DT != 1 && DT != 7 && DT != 8) return launch_kt<DT, 4, COS, RS, QH, MODE, SCHED, FL>(kt, grid, a, s);
+    case 4: if constexpr (DT != 1 && DT != 7 && DT != 8 && DT != 9) return launch_kt<DT, 4, COS, RS, QH, MODE, SCHED, FL>(kt, grid, a, s);
             else return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
@@ -1843,19 +1900,19 @@ size_t sk_lds_bytes(int sdt, bool cos, int ring, int qslots) {
   // scratch: W [8][32] + akeys [32] keys, grow / gnorm / gvalid [32], xk [32] keys, the floors' and the list bounds'
   // maxima, 6 ints
   const size_t verify = (size_t)(kWaves * 32 + 32 + 32 + 8) * 8 + 3 * 32 * 4;
-  const size_t factors = (size_t)4 * (sdt == KDT_SCREEN8 ? 192 : 64) * 4;
+  const size_t factors = (size_t)4 * (sdt == KDT_SCREEN8 || sdt == KDT_SCREEN9 ? 192 : 64) * 4;
   return sk::ring_bytes(ring) + sk::red_bytes(ring, qslots / 32) + factors + 4 * 4 + 3 * qslots * 4 + verify;
 }
 
 bool sk_supports_64(int sdt) { return sdt == KDT_BF16 || sdt == KDT_F32_SPLIT; }
 int sk_chunk_tiles(int sdt, int d, int ct8) {   // (the kernel's CT: CT0 by slabs per wave, or the int8 screen's ct8)
   const int ns = sk_slabs(sdt == KDT_SCREEN ? KDT_F32_X3 : sdt, d);
-  if (sdt == KDT_SCREEN8 && ct8 > 0) return ct8;
+  if ((sdt == KDT_SCREEN8 || sdt == KDT_SCREEN9) && ct8 > 0) return ct8;
   return ns >= 4 ? 2 : ns == 3 ? 3 : ns == 2 ? 4 : 8;
 }
 int sk_slabs(int sdt, int d) {
   // (the int8 screen: kernel rows of two corpus rows, 2 d bytes)
-  const int eb = sdt == KDT_BF16 || sdt == KDT_SCREEN16 || sdt == KDT_SCREEN8 ? 2 : 4;
+  const int eb = sdt == KDT_BF16 || sdt == KDT_SCREEN16 || sdt == KDT_SCREEN8 || sdt == KDT_SCREEN9 ? 2 : 4;
   const int ks = d * eb / kWaves;   // row bytes per wave
   if (d <= 0 || ks % sk::kSlabRowBytes != 0) return 0;
   const int ns = ks / sk::kSlabRowBytes;
@@ -1868,8 +1925,10 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
   const int ns = sk_slabs(sdt == KDT_SCREEN ? KDT_F32_X3 : sdt, a.d);
   if (!ns || a.b < 1 || a.b > qslots || a.n < 1 || (qslots != 32 && qslots != 64)) return hipErrorInvalidValue;
   if (ring == 0) ring = kSkRing;
-  if (mode == 1) {   // verify: exact fp32 arithmetic, 32 slots, one workgroup per query slot
-    if (sdt != KDT_F32_X3 || qslots != 32 || ring != 2 || grid != 32) return hipErrorInvalidValue;
+  if (mode == 1) {   // verify, one workgroup per query slot: exact fp32 arithmetic (32 slots) or bf16's (32 or 64)
+    if (ring != 2 || grid != qslots || kt > 16 + 16 * (qslots == 32)) return hipErrorInvalidValue;
+    if (sdt == KDT_BF16) return sk::launch_metric<1, 2, 1, 1>(metric, ns, kt, grid, a, s);
+    if (sdt != KDT_F32_X3 || qslots != 32) return hipErrorInvalidValue;
     return sk::launch_metric<3, 2, 1, 1>(metric, ns, kt, grid, a, s);
   }
   // the screen: dynamic schedule (9-wave form) when asked for and the lists fit its registers; short or full
@@ -1899,6 +1958,16 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
                  : sk::launch_metric<8, 2, 1, 0, 0, 1>(metric, ns8, kt, grid, a, s);
     return dyn ? sk::launch_metric<8, 2, 1, 0, 1>(metric, ns8, kt, grid, a, s)
                : sk::launch_metric<8, 2, 1>(metric, ns8, kt, grid, a, s);
+  }
+  if (sdt == KDT_SCREEN9) {   // bf16 storage's int8 screen: 64 slots, one query piece (a.q8 [64][d], a.q8s [4][64])
+    const int ns8 = sk_slabs(KDT_SCREEN9, a.d);
+    if (qslots != 64 || ring != 2 || !ns8 || kt > 16 || !a.q8 || !a.q8s || !a.sx8 || !a.e8 ||
+        a.n != (a.rows8 + 1) / 2)
+      return hipErrorInvalidValue;
+    // static schedule with the guided tail only: the 9-wave form's register budget (168) spills 10-39 VGPRs here
+    if (a.full_lists == 2) return sk::launch_metric<9, 2, 2, 0, 0, 2>(metric, ns8, kt, grid, a, s);
+    if (a.full_lists) return sk::launch_metric<9, 2, 2, 0, 0, 1>(metric, ns8, kt, grid, a, s);
+    return sk::launch_metric<9, 2, 2>(metric, ns8, kt, grid, a, s);
   }
   if (sdt == KDT_SCREEN16) {   // the screen over the f16 copy (a.corpus = that copy)
     const int ns16 = sk_slabs(KDT_SCREEN16, a.d);

@@ -316,7 +316,7 @@ class Index:
                "screen-fallback": RR_KERNEL_SCREEN_FALLBACK}
 
     def set_kernel(self, kernel: str) -> None:
-        """'auto' (split-K LDS-DMA kernel where the shape allows; fp32 storage: the screened search),
+        """'auto' (split-K LDS-DMA kernel where the shape allows; the screened search for fp32 storage and 64-slot bf16 blocks),
         'exact' (split-K, fp32 scored exactly in one pass), 'fused' (register-streaming kernel) or
         'screen-fallback' (test hook: the screened search's exact fallback pass always runs)."""
         _check(self._lib.rr_set_kernel(self._h, self.KERNELS[kernel]))
