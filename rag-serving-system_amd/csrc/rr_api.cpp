@@ -58,7 +58,7 @@ constexpr int kXSlots = 4;   // pipelined-exchange buffer sets (Shard::px_keys)
 // rr_search_staged, [1] the pipelined exchange's enqueue, [2] the ncclAllGather call alone, [3] the screened block's
 // screen + verify launches; nanoseconds and calls.
 struct HostProf {
-  int64_t ns[4] = {0, 0, 0, 0}, n[4] = {0, 0, 0, 0};
+  int64_t ns[10] = {}, n[10] = {};
 };
 inline int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
@@ -334,6 +334,17 @@ std::string wait_label(const rr_handle* h, const Shard& s, const char* stream, c
            s.dev, stream, what);
   return buf;
 }
+// Stream st waits for event ev — unless ev has already completed, which orders nothing. A cross-stream wait costs HIP a
+// barrier packet and ~4.5 us of host time on the next launch of st (tools/api_cost.hip: record + wait + launch 8.7 us
+// against 4.1 us for the three calls apart); the query costs 0.08 us. Most of a search block's waits (buffer slots four
+// blocks back, the other stream's last staging) are long complete when the block is enqueued.
+hipError_t wait_ev(hipStream_t st, hipEvent_t ev) {
+  const hipError_t q = hipEventQuery(ev);
+  if (q == hipSuccess) return hipSuccess;
+  if (q != hipErrorNotReady) return q;
+  return hipStreamWaitEvent(st, ev, 0);
+}
+
 int wait_stream(rr_handle* h, const Shard& s, hipStream_t st, const char* what = "device work", int scale = 1) {
   if (!deadline_on(h)) {
     HIP_TRY(hipStreamSynchronize(st));
@@ -1025,7 +1036,7 @@ hipStream_t cstream(const rr_handle* h, const Shard& s, int p) { return stream_o
 int join_main(Shard& s) {
   if (!s.c2_busy) return RR_OK;
   HIP_TRY(hipEventRecord(s.ev_join, s.cstream2));
-  HIP_TRY(hipStreamWaitEvent(s.stream, s.ev_join, 0));
+  HIP_TRY(wait_ev(s.stream, s.ev_join));
   s.c2_busy = false;
   return RR_OK;
 }
@@ -1052,10 +1063,10 @@ int stage_queries(rr_handle* h, int t, const void* src, size_t bytes, int src_de
     const int x = block_si(h, s, h->parity);
     const hipStream_t xs = stream_of(s, x);
     if (two) {
-      if (s.q_rd[t][x ^ 1]) HIP_TRY(hipStreamWaitEvent(xs, s.ev_q[t][x ^ 1], 0));   // its last readers there
+      if (s.q_rd[t][x ^ 1]) HIP_TRY(wait_ev(xs, s.ev_q[t][x ^ 1]));   // its last readers there
       s.q_rd[t][x ^ 1] = false;
       if (x == 1) {   // after other kinds of search on `stream` (they read query buffers too)
-        if (s.fork_pending) HIP_TRY(hipStreamWaitEvent(xs, s.ev_fork, 0));
+        if (s.fork_pending) HIP_TRY(wait_ev(xs, s.ev_fork));
         s.fork_pending = false;
         s.c2_busy = true;
       }
@@ -1089,7 +1100,7 @@ int local_gather(rr_handle* h, size_t per) {
     HIP_TRY(hipSetDevice(dst.dev));
     for (size_t i = 0; i < h->shards.size(); ++i) {
       const Shard& src = h->shards[i];
-      if (&src != &dst) HIP_TRY(hipStreamWaitEvent(dst.stream, src.keys_ready, 0));
+      if (&src != &dst) HIP_TRY(wait_ev(dst.stream, src.keys_ready));
       HIP_TRY(hipMemcpyPeerAsync(dst.gathered + i * per, dst.dev, src.shard_keys, src.dev, bytes,
                                  dst.stream));
     }
@@ -1110,27 +1121,40 @@ int issue_exchange(rr_handle* h, int x, int q0, int bb, int k, int kt, int slots
   for (Shard& dst : h->shards) {
     HIP_TRY(hipSetDevice(dst.dev));
     const hipStream_t xs = lane ? dst.xstream2 : dst.xstream;
+    int64_t tp = ns_gather ? now_ns() : 0;
+    auto lap = [&](int slot) {   // (RR_HOST_PROF: per-call host time)
+      if (!ns_gather) return;
+      const int64_t t = now_ns();
+      h->hp.ns[slot] += t - tp;
+      ++h->hp.n[slot];
+      tp = t;
+    };
     if (h->dist) {
-      HIP_TRY(hipStreamWaitEvent(xs, dst.ev_keys[x], 0));
+      HIP_TRY(wait_ev(xs, dst.ev_keys[x]));
+      lap(5);
       const int64_t ta = ns_gather ? now_ns() : 0;
       NCCL_TRY(ncclAllGather(dst.px_keys[x], dst.px_gathered[x], slot, ncclUint64, lane ? dst.comm2 : dst.comm, xs));
       if (ns_gather) *ns_gather += now_ns() - ta;
+      tp = ns_gather ? now_ns() : 0;
     } else {
       for (size_t i = 0; i < h->shards.size(); ++i) {
         const Shard& src = h->shards[i];
-        HIP_TRY(hipStreamWaitEvent(xs, src.ev_keys[x], 0));
+        HIP_TRY(wait_ev(xs, src.ev_keys[x]));
         HIP_TRY(hipMemcpyPeerAsync(dst.px_gathered[x] + i * slot, dst.dev, src.px_keys[x], src.dev, slot * 8, xs));
       }
     }
     if (h->x_delay_us > 0) HIP_TRY(rr::launch_delay(h->x_delay_us, xs));   // (A/B: a slower exchange)
-    if (dst.last_x >= 0 && (dst.last_x & 1) != lane) HIP_TRY(hipStreamWaitEvent(xs, dst.ev_xdone[dst.last_x], 0));
+    if (dst.last_x >= 0 && (dst.last_x & 1) != lane) HIP_TRY(wait_ev(xs, dst.ev_xdone[dst.last_x]));
+    lap(5);
     if (dst.rcopy_pending) {   // an asynchronous search's result copy still reads these rows (later merges follow this one)
-      HIP_TRY(hipStreamWaitEvent(xs, dst.ev_rcopy, 0));
+      HIP_TRY(wait_ev(xs, dst.ev_rcopy));
       dst.rcopy_pending = false;
     }
     HIP_TRY(rr::launch_merge(kt, dst.px_gathered[x], h->world, kt, bb, k, nullptr, dst.out_scores + (size_t)q0 * k,
                              dst.out_idx + (size_t)q0 * k, xs, slots, (int64_t)slot, (uint64_t*)dst.out_base));
+    lap(6);
     HIP_TRY(hipEventRecord(dst.ev_xdone[x], xs));
+    lap(7);
     dst.last_x = x;
   }
   return RR_OK;
@@ -1139,9 +1163,14 @@ int issue_exchange(rr_handle* h, int x, int q0, int bb, int k, int kt, int slots
 // Pipelined exchange of the block just scored into px_keys[x] (k <= RR_FUSED_KMAX, an exchange step): ev_keys[x] on the
 // block's compute stream, then the exchange's stream operations.
 int enqueue_exchange_px(rr_handle* h, int p, int x, int q0, int bb, int k, int kt, int slots, bool scr) {
+  const int64_t tk = h->host_prof ? now_ns() : 0;
   for (Shard& s : h->shards) {   // px_keys[x] is written on the block's compute stream (a screened block: its parity's)
     HIP_TRY(hipSetDevice(s.dev));
     HIP_TRY(hipEventRecord(s.ev_keys[x], scr ? cstream(h, s, p) : s.stream));
+  }
+  if (h->host_prof) {
+    h->hp.ns[4] += now_ns() - tk;
+    ++h->hp.n[4];
   }
   int64_t ng = 0;
   const int rc = issue_exchange(h, x, q0, bb, k, kt, slots, h->host_prof ? &ng : nullptr);
@@ -1232,7 +1261,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       if (local_multi)
         for (const Shard& o : h->shards)
           if (&o != &s)
-            if (hipError_t e = hipStreamWaitEvent(s.stream, o.copies_done, 0)) return e;
+            if (hipError_t e = wait_ev(s.stream, o.copies_done)) return e;
       return hipSuccess;
     };
     // pipelined exchange: px_keys[x] is rewritten only after every exchange that read it has finished
@@ -1242,7 +1271,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         if (slot < 0 || xs == slot)
           for (const Shard& o : h->shards)
             if (&o == &s || local_multi)
-              if (hipError_t e = hipStreamWaitEvent(ws, o.ev_xdone[xs], 0)) return e;
+              if (hipError_t e = wait_ev(ws, o.ev_xdone[xs])) return e;
       return hipSuccess;
     };
     const float* qb = s.qbuf[h->qpar] + (size_t)q0 * d;
@@ -1265,10 +1294,10 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       const int bsi = block_si(h, s, p), t = h->qpar;
       const hipStream_t cs = stream_of(s, bsi), vs = cs;
       if (two) {
-        if (s.stage_pending && bsi != s.stage_si) HIP_TRY(hipStreamWaitEvent(cs, s.ev_stage, 0));
+        if (s.stage_pending && bsi != s.stage_si) HIP_TRY(wait_ev(cs, s.ev_stage));
         if (bsi != s.stage_si) s.stage_pending = false;
         if (bsi == 1) {
-          if (s.fork_pending) HIP_TRY(hipStreamWaitEvent(cs, s.ev_fork, 0));
+          if (s.fork_pending) HIP_TRY(wait_ev(cs, s.ev_fork));
           s.fork_pending = false;
           s.c2_busy = true;
         }
@@ -1311,8 +1340,13 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         a.eps_b = s16 ? kScreen16EpsB : kScreenEpsB;
         if (s16) a.corpus = (const char*)s.scr16;
         if (s8) {   // the queries' int8 pieces on this stream first (the previous block's screen here is done with them)
+          const int64_t tq = h->host_prof ? now_ns() : 0;
           HIP_TRY(bf ? rr::launch_q8_prep(qb, bb, d, s.q8[bsi], s.q8s[bsi], cs, 1, slots)
                      : rr::launch_q8_prep(qb, bb, d, s.q8[bsi], s.q8s[bsi], cs));
+          if (h->host_prof) {
+            h->hp.ns[8] += now_ns() - tq;
+            ++h->hp.n[8];
+          }
           a.corpus = (const char*)s.scr8;
           a.n = (s.rows() + 1) / 2;
           a.rows8 = s.rows();
@@ -1324,13 +1358,18 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
           a.eps_a = kScreen8EpsA;
           a.eps_b = kScreen8EpsB;
         }
+        const int64_t tsc = h->host_prof ? now_ns() : 0;
         HIP_TRY(rr::launch_sk_args(sdt, h->metric, kt, 0, sgrid, slots, a, cs));
+        if (h->host_prof) {
+          h->hp.ns[9] += now_ns() - tsc;
+          ++h->hp.n[9];
+        }
       }
       if (timed) HIP_TRY(hipEventRecord(e1, cs));
       // results written in place (no exchange): this verify follows the previous one when that ran on the other
       // stream (the same rows of the result buffer)
       if (two && !multi && s.last_vsi >= 0 && s.last_vsi != bsi)
-        HIP_TRY(hipStreamWaitEvent(vs, s.ev_q[s.last_vq][s.last_vsi], 0));
+        HIP_TRY(wait_ev(vs, s.ev_q[s.last_vq][s.last_vsi]));
       if (s.rows() > 0 && !h->ab_no_verify) {
         rr::SkArgs v = sk_base(h, s, qb, bb);
         VerifyBlock me;
@@ -1470,8 +1509,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       }
       if (!multi) {   // results read back on the exchange stream (rr_search_async) come after these
         HIP_TRY(hipEventRecord(s.ev_cdone, s.stream));
-        HIP_TRY(hipStreamWaitEvent(s.xstream, s.ev_cdone, 0));
-        HIP_TRY(hipStreamWaitEvent(s.xstream2, s.ev_cdone, 0));
+        HIP_TRY(wait_ev(s.xstream, s.ev_cdone));
+        HIP_TRY(wait_ev(s.xstream2, s.ev_cdone));
       }
     } else {
       // k > RR_FUSED_KMAX: all keys of this shard, their top-k sorted (rr_topk.hip). The exchange
@@ -1535,7 +1574,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
     float* osc = s.out_scores + (size_t)q0 * k;
     int64_t* oix = s.out_idx + (size_t)q0 * k;
     if (s.rcopy_pending) {   // an asynchronous search's result copy (on an exchange lane) still reads these rows
-      HIP_TRY(hipStreamWaitEvent(s.stream, s.ev_rcopy, 0));
+      HIP_TRY(wait_ev(s.stream, s.ev_rcopy));
       s.rcopy_pending = false;
     }
     if (wk) {   // the world lists' union -> top-k (radix select), and the largest of their flag words
@@ -1562,8 +1601,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
     }
     // later pipelined exchanges write the results after this one
     HIP_TRY(hipEventRecord(s.ev_cdone, s.stream));
-    HIP_TRY(hipStreamWaitEvent(s.xstream, s.ev_cdone, 0));
-    HIP_TRY(hipStreamWaitEvent(s.xstream2, s.ev_cdone, 0));
+    HIP_TRY(wait_ev(s.xstream, s.ev_cdone));
+    HIP_TRY(wait_ev(s.xstream2, s.ev_cdone));
     s.last_x = -1;
   }
   return RR_OK;
@@ -1708,8 +1747,10 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
 void rr_destroy(rr_handle* h) {
   if (!h) return;
   if (h->host_prof) {
-    static const char* what[4] = {"rr_search_staged", "exchange enqueue", "ncclAllGather call", "screen+verify launches"};
-    for (int i = 0; i < 4; ++i)
+    static const char* what[10] = {"rr_search_staged", "exchange enqueue", "ncclAllGather call", "screen+verify launches",
+                                   "x: ev_keys record", "x: lane waits", "x: merge launch", "x: ev_xdone record",
+                                   "c: prep launch", "c: screen launch"};
+    for (int i = 0; i < 10; ++i)
       if (h->hp.n[i])
         fprintf(stderr, "[rr host prof] %s: %.2f us x %lld\n", what[i], h->hp.ns[i] / 1e3 / h->hp.n[i],
                 (long long)h->hp.n[i]);

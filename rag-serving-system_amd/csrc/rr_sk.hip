@@ -45,11 +45,12 @@
 //      (KT >= k + 3) by u per workgroup. At half the matrix-core work and a tenth of the vector work of
 //      DT 3 it streams at the LDS-DMA rate, also while the GPU's power management throttles the core
 //      clock during its first ~40 launches out of idle (profiles/r02/kbench_transient_screen.log).
-//   2. MODE 1, DT 3, one workgroup per query slot: merges the screen's lists into the global top-KT by u,
-//      gathers those KT rows and scores them with EXACTLY the DT 3 arithmetic (same K split, MFMA order
-//      and wave-reduction order: bit-identical to a full DT 3 pass), keeps the exact top-k. Complete
-//      when the exact k-th score is strictly above the KT-th upper bound (every other doc's exact score
-//      is at most its u, which is at most that bound) — or when the shard has fewer than KT docs.
+//   2. MODE 1, DT 3, one workgroup per query slot: merges the screen's lists into the global top-32 by u (one
+//      MFMA tile of rows; KT until r5), gathers those rows and scores them with EXACTLY the DT 3 arithmetic (same K
+//      split, MFMA order and wave-reduction order: bit-identical to a full DT 3 pass), keeps the exact top-k.
+//      Complete when the exact k-th score is strictly above the 32nd upper bound (every other doc's exact score
+//      is at most its u, which is at most that bound) — or when the shard has fewer than 32 docs. (Else the wide
+//      phase, or in repair mode the repair pass; bf16 storage: DT 9 screen, DT 1 verify, the same steps.)
 //   3. Otherwise (rare: > KT - k docs inside the bound's window) the verify raises the block's flag word
 //      (a monotonic sequence number; exchanged with the candidates when shards exchange) and the host
 //      re-runs that search with the exact one-pass kernel when it collects the results (rr_api.cpp).
@@ -274,28 +275,32 @@ struct QFrag<9, NS> { i32x4 c1[NS][4]; };   // the bf16 storage's int8 screen: o
 // LDS byte offset (within a slot) of 16-byte column position cp of tile row r (swizzled image)
 __device__ __forceinline__ int slab_off(int r, int cp) { return (r >> 3) * 1024 + (r & 7) * 128 + ((cp ^ (r & 7)) << 4); }
 
-// Verify stage (MODE 1): the screen's [QS][nlists][KT] upper-bound lists -> this query's global top-KT by u
-// in akeys[] (LDS, descending), by rank selection instead of KT rounds of wave-wide maxima:
+// Verify stage (MODE 1): the screen's [QS][nlists][KT] upper-bound lists -> this query's global top-NC by u
+// in akeys[] (LDS, descending; NC = 32 >= KT: one whole MFMA tile of rows), by rank selection instead of NC rounds of
+// wave-wide maxima:
 //   1. thread l holds list l (sorted; lists beyond kThreads folded into thread l % kThreads's list);
-//   2. H = the KT-th largest list head (its rank among the heads is KT - 1; 0 when fewer than KT heads are
-//      non-empty). Every key of the global top-KT is >= H: KT distinct heads are >= H, so a key below H has
-//      rank >= KT. Only the <= KT lists whose head is >= H can hold such keys: <= KT x KT candidates;
-//   3. the non-empty keys >= H are appended to an LDS array, and the candidate of rank r < KT is akeys[r].
+//   2. H = the NC-th largest list head (its rank among the heads is NC - 1; 0 when fewer than NC heads are
+//      non-empty). Every key of the global top-NC is >= H: NC distinct heads are >= H, so a key below H has
+//      rank >= NC. Only the <= NC lists whose head is >= H can hold such keys: <= NC x KT candidates;
+//   3. the non-empty keys >= H are appended to an LDS array, and the candidate of rank r < NC is akeys[r].
 // Keys are unique (distinct row indices), so ranks are distinct. Each list of the screen carries its workgroup's
 // floor after its KT keys (see KL in sk_score_kernel): their maximum goes to *floor_out (LDS; valid after the return).
-// Lists folded into another thread's list drop keys only below that list's last entry, which stays in the global
-// top-KT's bound (every key left out is at most the KT-th candidate). Scratch: LDS free in MODE 1 (the slab ring):
-// [kThreads] heads, [KT * KT] candidates, H, count, floor maximum.
-template <int KT>
+// Keys a folded list loses (below the thread's list's last entry) join the floor maximum, so every key left out of
+// akeys is at most max(akeys[NC - 1], *floor_out). Scratch: LDS free in MODE 1 (the slab ring): [kThreads] heads,
+// [NC * KT] candidates, H, count, floor maximum.
+// (r5: NC = 32 instead of KT — the first tile rescored 16 rows of its 32 — so the int8 screen's looser bound proves
+// most slots without the wide phase.)
+template <int KT, int NC = 32>
 __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict__ in, int nlists, int qslots, int q,
                                                       uint64_t* scratch, uint64_t* akeys, uint64_t* floor_out,
                                                       uint64_t* tail_out) {
   const int tid = threadIdx.x;
   uint64_t* heads = scratch;
   uint64_t* cand = scratch + kThreads;
-  uint64_t* hs = cand + KT * KT;
+  uint64_t* hs = cand + NC * KT;
   int* cnt = (int*)(hs + 1);
   constexpr int LS = KT + 1;   // list stride: KT keys + the workgroup's floor
+  static_assert(NC >= KT && NC <= 32, "the first verify tile rescores NC <= 32 rows");
   TopK<KT> tk;
   uint64_t fl = 0, tl = 0;     // floors; and every list's own bound, max(its KT-th key, its floor) (wide verify)
   if (tid < nlists) {
@@ -313,7 +318,11 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
     tl = umax64(tl, umax64(src[KT], src[KT - 1]));
     for (int i = 0; i < KT; ++i) {
       const uint64_t key = src[i];
-      if (key <= tk.last()) break;
+      if (key <= tk.last()) {   // (this and the rest of the list are left out: the floor covers them)
+        fl = umax64(fl, key);
+        break;
+      }
+      fl = umax64(fl, tk.last());   // the entry the insert pushes out
       tk.insert(key);
     }
   }
@@ -361,9 +370,9 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
     if (hh < nl && me != 0) rank = half ? count_above(me, g8, nlp / 2) : count_above(me, 0, g8);
     if (half == 1) part[hh] = rank;
     __syncthreads();
-    if (!half && hh < nl && me != 0 && rank + part[hh] == KT - 1) hs[0] = me;
+    if (!half && hh < nl && me != 0 && rank + part[hh] == NC - 1) hs[0] = me;
   } else if (tid < nl && tk.v[0] != 0) {
-    if (count_above(tk.v[0], 0, nlp / 2) == KT - 1) hs[0] = tk.v[0];
+    if (count_above(tk.v[0], 0, nlp / 2) == NC - 1) hs[0] = tk.v[0];
   }
   __syncthreads();
   if (tid == 0) {
@@ -389,12 +398,12 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
   __syncthreads();
   SK_PROBE2(3);   // candidates appended
   const int m = cnt[0];
-  if (tid < KT && tid >= m) akeys[tid] = 0;   // fewer than KT keys in all: empty tail
+  if (tid < NC && tid >= m) akeys[tid] = 0;   // fewer than NC keys in all: empty tail
   for (int c = tid; c < m; c += kThreads) {
     const uint64_t me = cand[c];
     int rank = 0;
     for (int j = 0; j < m; ++j) rank += cand[j] > me ? 1 : 0;
-    if (rank < KT) akeys[rank] = me;
+    if (rank < NC) akeys[rank] = me;
   }
   __syncthreads();
 }
@@ -479,8 +488,8 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // place in this workgroup's 32-column lane mapping and query scalars at vql)
   const int vql = vq & 31;
   uint64_t* vW = (uint64_t*)(qexp + QS);
-  uint64_t* akeys = vW + kWaves * KT;
-  int* grow = (int*)(akeys + KT);
+  uint64_t* akeys = vW + kWaves * KT;   // [32]: the first tile's candidates (merge_lists_for_query NC)
+  int* grow = (int*)(akeys + 32);
   float* gnorm = (float*)(grow + 32);
   int* gvalid = (int*)(gnorm + 32);
   uint64_t* xk = (uint64_t*)(gvalid + 32);
@@ -915,14 +924,14 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // ---- MODE 1: this query's candidates (the queries' fragments and scalars above are already built, so
   // their loads overlapped the list loads), then their rows straight into registers ---------------------------
   if constexpr (MODE == 1) {
-    static_assert((size_t)(kThreads + KT * KT + 4 + 2 * kWaves) * 8 + kThreads / 2 * 4 <= kWideListOff,
+    static_assert((size_t)(kThreads + 32 * KT + 4 + 2 * kWaves) * 8 + kThreads / 2 * 4 <= kWideListOff,
                   "verify merge scratch in the slab ring");
     SK_PROBE(6);
     merge_lists_for_query<KT>(a.vin, a.nlists, QS, vq, (uint64_t*)smem, akeys, vfloor, vtail);
     SK_PROBE(7);
     if (tid < 32) {
       const uint64_t k0 = akeys[0];
-      const uint64_t key = tid < KT ? akeys[tid] : 0;
+      const uint64_t key = akeys[tid];
       const int64_t first = k0 ? (int64_t)(0xFFFFFFFFu - (uint32_t)k0) - idx_base : 0;
       const int64_t row = key ? (int64_t)(0xFFFFFFFFu - (uint32_t)key) - idx_base : first;
       grow[tid] = (int)row;
@@ -1674,9 +1683,11 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     };
     lane_merge();
     if (leader) {
-      // Every key not rescored is at most the KT-th candidate's bound or a workgroup's floor (0, 0: fewer than KT
-      // docs here and nothing dropped).
-      const uint64_t ukt = umax64(akeys[KT - 1], *vfloor);
+      // Every key not rescored is at most the 32nd candidate's bound, or — left out of its list — at most that list's
+      // KT-th key or its workgroup's floor, both within vtail (0, 0: fewer than 32 docs here and nothing dropped). With
+      // 32 candidates from lists of KT < 32 the 32nd can lie below a list's KT-th (a cluster filling one list): vtail
+      // must be checked, where the KT-th candidate bounded every list's KT-th by itself.
+      const uint64_t ukt = umax64(akeys[31], *vtail);
       const uint64_t ek = xk[a.k_out - 1];         // the exact k-th key
       const bool complete = ukt == 0 || (ek != 0 && (uint32_t)(ek >> 32) > (uint32_t)(ukt >> 32));
       // Not proven: the wide phase can still prove it when the k-th largest bound of all lies above the largest

@@ -5,8 +5,8 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DRR_SK_PROBE -DRR_SK_NO_DISPATCH -I include \
 //         -I rag-serving-system_amd/csrc tools/probe_screen.hip -o tools/probe_screen
-//   tools/probe_screen [rows=125000] [grid=256] [ct8=2] [prep=0] [guided=1] [streams_test=0]
-// prep = 1: the launch preps its int8 query pieces in 32 joiner workgroups (SkArgs::prep; grid includes them).
+//   tools/probe_screen [rows=125000] [grid=256] [ct8=2] [unused=0] [guided=1] [streams_test=0]
+// (argument 4 was the rejected joiner prep, removed from the product kernel in r5; kept as a placeholder)
 // Phases per workgroup: start -> (1) prologue + query fragments -> (2) first tile -> (3) second tile -> (4) the rest of
 // its tiles -> (5) list merge and write. Printed: min / median / max over the workgroups, and the launch span.
 #include "../rag-serving-system_amd/csrc/rr_kernels.hip"
@@ -89,13 +89,8 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  a.prep = prep;
   a.no_guided = !guided;
-  a.psync = (uint64_t*)(ctr + 64);
-  a.sflag = flag;
-  a.sseq = 1;
   for (int rep = 0; rep < 30; ++rep) {
-    a.pbase = (uint64_t)rep * 32;
     CK(hipEventRecord(e0, s));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads + 64), lds, s, a);
     CK(hipGetLastError());
@@ -118,8 +113,6 @@ int main(int argc, char** argv) {
     SkArgs b2 = a;
     b2.ctr = ctr2;
     b2.out = cand2;
-    b2.prep = 0;
-    a.prep = 0;
     for (int round = 0; round < 2; ++round)
       for (int two = 0; two < 2; ++two) {
         CK(hipDeviceSynchronize());

@@ -1,6 +1,7 @@
 // verify_probe.hip — per-phase timestamps of the screened search's verify kernel (development probe).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DRR_SK_PROBE -I include -I rag-serving-system_amd/csrc \
-//         tools/verify_probe.hip -o tools/verify_probe && tools/verify_probe [n_docs]
+//         tools/verify_probe.hip -o tools/verify_probe && tools/verify_probe [n_docs] [int8=1]
+// int8 = 1: the verify of an int8 screen (DT 8 over the int8 copy, wide phase on) — the headline path; 0: the DT 6 screen.
 #include "../rag-serving-system_amd/csrc/rr_kernels.hip"
 #include "../rag-serving-system_amd/csrc/rr_sk.hip"
 
@@ -22,7 +23,8 @@ using namespace rr;
 
 int main(int argc, char** argv) {
   const int64_t n = argc > 1 ? atoll(argv[1]) : 1000000;
-  const int d = 1024, b = 32, k = 5, kt = 16;
+  const int i8 = argc > 2 ? atoi(argv[2]) : 1;
+  const int d = 1024, b = 32, k = 5;
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   hipStream_t s;
@@ -45,21 +47,48 @@ int main(int argc, char** argv) {
   CK(launch_permute_f32(tmp, c32, n, d, 0, s));
   CK(launch_row_norms(0, c32, n, d, norms, s));
   CK(launch_synth(1, 99, 0, b, d, q, s));
+  const int64_t r2 = (n + 1) / 2 * 2;
+  int8_t *c8, *q8;
+  float *sx, *e8, *q8s;
+  uint32_t* ctr;
+  int* wcount;
+  CK(hipMalloc(&c8, (size_t)r2 * d));
+  CK(hipMalloc(&sx, (size_t)r2 * 4));
+  CK(hipMalloc(&e8, (size_t)r2 * 4));
+  CK(hipMalloc(&q8, (size_t)2 * 32 * d));
+  CK(hipMalloc(&q8s, (size_t)4 * 64 * 4));
+  CK(hipMalloc(&ctr, 512));
+  CK(hipMalloc(&wcount, 64));
+  CK(hipMemset(ctr, 0, 512));
+  CK(hipMemset(wcount, 0, 64));
+  CK(hipMemset(c8 + (size_t)n * d, 0, (size_t)(r2 - n) * d));
+  CK(hipMemset(sx + n, 0, (size_t)(r2 - n) * 4));
+  CK(hipMemset(e8 + n, 0, (size_t)(r2 - n) * 4));
+  CK(launch_f32_to_i8(tmp, n, d, c8, sx, e8, s));
+  CK(launch_q8_prep(q, b, d, q8, q8s, s));
   CK(hipStreamSynchronize(s));
   SkArgs a{};
   a.corpus = (const char*)c32; a.norms = norms; a.queries = q; a.n = n; a.d = d; a.b = b; a.out = cand;
   a.eps_a = 6e-4f; a.eps_b = 4e-8f; a.sqrt_d = 32.0f;
   SkArgs v = a;
   v.vin = cand; v.nlists = cus; v.k_out = k; v.out_scores = osc; v.out_idx = oix; v.flag = flag; v.count = count;
+  v.wide_verify = 1;
+  v.wide_count = wcount;
+  if (i8) {
+    a.corpus = (const char*)c8; a.n = (n + 1) / 2; a.rows8 = n; a.q8 = q8; a.q8s = q8s; a.sx8 = sx; a.e8 = e8; a.ct8 = 2;
+    a.eps_a = 6.0e-5f; a.eps_b = 4.0e-8f; a.sqrt_d = 32.0f * (1.0f + 0x1p-20f); a.ctr = ctr; a.dyn = 1;
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   std::vector<unsigned long long> h((size_t)32 * 8);
   for (int rep = 0; rep < 6; ++rep) {
     v.seq = rep + 1;
-    CK(launch_sk_args(KDT_SCREEN, 1, kt, 0, cus, 32, a, s));
+    // (the product's instantiations, launched directly: this probe builds without the dispatch table)
+    if (i8) CK((sk::launch_t<8, 2, 16, true, 2, 1, 0, 1, 0>(cus, a, s)));
+    else CK((sk::launch_t<6, 4, 16, true, 2, 1, 0, 0, 0>(cus, a, s)));
     CK(hipEventRecord(e0, s));
-    CK(launch_sk_args(KDT_F32_X3, 1, kt, 1, 32, 32, v, s));
+    CK((sk::launch_t<3, 4, 16, true, 2, 1, 1, 0, 0>(32, v, s)));
     CK(hipEventRecord(e1, s));
     CK(hipStreamSynchronize(s));
     float ms = 0;
@@ -67,10 +96,13 @@ int main(int argc, char** argv) {
     CK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(rr::sk::probe), h.size() * 8));
     unsigned long long t0 = ~0ull;
     for (int g = 0; g < 32; ++g) t0 = std::min(t0, h[g * 8]);
-    printf("{\"rep\": %d, \"verify_event_us\": %.1f", rep, ms * 1e3);
-    const int order[] = {0, 6, 7, 3, 1, 2, 4};
-    const char* nm[] = {"start", "frags_norms", "merged", "rows_known", "loop_start", "tile_done", "loop_end"};
-    for (int i = 0; i < 7; ++i) {
+    int wc = 0;
+    CK(hipMemcpy(&wc, wcount, 4, hipMemcpyDeviceToHost));
+    printf("{\"rows\": %lld, \"int8\": %d, \"rep\": %d, \"verify_event_us\": %.1f, \"wide_slots_total\": %d", (long long)n,
+           i8, rep, ms * 1e3, wc);
+    const int order[] = {0, 6, 7, 3, 1, 2, 4, 5};
+    const char* nm[] = {"start", "frags_norms", "merged", "rows_known", "loop_start", "tile_done", "loop_end", "end"};
+    for (int i = 0; i < 8; ++i) {
       std::vector<double> x;
       for (int g = 0; g < 32; ++g)
         if (order[i] != 5 || g < 4) x.push_back((h[g * 8 + order[i]] - t0) / 100.0);
