@@ -410,7 +410,7 @@ int dmalloc(T** p, size_t bytes) {
 
 int free_shard(Shard& s) {
   hipSetDevice(s.dev);
-  void* ptrs[] = {s.corpus, s.scr16, s.scr8, s.sx8, s.e8, s.q8[0], s.q8[1], s.q8s[0], s.q8s[1], s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.wcount, s.ctr, s.shard_keys, s.gathered, s.out_base,
+  void* ptrs[] = {s.corpus, s.scr16, s.scr8, s.sx8, s.e8, s.q8[0], s.q8[1], s.q8s[0], s.q8s[1], s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.ctr, s.shard_keys, s.gathered, s.out_base,
                   s.full_keys, s.sort_temp, s.wcand, s.wfloor, s.wsel, s.rcmax[0], s.rcmax[1], s.rbits[0], s.rbits[1],
                   s.rlist[0], s.rlist[1], s.rcnt[0], s.rcnt[1]};
   for (void* p : ptrs)
@@ -702,7 +702,7 @@ int drop_work_buffers(rr_handle* h) {
     s.last_x = -1;
     s.q_rd[0][0] = s.q_rd[0][1] = s.q_rd[1][0] = s.q_rd[1][1] = false;
     s.last_vsi = -1;
-    void** ptrs[] = {(void**)&s.qbuf[0], (void**)&s.qbuf[1], (void**)&s.cand, (void**)&s.scount, (void**)&s.wcount, (void**)&s.ctr, (void**)&s.shard_keys, (void**)&s.gathered,
+    void** ptrs[] = {(void**)&s.qbuf[0], (void**)&s.qbuf[1], (void**)&s.cand, (void**)&s.scount, (void**)&s.ctr, (void**)&s.shard_keys, (void**)&s.gathered,
                      (void**)&s.out_base, (void**)&s.full_keys, &s.sort_temp,
                      (void**)&s.wcand, (void**)&s.wfloor, (void**)&s.wsel, (void**)&s.rcmax[0], (void**)&s.rcmax[1],
                      (void**)&s.rbits[0], (void**)&s.rbits[1], (void**)&s.rlist[0], (void**)&s.rlist[1],
@@ -716,6 +716,7 @@ int drop_work_buffers(rr_handle* h) {
         if (*p) HIP_TRY(hipFree(*p));
         *p = nullptr;
       }
+    s.wcount = nullptr;   // (inside scount's allocation, freed above)
     s.q_cap = s.k_cap = s.cand_grid = 0;
     s.rcap = 0;
     s.full_cap = s.sort_temp_bytes = 0;
@@ -807,12 +808,12 @@ int ensure_buffers(rr_handle* h, int b, int k) {
     if (!s.cand) {
       s.cand_grid = s.cus;
       if (int rc = dmalloc(&s.cand, 2 * cand_half(s) * 8)) return rc;
-      if (int rc = dmalloc(&s.scount, 2 * sizeof(int))) return rc;
-      HIP_TRY(hipMemset(s.scount, 0, 2 * sizeof(int)));
-      if (int rc = dmalloc(&s.wcount, 2 * sizeof(int))) return rc;
-      HIP_TRY(hipMemset(s.wcount, 0, 2 * sizeof(int)));
-      if (!s.pin_scount) HIP_TRY(hipHostMalloc((void**)&s.pin_scount, 2 * sizeof(int), hipHostMallocDefault));
-      ((volatile int*)s.pin_scount)[0] = ((volatile int*)s.pin_scount)[1] = 0;
+      // scount [2] and wcount [2] in one allocation: rr_screen_counts reads all four in one copy
+      if (int rc = dmalloc(&s.scount, 4 * sizeof(int))) return rc;
+      HIP_TRY(hipMemset(s.scount, 0, 4 * sizeof(int)));
+      s.wcount = s.scount + 2;
+      if (!s.pin_scount) HIP_TRY(hipHostMalloc((void**)&s.pin_scount, 4 * sizeof(int), hipHostMallocDefault));
+      for (int i = 0; i < 4; ++i) ((volatile int*)s.pin_scount)[i] = 0;
       if (int rc = dmalloc(&s.ctr, 4 * kCtrStride * sizeof(uint32_t))) return rc;
       HIP_TRY(hipMemset(s.ctr, 0, 4 * kCtrStride * sizeof(uint32_t)));
     }
@@ -2149,7 +2150,7 @@ int rr_synchronize(rr_handle* h) {
   if (!h) return fail(RR_E_INVALID, "null handle");
   if (h->failed) return failed_handle();
   if (int rc = sync_streams(h)) return rc;
-  if (!h->last_screened) return RR_OK;
+  if (!h->last_screened || h->last_settled) return RR_OK;   // (settled: nothing to read)
   uint64_t flag = 0;
   if (int rc = read_flag(h, &flag)) return rc;
   bool rerun = false;
@@ -2325,14 +2326,10 @@ int rr_screen_counts(rr_handle* h, int64_t* blocks, int64_t* flagged, int64_t* r
   for (Shard& s : h->shards) {
     if (!s.scount) continue;
     HIP_TRY(hipSetDevice(s.dev));
-    int wv = 0;
-    HIP_TRY(hipMemcpyAsync(s.pin_scount, s.scount, sizeof(int), hipMemcpyDeviceToHost, s.stream));
-    if (int rc = wait_stream(h, s, s.stream, "the flagged-block count")) return rc;
-    fb += *(volatile int*)s.pin_scount;
-    HIP_TRY(hipMemcpyAsync(s.pin_scount, s.wcount, sizeof(int), hipMemcpyDeviceToHost, s.stream));
-    if (int rc = wait_stream(h, s, s.stream, "the wide-verify count")) return rc;
-    wv = *(volatile int*)s.pin_scount;
-    ws += wv;
+    HIP_TRY(hipMemcpyAsync(s.pin_scount, s.scount, 4 * sizeof(int), hipMemcpyDeviceToHost, s.stream));
+    if (int rc = wait_stream(h, s, s.stream, "the screened-search counts")) return rc;
+    fb += ((volatile int*)s.pin_scount)[0];
+    ws += ((volatile int*)s.pin_scount)[2];   // (wcount = scount + 2)
   }
   if (blocks) *blocks = h->screen_blocks * (int64_t)h->shards.size();
   if (flagged) *flagged = fb;
