@@ -11,7 +11,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <climits>
 #include <cmath>
 #include <cstdarg>
@@ -100,6 +103,11 @@ struct Shard {
   hipStream_t cstream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_stage = nullptr;
   hipEvent_t ev_q[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  // with an exchange step the block's keys-ready event (ev_keys) marks the same point of its stream: ev_q is then not
+  // recorded, evq_alias points to that event instead (one marker packet fewer in the compute stream per block;
+  // ev_keys[x] is re-recorded kXSlots blocks later, on the same stream — a later point, which only orders more)
+  hipEvent_t evq_alias[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  hipEvent_t evq(int t, int i) const { return evq_alias[t][i] ? evq_alias[t][i] : ev_q[t][i]; }
   bool q_rd[2][2] = {{false, false}, {false, false}};   // ev_q[t][i] recorded, no writer of buffer t waited on it yet
   bool fork_pending = false;   // ev_fork was recorded since cstream2 last waited on it
   bool c2_busy = false;        // cstream2 holds work `stream` has not joined
@@ -198,6 +206,10 @@ struct AsyncSlot {
 };
 constexpr int kAsyncSlots = 4;
 
+namespace {
+struct XWorker;
+}  // namespace
+
 struct rr_handle {
   int dtype = RR_DTYPE_F32;
   int metric = RR_METRIC_COSINE;
@@ -214,6 +226,7 @@ struct rr_handle {
   bool timing = false;
   int kernel = RR_KERNEL_AUTO;   // rr_set_kernel
   int parity = 0;                // the next search block's parity (candidate half, compute stream)
+  XWorker* xw = nullptr;         // multi-process mode: the exchange issue thread (XWorker below; null: inline)
   int xslot = 0;                 // the next pipelined exchange's buffer set (Shard::px_keys)
   double t_ms = 0.0;
   int64_t t_count = 0;
@@ -241,6 +254,7 @@ struct rr_handle {
   int verify_cus = 32;           // (kVerifyCUs) CUs an overlapping screen leaves to the other stream's verify (A/B: RR_VERIFY_CUS)
   int xslots = kXSlots;         // pipelined-exchange buffer sets in use (A/B: RR_X_SLOTS, 2..kXSlots)
   int x_delay_us = 0;           // A/B: RR_X_EXCHANGE_DELAY_US, a stand-in for a slower exchange
+  int x_host_wait_us = 500;     // exchange issue thread: host wait for a px slot's previous exchange (RR_X_HOST_WAIT_US)
   int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy); bf16: the int8 one
   int screen_i8 = 1;            // ... and an int8 copy, screened first (rr_screen_int8; RR_SCREEN_I8=0 at creation: off)
   int ct8 = 0;                  // the int8 screen's tiles per chunk (0: by shard size; A/B: RR_SCREEN_CT8)
@@ -345,7 +359,10 @@ hipError_t wait_ev(hipStream_t st, hipEvent_t ev) {
   return hipStreamWaitEvent(st, ev, 0);
 }
 
+int xw_drain(rr_handle* h);   // (the exchange issue thread: every posted exchange issued, below)
 int wait_stream(rr_handle* h, const Shard& s, hipStream_t st, const char* what = "device work", int scale = 1) {
+  if (h->xw)   // every host wait first sees every posted exchange issued
+    if (int rc = xw_drain(h)) return rc;
   if (!deadline_on(h)) {
     HIP_TRY(hipStreamSynchronize(st));
     return RR_OK;
@@ -354,6 +371,8 @@ int wait_stream(rr_handle* h, const Shard& s, hipStream_t st, const char* what =
                     scale);
 }
 int wait_event(rr_handle* h, const Shard& s, hipEvent_t ev, const char* what = "device event") {
+  if (h->xw)
+    if (int rc = xw_drain(h)) return rc;
   if (!deadline_on(h)) {
     HIP_TRY(hipEventSynchronize(ev));
     return RR_OK;
@@ -558,6 +577,7 @@ int finish_corpus(rr_handle* h, Shard& s, bool* screen_ok) {
 // `scale` multiplies the deadline (ranks reach a load's agreement at different times). Without rr_init_dist: v as is.
 int agree_min(rr_handle* h, int* v, int n, const char* what, int scale) {
   if (!h->dist) return RR_OK;
+  if (int rc = xw_drain(h)) return rc;   // (its collectives and this one share the communicator)
   Shard& s = h->shards[0];
   HIP_TRY(hipSetDevice(s.dev));
   int* dv = nullptr;
@@ -1064,7 +1084,7 @@ int stage_queries(rr_handle* h, int t, const void* src, size_t bytes, int src_de
     const int x = block_si(h, s, h->parity);
     const hipStream_t xs = stream_of(s, x);
     if (two) {
-      if (s.q_rd[t][x ^ 1]) HIP_TRY(wait_ev(xs, s.ev_q[t][x ^ 1]));   // its last readers there
+      if (s.q_rd[t][x ^ 1]) HIP_TRY(wait_ev(xs, s.evq(t, x ^ 1)));   // its last readers there
       s.q_rd[t][x ^ 1] = false;
       if (x == 1) {   // after other kinds of search on `stream` (they read query buffers too)
         if (s.fork_pending) HIP_TRY(wait_ev(xs, s.ev_fork));
@@ -1108,6 +1128,127 @@ int local_gather(rr_handle* h, size_t per) {
     HIP_TRY(hipEventRecord(dst.copies_done, dst.stream));
   }
   return RR_OK;
+}
+
+// Exchange issue thread (multi-process mode, r5). On the 8-GPU shard the caller's thread set the step: ~40 us of host
+// enqueue per block against ~34 us of device work (tools/host_calls.py), ~18 us of it the exchange — the all-gather
+// call, the merge launch, two event records and two waits on pending events, each ~3.6 us (tools/api_cost.hip). The
+// caller now records the block's keys-ready event and posts the exchange; this thread issues it (issue_exchange, in
+// post order: the communicators' collectives keep one order on every rank). The caller never runs ahead of it by more
+// than kXLag blocks (px_keys slot reuse, enqueue_block), and drains it (every posted exchange issued) before any host
+// wait, any collective of its own and any read of the exchange state (last_x, rcopy): a drained worker is idle, so
+// the two threads never touch that state or a communicator at the same time. (r4 measured an issue thread 2-6 %
+// slower while the device set the step; RR_X_THREAD=0: inline.)
+struct XJob {
+  int x, q0, bb, k, kt, slots;
+};
+struct XWorker {
+  static constexpr int kRing = 16;
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::atomic<int64_t> posted{0}, done{0};
+  std::atomic<bool> stop{false}, sleeping{false};
+  std::atomic<int> err{0};
+  std::string errmsg;   // written by the worker before err (release), read by the caller after it (acquire)
+  XJob ring[kRing];
+};
+constexpr int kXLag = 2;   // posted exchanges not yet issued, at most, when a block is enqueued (kXSlots - 2)
+
+int issue_exchange(rr_handle* h, int x, int q0, int bb, int k, int kt, int slots, int64_t* ns_gather);
+
+void xw_main(rr_handle* h, XWorker* w) {
+  int64_t idle_since = now_ns();
+  for (;;) {
+    const int64_t d = w->done.load(std::memory_order_relaxed);
+    if (d < w->posted.load(std::memory_order_acquire)) {
+      const XJob j = w->ring[d % XWorker::kRing];
+      if (w->err.load(std::memory_order_relaxed) == 0) {
+        int64_t ng = 0;
+        const int rc = issue_exchange(h, j.x, j.q0, j.bb, j.k, j.kt, j.slots, h->host_prof ? &ng : nullptr);
+        if (ng) {
+          h->hp.ns[2] += ng;
+          ++h->hp.n[2];
+        }
+        if (rc) {
+          w->errmsg = g_err;   // (this thread's message)
+          w->err.store(rc, std::memory_order_release);
+        }
+      }
+      w->done.store(d + 1, std::memory_order_release);
+      idle_since = now_ns();
+      continue;
+    }
+    if (w->stop.load(std::memory_order_acquire)) return;
+    if (now_ns() - idle_since < 200000) {   // spin 200 us after the last job (the next block's comes within ~40 us)
+      std::this_thread::yield();
+      continue;
+    }
+    std::unique_lock<std::mutex> lk(w->mu);
+    w->sleeping.store(true, std::memory_order_seq_cst);
+    if (w->done.load() == w->posted.load() && !w->stop.load())
+      w->cv.wait_for(lk, std::chrono::milliseconds(5));
+    w->sleeping.store(false, std::memory_order_relaxed);
+    idle_since = now_ns();
+  }
+}
+
+// the worker's first error, reported on the caller's thread
+int xw_check(rr_handle* h) {
+  XWorker* w = h->xw;
+  if (const int e = w->err.load(std::memory_order_acquire)) return fail(e, "exchange issue thread: %s", w->errmsg.c_str());
+  return RR_OK;
+}
+// wait until at most `lag` posted exchanges are not yet issued. Bounded by 30 s or the handle's deadline if longer —
+// not by a short deadline: that bounds device work, and the worker only enqueues (its wake-up alone can take
+// milliseconds on a loaded host); an RCCL enqueue that blocks on a dead peer is what the bound is for.
+int xw_wait(rr_handle* h, int64_t lag) {
+  XWorker* w = h->xw;
+  if (!w) return RR_OK;
+  const auto t0 = std::chrono::steady_clock::now();
+  const int64_t limit_ms = std::max<int64_t>(30000, h->timeout_ms);
+  while (w->posted.load(std::memory_order_relaxed) - w->done.load(std::memory_order_acquire) > lag) {
+    std::this_thread::yield();
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(limit_ms)) {
+      h->failed = true;
+      return fail(RR_E_TIMEOUT, "rank %d of %d: the exchange issue thread did not issue its posted exchanges within "
+                  "%lld ms (an all-gather enqueue blocked: a peer rank that never joined?)", h->shard_base, h->world,
+                  (long long)limit_ms);
+    }
+  }
+  return xw_check(h);
+}
+int xw_drain(rr_handle* h) { return xw_wait(h, 0); }
+int xw_post(rr_handle* h, const XJob& j) {
+  XWorker* w = h->xw;
+  if (int rc = xw_wait(h, XWorker::kRing - 1)) return rc;
+  const int64_t p = w->posted.load(std::memory_order_relaxed);
+  w->ring[p % XWorker::kRing] = j;
+  w->posted.store(p + 1, std::memory_order_seq_cst);
+  if (w->sleeping.load(std::memory_order_seq_cst)) {
+    std::lock_guard<std::mutex> lk(w->mu);
+    w->cv.notify_one();
+  }
+  return RR_OK;
+}
+void xw_start(rr_handle* h) {
+  if (h->xw) return;
+  if (const char* e = getenv("RR_X_THREAD"))
+    if (atoi(e) == 0) return;
+  h->xw = new XWorker();
+  h->xw->th = std::thread(xw_main, h, h->xw);
+}
+void xw_stop(rr_handle* h) {
+  XWorker* w = h->xw;
+  if (!w) return;
+  {
+    std::lock_guard<std::mutex> lk(w->mu);
+    w->stop.store(true, std::memory_order_release);
+    w->cv.notify_one();
+  }
+  w->th.join();   // (it issues every posted exchange first)
+  delete w;
+  h->xw = nullptr;
 }
 
 // Pipelined exchange (k <= RR_FUSED_KMAX, world > 1) of the search block just scored into px_keys[x]:
@@ -1167,12 +1308,14 @@ int enqueue_exchange_px(rr_handle* h, int p, int x, int q0, int bb, int k, int k
   const int64_t tk = h->host_prof ? now_ns() : 0;
   for (Shard& s : h->shards) {   // px_keys[x] is written on the block's compute stream (a screened block: its parity's)
     HIP_TRY(hipSetDevice(s.dev));
-    HIP_TRY(hipEventRecord(s.ev_keys[x], scr ? cstream(h, s, p) : s.stream));
+    // (a screened block with two compute streams recorded it after its verify already: enqueue_block_body)
+    if (!(scr && two_streams(h, s))) HIP_TRY(hipEventRecord(s.ev_keys[x], scr ? cstream(h, s, p) : s.stream));
   }
   if (h->host_prof) {
     h->hp.ns[4] += now_ns() - tk;
     ++h->hp.n[4];
   }
+  if (h->xw) return xw_post(h, XJob{x, q0, bb, k, kt, slots});
   int64_t ng = 0;
   const int rc = issue_exchange(h, x, q0, bb, k, kt, slots, h->host_prof ? &ng : nullptr);
   if (ng) {
@@ -1303,7 +1446,20 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
           s.c2_busy = true;
         }
       }
-      if (multi) HIP_TRY(wait_px(x, cs));
+      if (multi) {
+        // px_keys[x]'s last reader is the exchange of the block kXSlots back. A stream wait on it is a barrier packet in
+        // this compute stream's chain (prep, screen, verify): ~10-16 us of device latency per block even when the
+        // exchange finished long before the stream reaches it (tools/api_cost.hip, r5 timelines). When the caller runs
+        // ahead of the device (the exchange issue thread), the host waits for it instead, before enqueuing — the
+        // compute chain then holds no cross-stream barrier; the device still has kXSlots blocks queued.
+        // (a short host wait only: an exchange slower than ~0.5 ms gets the stream wait, and the handle's deadline
+        // applies where the caller waits for results)
+        if (h->xw && h->x_host_wait_us > 0) {
+          const int64_t t_end = now_ns() + (int64_t)h->x_host_wait_us * 1000;
+          while (hipEventQuery(s.ev_xdone[x]) == hipErrorNotReady && now_ns() < t_end) std::this_thread::yield();
+        }
+        HIP_TRY(wait_px(x, cs));
+      }
       uint64_t* candp = s.cand + (size_t)p * cand_half(s);
       // the f16 copy holds exactly the values the fp32-reading screen rounds to: half the bytes
       const bool bf = h->dtype == RR_DTYPE_BF16;   // (bf16: the int8 copy, DT 9, 64 slots; verified by the bf16 pass)
@@ -1312,7 +1468,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       const bool s8 = bf || (s16 && s.scr8 && i8_active(h));
       const int sdt = bf ? rr::KDT_SCREEN9 : s8 ? rr::KDT_SCREEN8 : s16 ? rr::KDT_SCREEN16 : rr::KDT_SCREEN;
       const bool alone = !two || s.last_vsi < 0 || s.last_vsi == bsi ||
-                         hipEventQuery(s.ev_q[s.last_vq][s.last_vsi]) == hipSuccess;
+                         hipEventQuery(s.evq(s.last_vq, s.last_vsi)) == hipSuccess;
       const int sgrid = screen_grid(h, s, alone);
       const int ct8 = h->ct8 > 0 ? h->ct8 : s.rows() < 500000 ? 2 : 4;   // the int8 screen's tiles per chunk (A/B: RR_SCREEN_CT8)
       // repair mode (rr_sk.hip "Repair"): the screen's chunk geometry, which its per-chunk maxima are indexed by
@@ -1370,7 +1526,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       // results written in place (no exchange): this verify follows the previous one when that ran on the other
       // stream (the same rows of the result buffer)
       if (two && !multi && s.last_vsi >= 0 && s.last_vsi != bsi)
-        HIP_TRY(wait_ev(vs, s.ev_q[s.last_vq][s.last_vsi]));
+        HIP_TRY(wait_ev(vs, s.evq(s.last_vq, s.last_vsi)));
       if (s.rows() > 0 && !h->ab_no_verify) {
         rr::SkArgs v = sk_base(h, s, qb, bb);
         VerifyBlock me;
@@ -1418,7 +1574,13 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         ++h->hp.n[3];
       }
       if (two) {   // this verify (the last reader of query buffer t on this stream)
-        HIP_TRY(hipEventRecord(s.ev_q[t][bsi], vs));
+        if (multi) {   // the keys-ready event of the exchange (enqueue_exchange_px then records none)
+          HIP_TRY(hipEventRecord(s.ev_keys[x], vs));
+          s.evq_alias[t][bsi] = s.ev_keys[x];
+        } else {
+          HIP_TRY(hipEventRecord(s.ev_q[t][bsi], vs));
+          s.evq_alias[t][bsi] = nullptr;
+        }
         s.q_rd[t][bsi] = true;
         s.last_vsi = bsi;
         s.last_vq = t;
@@ -1564,6 +1726,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
   // (large-k lists carry the shard's flag word after the keys)
   const size_t per = (size_t)rr::kQSlots * k + (wk ? kXTail : 0);
   if (h->dist) {   // one process per GPU: one RCCL all-gather over xGMI
+    if (int rc = xw_drain(h)) return rc;   // (the pipelined exchanges' collectives come first, on every rank)
     Shard& s = h->shards[0];
     HIP_TRY(hipSetDevice(s.dev));
     NCCL_TRY(ncclAllGather(s.shard_keys, s.gathered, per, ncclUint64, s.comm, s.stream));
@@ -1612,6 +1775,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
 // Enqueue one block: a screened block goes on its parity's compute stream; any other block runs on `stream`
 // after everything on cstream2, and later cstream2 blocks follow it.
 int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
+  if (h->xw)   // the exchange of the block kXSlots back (its px slot's last reader) must be issued
+    if (int rc = xw_wait(h, kXLag)) return rc;
   const bool scr = screened(h, k, slots);
   if (!scr)
     for (Shard& s : h->shards) {
@@ -1730,6 +1895,7 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   if (const char* e = getenv("RR_VERIFY_CUS")) h->verify_cus = std::max(0, atoi(e));                 // (A/B)
   if (const char* e = getenv("RR_X_SLOTS")) h->xslots = std::min(kXSlots, std::max(2, atoi(e)));     // (A/B)
   if (const char* e = getenv("RR_X_EXCHANGE_DELAY_US")) h->x_delay_us = std::min(1000, std::max(0, atoi(e)));
+  if (const char* e = getenv("RR_X_HOST_WAIT_US")) h->x_host_wait_us = std::max(0, atoi(e));
   if (const char* e = getenv("RR_DIST_TIMEOUT_MS")) h->timeout_ms = std::max(0, atoi(e));   // (the round-3 name)
   if (const char* e = getenv("RR_TIMEOUT_MS")) h->timeout_ms = std::max(0, atoi(e));
   if (const char* e = getenv("RR_WIDE_VERIFY")) h->wide_verify = atoi(e) ? 1 : 0;   // (A/B)
@@ -1747,6 +1913,7 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
 
 void rr_destroy(rr_handle* h) {
   if (!h) return;
+  xw_stop(h);
   if (h->host_prof) {
     static const char* what[10] = {"rr_search_staged", "exchange enqueue", "ncclAllGather call", "screen+verify launches",
                                    "x: ev_keys record", "x: lane waits", "x: merge launch", "x: ev_xdone record",
@@ -1805,6 +1972,7 @@ int rr_init_dist(rr_handle* h, int world, int rank, const char* unique_id) {
   h->world = world;
   h->shard_base = rank;
   h->dist = true;
+  xw_start(h);
   return RR_OK;
 }
 
@@ -2235,6 +2403,7 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
   Shard& s0 = h->shards[0];
   HIP_TRY(hipSetDevice(s0.dev));
   const bool xchg = h->world > 1 || h->dist;
+  if (int rc = xw_drain(h)) return rc;   // (last_x, rcopy: the exchange state is the caller's once drained)
   // without an exchange: after a screened search, on the stream of its last verify (the copy then holds back the
   // next verify on the other stream, which rewrites the rows: ev_q re-recorded below); else on `stream`
   const bool on_v = !xchg && h->last_scr_block && s0.last_vsi >= 0;
@@ -2249,7 +2418,10 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
   // the next writer of these result rows on another stream must wait for the copy: the next screened verify on the
   // other compute stream (ev_q), a cstream2 block after a search on `stream` (ev_fork), an exchange merge on the other
   // lane or a serial exchange on `stream` (ev_rcopy)
-  if (on_v) HIP_TRY(hipEventRecord(s0.ev_q[s0.last_vq][s0.last_vsi], rs));
+  if (on_v) {
+    HIP_TRY(hipEventRecord(s0.ev_q[s0.last_vq][s0.last_vsi], rs));
+    s0.evq_alias[s0.last_vq][s0.last_vsi] = nullptr;
+  }
   if (!xchg && !on_v) {
     if (int rc = fork_point(s0)) return rc;
   }

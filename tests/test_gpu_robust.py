@@ -166,8 +166,12 @@ def test_dist_deadline_fails_loudly(Index, monkeypatch):
     corpus = synth.unit_norm_gaussian(71, 8000, 512)
     q = synth.unit_norm_gaussian(72, 32, 512)
     monkeypatch.setenv("RR_X_EXCHANGE_DELAY_US", "1000")
+    # (the exchange issue thread's short host wait for a slot's previous exchange would otherwise pace the 24 blocks
+    # to the stalled lanes, leaving less than the deadline outstanding at the synchronize)
+    monkeypatch.setenv("RR_X_HOST_WAIT_US", "0")
     ix = Index(dtype="fp32", metric="cosine")
     monkeypatch.delenv("RR_X_EXCHANGE_DELAY_US")
+    monkeypatch.delenv("RR_X_HOST_WAIT_US")
     ix.init_dist(1, 0, get_unique_id())
     ix.load(corpus)
     ix.search(q, 5)                                            # warm: no deadline yet (default 120 s)

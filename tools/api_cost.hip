@@ -2,6 +2,7 @@
 // event, event query, set device), each timed over 2000 calls on an otherwise idle high-priority stream pair.
 // Development tool: hipcc --offload-arch=gfx950 -O2 tools/api_cost.hip -o tools/api_cost
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <chrono>
 #include <cstdio>
 
@@ -10,7 +11,7 @@ __global__ void stamp_kernel(unsigned long long* ts, int slot, unsigned long lon
   const unsigned long long t0 = wall_clock64();
   if (ticks)
     while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
-  if (threadIdx.x == 0) ts[slot] = wall_clock64();
+  if (threadIdx.x == 0 && ts) ts[slot & 1] = wall_clock64();
 }
 
 __global__ void empty_kernel(int* p) {
@@ -88,6 +89,106 @@ int main() {
       cross += (double)(h[1] - h[0]) / 100.0;
     }
     printf("{\"dep_latency_same_stream_us\": %.2f, \"dep_latency_cross_stream_event_us\": %.2f}\n", same / 20, cross / 20);
+  }
+  // the record after a launch on the same stream, vs a launch whose stop event its packet records (hipExtLaunchKernelGGL)
+  {
+    const double t_launch_record = per_call_us(n, [&](int i) {
+      hipLaunchKernelGGL(empty_kernel, dim3(32), dim3(64), 0, a, nullptr);
+      (void)hipEventRecord(ev[i & 63], a);
+    });
+    sync();
+    const double t_ext_stop = per_call_us(n, [&](int i) {
+      hipExtLaunchKernelGGL(empty_kernel, dim3(32), dim3(64), 0, a, nullptr, ev[i & 63], 0, nullptr);
+    });
+    sync();
+    // a wait on a pending event (recorded behind a 40 us kernel on the other stream), then a launch
+    double t_wait_pending = 0;
+    for (int rep = 0; rep < 200; ++rep) {
+      hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, a, (unsigned long long*)nullptr, 2, 4000ull);
+      (void)hipEventRecord(ev[rep & 63], a);
+      const auto t0 = std::chrono::steady_clock::now();
+      (void)hipStreamWaitEvent(b, ev[rep & 63], 0);
+      const auto t1 = std::chrono::steady_clock::now();
+      t_wait_pending += std::chrono::duration<double, std::micro>(t1 - t0).count();
+      hipLaunchKernelGGL(empty_kernel, dim3(32), dim3(64), 0, b, nullptr);
+      sync();
+    }
+    printf("{\"launch_then_record_us\": %.2f, \"ext_launch_with_stop_event_us\": %.2f, \"wait_pending_event_us\": %.2f}\n",
+           t_launch_record, t_ext_stop, t_wait_pending / 200);
+  }
+  // stream memory operations instead of events: hipStreamWriteValue32 on a (after its kernel), hipStreamWaitValue32
+  // on b, then a launch on b — host cost per hand-off and the device-side dependency latency
+  {
+    uint32_t* flag = nullptr;
+    CK(hipMalloc(&flag, 64));
+    CK(hipMemset(flag, 0, 64));
+    unsigned long long* ts = nullptr;
+    CK(hipMalloc(&ts, 64));
+    double host = 0, dev = 0;
+    for (int rep = 1; rep <= 200; ++rep) {
+      hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, a, ts, 0, 4000ull);
+      const auto t0 = std::chrono::steady_clock::now();
+      (void)hipStreamWriteValue32(a, flag, (uint32_t)rep, 0);
+      (void)hipStreamWaitValue32(b, flag, (uint32_t)rep, hipStreamWaitValueGte, 0xFFFFFFFFu);
+      hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, b, ts, 1, 0ull);
+      const auto t1 = std::chrono::steady_clock::now();
+      host += std::chrono::duration<double, std::micro>(t1 - t0).count();
+      sync();
+      unsigned long long h[2];
+      CK(hipMemcpy(h, ts, 16, hipMemcpyDeviceToHost));
+      dev += (double)(h[1] - h[0]) / 100.0;
+    }
+    // the event form of the same hand-off, same shape
+    double host_e = 0, dev_e = 0;
+    for (int rep = 0; rep < 200; ++rep) {
+      hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, a, ts, 0, 4000ull);
+      const auto t0 = std::chrono::steady_clock::now();
+      (void)hipEventRecord(ev[rep & 63], a);
+      (void)hipStreamWaitEvent(b, ev[rep & 63], 0);
+      hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, b, ts, 1, 0ull);
+      const auto t1 = std::chrono::steady_clock::now();
+      host_e += std::chrono::duration<double, std::micro>(t1 - t0).count();
+      sync();
+      unsigned long long h[2];
+      CK(hipMemcpy(h, ts, 16, hipMemcpyDeviceToHost));
+      dev_e += (double)(h[1] - h[0]) / 100.0;
+    }
+    printf("{\"handoff_write_wait_value_host_us\": %.2f, \"handoff_write_wait_value_device_us\": %.2f, "
+           "\"handoff_event_host_us\": %.2f, \"handoff_event_device_us\": %.2f}\n",
+           host / 200, dev / 200, host_e / 200, dev_e / 200);
+  }
+  // same-stream gap K1 -> K2 with packets between them: (a) nothing, (b) one event record, (c) two records, (d) a wait
+  // on an event of the other stream that completed long ago, (e) a wait on an event of the other stream that completes
+  // while K1 still runs (recorded behind a 10 us kernel there)
+  {
+    unsigned long long* ts = nullptr;
+    CK(hipMalloc(&ts, 64));
+    double g[5] = {0, 0, 0, 0, 0};
+    const int reps = 50;
+    for (int rep = 0; rep < reps; ++rep)
+      for (int v = 0; v < 5; ++v) {
+        if (v == 3) {   // an old event on b, complete
+          hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, b, nullptr);
+          (void)hipEventRecord(ev[2], b);
+          sync();
+        }
+        hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, a, ts, 0, 4000ull);
+        if (v == 1 || v == 2) (void)hipEventRecord(ev[3], a);
+        if (v == 2) (void)hipEventRecord(ev[4], a);
+        if (v == 3) (void)hipStreamWaitEvent(a, ev[2], 0);
+        if (v == 4) {
+          hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, b, (unsigned long long*)nullptr, 2, 1000ull);
+          (void)hipEventRecord(ev[5], b);
+          (void)hipStreamWaitEvent(a, ev[5], 0);
+        }
+        hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, a, ts, 1, 0ull);
+        sync();
+        unsigned long long h[2];
+        CK(hipMemcpy(h, ts, 16, hipMemcpyDeviceToHost));
+        g[v] += (double)(h[1] - h[0]) / 100.0;
+      }
+    printf("{\"gap_plain_us\": %.2f, \"gap_record_us\": %.2f, \"gap_two_records_us\": %.2f, \"gap_wait_done_event_us\": %.2f, "
+           "\"gap_wait_event_done_before_k1_end_us\": %.2f}\n", g[0] / reps, g[1] / reps, g[2] / reps, g[3] / reps, g[4] / reps);
   }
   printf("{\"launch_us\": %.2f, \"launch_224x576_us\": %.2f, \"event_record_us\": %.2f, \"stream_wait_event_us\": %.2f, "
          "\"event_query_us\": %.2f, \"set_device_us\": %.2f, \"get_last_error_us\": %.3f, \"record_wait_launch_us\": %.2f}\n",
