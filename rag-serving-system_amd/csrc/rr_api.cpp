@@ -1292,11 +1292,10 @@ int issue_exchange(rr_handle* h, int x, int q0, int bb, int k, int kt, int slots
       HIP_TRY(wait_ev(xs, dst.ev_rcopy));
       dst.rcopy_pending = false;
     }
+    rr::set_launch_events(nullptr, dst.ev_xdone[x]);   // (recorded by the merge's launch packet)
     HIP_TRY(rr::launch_merge(kt, dst.px_gathered[x], h->world, kt, bb, k, nullptr, dst.out_scores + (size_t)q0 * k,
                              dst.out_idx + (size_t)q0 * k, xs, slots, (int64_t)slot, (uint64_t*)dst.out_base));
     lap(6);
-    HIP_TRY(hipEventRecord(dst.ev_xdone[x], xs));
-    lap(7);
     dst.last_x = x;
   }
   return RR_OK;
@@ -1480,7 +1479,9 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         if (int rc = ensure_repair(s, geo.C)) return rc;
       }
       const int64_t tl = h->host_prof ? now_ns() : 0;
-      if (timed) HIP_TRY(hipEventRecord(e0, cs));
+      // (timed: e0 / e1 ride on the prep's and the screen's launch packets — a separate record would hold the next
+      // kernel of this stream ~3 us; rr_internal.h set_launch_events)
+      if (timed && s.rows() <= 0) HIP_TRY(hipEventRecord(e0, cs));
       if (s.rows() > 0) {
         rr::SkArgs a = sk_base(h, s, qb, bb);
         a.out = candp;
@@ -1498,6 +1499,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         if (s16) a.corpus = (const char*)s.scr16;
         if (s8) {   // the queries' int8 pieces on this stream first (the previous block's screen here is done with them)
           const int64_t tq = h->host_prof ? now_ns() : 0;
+          if (timed) rr::set_launch_events(e0, nullptr);
           HIP_TRY(bf ? rr::launch_q8_prep(qb, bb, d, s.q8[bsi], s.q8s[bsi], cs, 1, slots)
                      : rr::launch_q8_prep(qb, bb, d, s.q8[bsi], s.q8s[bsi], cs));
           if (h->host_prof) {
@@ -1516,13 +1518,18 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
           a.eps_b = kScreen8EpsB;
         }
         const int64_t tsc = h->host_prof ? now_ns() : 0;
+        if (timed) rr::set_launch_events(s8 ? nullptr : e0, e1);
         HIP_TRY(rr::launch_sk_args(sdt, h->metric, kt, 0, sgrid, slots, a, cs));
         if (h->host_prof) {
           h->hp.ns[9] += now_ns() - tsc;
           ++h->hp.n[9];
         }
       }
-      if (timed) HIP_TRY(hipEventRecord(e1, cs));
+      if (timed && s.rows() <= 0) HIP_TRY(hipEventRecord(e1, cs));
+      // the verify's completion event (the last kernel of the block on this stream records it through its launch
+      // packet): with an exchange the keys-ready event, else ev_q (this verify, the last reader of query buffer t here)
+      const hipEvent_t vdone = two ? (multi ? s.ev_keys[x] : s.ev_q[t][bsi]) : nullptr;
+      bool vdone_set = false;
       // results written in place (no exchange): this verify follows the previous one when that ran on the other
       // stream (the same rows of the result buffer)
       if (two && !multi && s.last_vsi >= 0 && s.last_vsi != bsi)
@@ -1553,6 +1560,10 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
           v.repair_count = s.wcount + 1;
         }
         const int xdt = bf ? rr::KDT_BF16 : rr::KDT_F32_X3;   // the storage's exact arithmetic
+        if (vdone && !rmode) {
+          rr::set_launch_events(nullptr, vdone);
+          vdone_set = true;
+        }
         HIP_TRY(rr::launch_sk_args(xdt, h->metric, kt, 1, slots, slots, v, vs));
         if (rmode) {
           HIP_TRY(rr::launch_compact_bits(s.rbits[p], (int)((geo.C + 31) / 32), s.rlist[p], s.rcnt[p], vs));
@@ -1563,6 +1574,10 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
           r.rs = geo;
           r.rs_rows = s8 ? 64 : 32;
           HIP_TRY(rr::launch_sk_args(xdt, h->metric, kt, 0, rgrid, slots, r, vs));
+          if (vdone) {
+            rr::set_launch_events(nullptr, vdone);
+            vdone_set = true;
+          }
           HIP_TRY(rr::launch_merge(kt, rbase, rgrid + 1, kt, bb, k, multi ? s.px_keys[x] : nullptr,
                                    multi ? nullptr : osc, multi ? nullptr : oix, vs, slots));
         }
@@ -1574,13 +1589,9 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         ++h->hp.n[3];
       }
       if (two) {   // this verify (the last reader of query buffer t on this stream)
-        if (multi) {   // the keys-ready event of the exchange (enqueue_exchange_px then records none)
-          HIP_TRY(hipEventRecord(s.ev_keys[x], vs));
-          s.evq_alias[t][bsi] = s.ev_keys[x];
-        } else {
-          HIP_TRY(hipEventRecord(s.ev_q[t][bsi], vs));
-          s.evq_alias[t][bsi] = nullptr;
-        }
+        if (!vdone_set) HIP_TRY(hipEventRecord(vdone, vs));   // (no verify launch: a shard without rows, the A/B knob)
+        // with an exchange the keys-ready event (enqueue_exchange_px then records none), ev_q's stand-in
+        s.evq_alias[t][bsi] = multi ? s.ev_keys[x] : nullptr;
         s.q_rd[t][bsi] = true;
         s.last_vsi = bsi;
         s.last_vq = t;
@@ -1588,10 +1599,12 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
     } else if (kt) {
       int grid = fused_grid(s);
       HIP_TRY(wait_px(-1, s.stream));   // no screened verify still reads cand or writes the results
-      if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
+      const bool ev_packet = s.rows() > 0 && use_sk(h);   // (timed: events on the launch packet, as above)
+      if (timed && !ev_packet) HIP_TRY(hipEventRecord(e0, s.stream));
       if (s.rows() > 0) {
         if (use_sk(h)) {
           const int sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(s.cand_grid, (s.rows() + 31) / 32));
+          if (timed) rr::set_launch_events(e0, e1);
           HIP_TRY(rr::launch_sk(sk_dtype_of(h->dtype), h->metric, kt, sgrid, s.corpus, s.norms, s.rscale, qb,
                                 s.rows(), d, bb, base, s.cand, s.stream, 0, slots, h->dyn_sched ? s.ctr : nullptr));
           grid = sgrid;
@@ -1602,7 +1615,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       } else {
         HIP_TRY(hipMemsetAsync(s.cand, 0, (size_t)slots * kt * 8, s.stream));
       }
-      if (timed) HIP_TRY(hipEventRecord(e1, s.stream));
+      if (timed && !ev_packet) HIP_TRY(hipEventRecord(e1, s.stream));
       if (!multi) {
         HIP_TRY(rr::launch_merge(kt, s.cand, grid, kt, bb, k, nullptr, osc, oix, s.stream, slots));
       } else {

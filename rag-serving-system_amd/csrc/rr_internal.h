@@ -2,6 +2,7 @@
 // (rr_kernels.hip). Not part of the public ABI (see include/rag_retrieval.h).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 namespace rr {
@@ -141,6 +142,25 @@ struct SkArgs {
   ChunkGeo rs;
   int rs_rows;
 };
+
+// Events recorded by the NEXT kernel launch of the calling thread through its launch packet (hipExtLaunchKernelGGL:
+// start / stop), instead of hipEventRecord after it: a record is a separate barrier packet that holds the stream's
+// next kernel ~3 us on the device (tools/api_cost.hip: kernel -> record -> kernel 4.5 us, kernel with its stop event
+// -> kernel 1.4 us, as with nothing between). Taken (and cleared) by launch_sk / launch_sk_args, launch_merge and
+// launch_q8_prep; set it right before the launch it is meant for.
+struct LaunchEvents {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+void set_launch_events(hipEvent_t start, hipEvent_t stop);
+LaunchEvents take_launch_events();
+#define RR_LAUNCH(K, G, B, SH, S, ...)                                                      \
+  do {                                                                                    \
+    const ::rr::LaunchEvents le_ = ::rr::take_launch_events();                            \
+    if (le_.start || le_.stop)                                                            \
+      hipExtLaunchKernelGGL(K, G, B, SH, S, le_.start, le_.stop, 0, __VA_ARGS__);         \
+    else                                                                                  \
+      hipLaunchKernelGGL(K, G, B, SH, S, __VA_ARGS__);                                    \
+  } while (0)
 
 // Split-K streaming kernel (rr_sk.hip): same output contract as launch_fused. sdt = KDT_* (0..3).
 // sk_slabs(sdt, d) = 128-byte slabs per wave per row (1..4; bf16 1..2), 0 if d is not supported.

@@ -1072,10 +1072,10 @@ hipError_t launch_merge(int kt, const uint64_t* in, int nlists, int in_kt, int b
   if (b > slots) return hipErrorInvalidValue;
   const int grid = out_keys ? slots : b;
   switch (kt) {
-    case 4: hipLaunchKernelGGL(merge_kernel<4>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out, clear_word); break;
-    case 8: hipLaunchKernelGGL(merge_kernel<8>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out, clear_word); break;
-    case 16: hipLaunchKernelGGL(merge_kernel<16>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out, clear_word); break;
-    case 32: hipLaunchKernelGGL(merge_kernel<32>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out, clear_word); break;
+    case 4: RR_LAUNCH(merge_kernel<4>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out, clear_word); break;
+    case 8: RR_LAUNCH(merge_kernel<8>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out, clear_word); break;
+    case 16: RR_LAUNCH(merge_kernel<16>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out, clear_word); break;
+    case 32: RR_LAUNCH(merge_kernel<32>, dim3(grid), dim3(256), 0, s, in, nlists, slots, b, k_out, out_keys, out_scores, out_idx, list_stride, flag_out, clear_word); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1133,6 +1133,16 @@ hipError_t launch_f32_to_f16(const float* in, uint16_t* out, int64_t nrows, int 
   return hipGetLastError();
 }
 
+namespace {
+thread_local LaunchEvents g_launch_events;
+}  // namespace
+void set_launch_events(hipEvent_t start, hipEvent_t stop) { g_launch_events = LaunchEvents{start, stop}; }
+LaunchEvents take_launch_events() {
+  const LaunchEvents e = g_launch_events;
+  g_launch_events = LaunchEvents{};
+  return e;
+}
+
 hipError_t launch_f32_to_i8(const float* in, int64_t nrows, int d, int8_t* out, float* sx, float* e, hipStream_t s,
                             int bf16) {
   if (nrows < 1 || d % 4 != 0) return hipErrorInvalidValue;
@@ -1146,10 +1156,10 @@ hipError_t launch_q8_prep(const float* q, int b, int d, int8_t* q8, float* q8s, 
   if (b < 1 || d < 1 || d % 4 != 0) return hipErrorInvalidValue;
   if (pieces == 2) {
     if (b > kQSlots || slots != kQSlots) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(q8_prep_kernel, dim3(kQSlots), dim3(64), 0, s, q, b, d, q8, q8s);
+    RR_LAUNCH(q8_prep_kernel, dim3(kQSlots), dim3(64), 0, s, q, b, d, q8, q8s);
   } else {   // one piece: [64][d] pieces and [4][64] scalars, `slots` of them written (32 or 64)
     if (pieces != 1 || b > slots || (slots != 32 && slots != 64)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(q9_prep_kernel, dim3(slots), dim3(64), 0, s, q, b, d, q8, q8s);
+    RR_LAUNCH(q9_prep_kernel, dim3(slots), dim3(64), 0, s, q, b, d, q8, q8s);
   }
   return hipGetLastError();
 }

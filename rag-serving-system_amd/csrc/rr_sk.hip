@@ -1866,7 +1866,7 @@ hipError_t launch_t(int grid, const SkArgs& a, hipStream_t s) {
       return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads + (SCHED ? 64 : 0)), lds, s, a);
+  RR_LAUNCH(kern, dim3(grid), dim3(kThreads + (SCHED ? 64 : 0)), lds, s, a);
   return hipGetLastError();
 }
 

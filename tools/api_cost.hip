@@ -187,6 +187,17 @@ int main() {
         CK(hipMemcpy(h, ts, 16, hipMemcpyDeviceToHost));
         g[v] += (double)(h[1] - h[0]) / 100.0;
       }
+    // (f) K1 launched with its stop event in the launch packet (hipExtLaunchKernelGGL) instead of a separate record
+    double gf = 0;
+    for (int rep = 0; rep < reps; ++rep) {
+      hipExtLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, a, nullptr, ev[6], 0, ts, 0, 4000ull);
+      hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, a, ts, 1, 0ull);
+      sync();
+      unsigned long long h[2];
+      CK(hipMemcpy(h, ts, 16, hipMemcpyDeviceToHost));
+      gf += (double)(h[1] - h[0]) / 100.0;
+    }
+    printf("{\"gap_ext_launch_stop_event_us\": %.2f}\n", gf / reps);
     printf("{\"gap_plain_us\": %.2f, \"gap_record_us\": %.2f, \"gap_two_records_us\": %.2f, \"gap_wait_done_event_us\": %.2f, "
            "\"gap_wait_event_done_before_k1_end_us\": %.2f}\n", g[0] / reps, g[1] / reps, g[2] / reps, g[3] / reps, g[4] / reps);
   }
