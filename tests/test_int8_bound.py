@@ -1,5 +1,6 @@
-"""CPU restatement of the int8 screen's bound (rr_kernels.hip f32_to_i8_kernel / q8_prep_kernel, rr_sk.hip DT 8
-epilogue) in float32 numpy, checked against float64 dot products: the bound must hold for every row, including rows
+"""CPU restatement of the int8 screens' bound (rr_kernels.hip f32_to_i8_kernel / q8_prep_kernel / q9_prep_kernel,
+rr_sk.hip DT 8 and DT 9 epilogues — DT 9: bf16 storage's screen, the rows' bf16 roundings against ONE query piece) in
+float32 numpy, checked against float64 dot products: the bound must hold for every row, including rows
 the int8 copy represents badly (a spike sets the scale and every other element rounds to zero), zero rows, tiny and
 huge magnitudes. This pins the ALGEBRA of the bound (Cauchy-Schwarz on the two residuals); the GPU tests
 (test_gpu_int8.py) pin the kernels against the exact kernel."""
@@ -23,9 +24,10 @@ def quantize_rows(x):
     return q.astype(np.int8), s, e
 
 
-def quantize_query(v):
+def quantize_query(v, pieces=2):
     """q8_prep_kernel: t = q / s, p1 = clamp(rint(t)), p2 = clamp(rint((t - p1) 64)); eq from the exact scaled
-    residual t - p1 - p2 / 64."""
+    residual t - p1 - p2 / 64. pieces = 1 (q9_prep_kernel, rr_device.h q8_prep_slot<1>): p2 = 0, the residual t - p1,
+    the scale s itself."""
     m = F(np.abs(v).max())
     s = F(m / F(127)) if m > 0 else F(0)
     with np.errstate(under="ignore"):
@@ -33,20 +35,27 @@ def quantize_query(v):
             t = (v / s).astype(F)
             a = np.clip(np.rint(t), -127, 127).astype(F)
             ta = (t - a).astype(F)
-            c = np.clip(np.rint(ta * F(64)), -127, 127).astype(F)
-            r = (ta - c * F(2 ** -6)).astype(F)
+            if pieces == 2:
+                c = np.clip(np.rint(ta * F(64)), -127, 127).astype(F)
+                r = (ta - c * F(2 ** -6)).astype(F)
+            else:
+                c = np.zeros_like(v)
+                r = ta
         else:
             a = c = r = np.zeros_like(v)
         eq = F(F(s * np.sqrt((r * r).sum(dtype=F))) * F(1 + 2 ** -12)
                + (m * F(np.sqrt(v.size) * 2 ** -21) + F(2 ** -140)))
         qn = F(np.sqrt((v * v).sum(dtype=F)))
         qsa = F(np.abs(v).sum(dtype=F) * F(1 + 2 ** -18))
-        return a.astype(np.int8), c.astype(np.int8), F(s * F(2 ** -6)), eq, qn, qsa
+        if pieces == 1:   # (the DT 9 MFMA sums x8 . p1: the bound's "64 p1 + p2" with p1 taken once and p2 = 0)
+            return a.astype(np.int8), c.astype(np.int8), F(s), eq, qn, qsa, 1
+        return a.astype(np.int8), c.astype(np.int8), F(s * F(2 ** -6)), eq, qn, qsa, 64
 
 
-def bound(xq, sx, e, nd, p1, p2, qsc, eq, qn, qsa, eps_a=6e-5, eps_b=4e-8):
-    """The DT 8 epilogue's upper bound of x . q (nd: the fp32 row norm the kernel reads, short when squares underflow)."""
-    acc = xq.astype(np.int64) @ (64 * p1.astype(np.int64) + p2.astype(np.int64))   # exact, as the int32 MFMA sums
+def bound(xq, sx, e, nd, p1, p2, qsc, eq, qn, qsa, w1=64, eps_a=6e-5, eps_b=4e-8):
+    """The DT 8 / DT 9 epilogue's upper bound of x . q (nd: the fp32 row norm the kernel reads, short when squares
+    underflow; w1: the first piece's weight, 64 with two pieces, 1 with one)."""
+    acc = xq.astype(np.int64) @ (w1 * p1.astype(np.int64) + p2.astype(np.int64))   # exact, as the int32 MFMA sums
     s = acc.astype(F)
     est = (s * sx).astype(F) * qsc
     sqrt_d = F(np.sqrt(xq.shape[1]) * (1 + 2 ** -20))
@@ -67,8 +76,18 @@ KINDS = ["gauss", "spiky", "scaled", "tiny", "small", "huge", "zero_rows", "spar
          "both_2^-60", "both_2^-64", "rows_2^-100_q_2^-30", "rows_2^-30_q_2^-100", "rows_2^-120"]
 
 
+def bf16_round(x):
+    """fp32 -> its bf16 rounding (RNE), as fp32: the values bf16 storage holds (f32_to_i8_kernel's bf16 = 1 quantises
+    them, and the verify's exact score is of them)."""
+    u = np.ascontiguousarray(x, dtype=F).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000
+    return u.astype(np.uint32).view(F)
+
+
+@pytest.mark.parametrize("pieces", [2, 1])
 @pytest.mark.parametrize("kind", KINDS)
-def test_int8_bound_holds(kind):
+def test_int8_bound_holds(kind, pieces):
+    """pieces 2: DT 8 (fp32 rows); pieces 1: DT 9 (the rows' bf16 roundings; their exact score is of those values)."""
     rng = np.random.default_rng(sum(map(ord, kind)))
     n, d = 3000, 1024
     x = rng.standard_normal((n, d)).astype(F)
@@ -97,6 +116,9 @@ def test_int8_bound_holds(kind):
         x = (x.astype(np.float64) * 2.0 ** int(parts[1].split("^")[1])).astype(F)
         if len(parts) > 2:
             qscale = 2.0 ** int(parts[3].split("^")[1])
+    if pieces == 1:
+        with np.errstate(over="ignore"):
+            x = bf16_round(x)
     xq, sx, e = quantize_rows(x)
     with np.errstate(under="ignore"):   # the fp32 norm the kernels read (row_norms_kernel): squares may underflow
         nd = np.sqrt((x * x).sum(axis=1, dtype=F)).astype(F)
@@ -107,7 +129,7 @@ def test_int8_bound_holds(kind):
             v = (v.astype(np.float64) / max(float(np.abs(v).max()), 1e-300)).astype(F)
         v = (v.astype(np.float64) * qscale).astype(F)
         with np.errstate(under="ignore"):
-            u = bound(xq, sx, e, nd, *quantize_query(v))
+            u = bound(xq, sx, e, nd, *quantize_query(v, pieces))
         exact = x.astype(np.float64) @ v.astype(np.float64)
         assert np.all(u.astype(np.float64) >= exact), float(np.max(exact - u))
 
@@ -125,3 +147,20 @@ def test_int8_bound_is_about_a_quarter_sigma_on_unit_norm_rows():
     slack = u.astype(np.float64) - x.astype(np.float64) @ v.astype(np.float64)
     assert slack.min() >= 0
     assert 0.006 < np.median(slack) < 0.010
+
+
+def test_one_piece_bound_on_unit_norm_bf16_rows():
+    """DT 9 on config 5's data (unit-norm rows stored as bf16, one query piece): the bound holds and its slack stays
+    within ~2x the two-piece screen's — the one-piece residual (up to 64x the two-piece one per element) adds
+    eq |x| ~ 0.008 on unit-norm rows, next to the rows' own e (the 32-candidate verify proves it: profiles/r05)."""
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((4000, 1024)).astype(F)
+    x = bf16_round(x / np.linalg.norm(x, axis=1, keepdims=True))
+    v = rng.standard_normal(1024).astype(F)
+    v /= np.linalg.norm(v)
+    xq, sx, e = quantize_rows(x)
+    nd = np.sqrt((x * x).sum(axis=1, dtype=F)).astype(F)
+    u = bound(xq, sx, e, nd, *quantize_query(v, 1))
+    slack = u.astype(np.float64) - x.astype(np.float64) @ v.astype(np.float64)
+    assert slack.min() >= 0
+    assert 0.008 < np.median(slack) < 0.02, float(np.median(slack))
