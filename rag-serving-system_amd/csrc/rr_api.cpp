@@ -258,6 +258,7 @@ struct rr_handle {
   int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy); bf16: the int8 one
   int screen_i8 = 1;            // ... and an int8 copy, screened first (rr_screen_int8; RR_SCREEN_I8=0 at creation: off)
   int ct8 = 0;                  // the int8 screen's tiles per chunk (0: by shard size; A/B: RR_SCREEN_CT8)
+  int i8_pieces = 2;            // fp32 storage's int8 screen: query pieces (A/B: RR_SCREEN_I8_PIECES=1, the DT 9 form)
   int guided = 1;               // split-K chunks: 2-tile chunks at the end of a launch (A/B: RR_SCREEN_GUIDED=0)
   int64_t i8_min_rows = 65536;  // ... for shards of at least this many rows (RR_SCREEN_I8_MIN_ROWS): below, a search is
                                 // launch-bound and lists holding a large share of the shard's rows leave the looser
@@ -1465,7 +1466,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       const bool s16 = !bf && s.scr16 && h->screen_copy && rr::sk_slabs(rr::KDT_SCREEN16, d);
       // the int8 copy: a quarter of the fp32 bytes, a bound ~8x looser (more rows reach the verify's wide phase)
       const bool s8 = bf || (s16 && s.scr8 && i8_active(h));
-      const int sdt = bf ? rr::KDT_SCREEN9 : s8 ? rr::KDT_SCREEN8 : s16 ? rr::KDT_SCREEN16 : rr::KDT_SCREEN;
+      const bool one_piece = bf || (s8 && h->i8_pieces == 1);   // (one int8 query piece: DT 9)
+      const int sdt = one_piece ? rr::KDT_SCREEN9 : s8 ? rr::KDT_SCREEN8 : s16 ? rr::KDT_SCREEN16 : rr::KDT_SCREEN;
       const bool alone = !two || s.last_vsi < 0 || s.last_vsi == bsi ||
                          hipEventQuery(s.evq(s.last_vq, s.last_vsi)) == hipSuccess;
       const int sgrid = screen_grid(h, s, alone);
@@ -1500,7 +1502,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         if (s8) {   // the queries' int8 pieces on this stream first (the previous block's screen here is done with them)
           const int64_t tq = h->host_prof ? now_ns() : 0;
           if (timed) rr::set_launch_events(e0, nullptr);
-          HIP_TRY(bf ? rr::launch_q8_prep(qb, bb, d, s.q8[bsi], s.q8s[bsi], cs, 1, slots)
+          HIP_TRY(one_piece ? rr::launch_q8_prep(qb, bb, d, s.q8[bsi], s.q8s[bsi], cs, 1, slots)
                      : rr::launch_q8_prep(qb, bb, d, s.q8[bsi], s.q8s[bsi], cs));
           if (h->host_prof) {
             h->hp.ns[8] += now_ns() - tq;
@@ -1917,6 +1919,7 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   if (const char* e = getenv("RR_SCREEN_I8")) h->screen_i8 = atoi(e) != 0;         // (A/B: 0 = the f16 copy only)
   if (const char* e = getenv("RR_SCREEN_I8_MIN_ROWS")) h->i8_min_rows = atoll(e);
   if (const char* e = getenv("RR_SCREEN_CT8")) h->ct8 = atoi(e);
+  if (const char* e = getenv("RR_SCREEN_I8_PIECES")) h->i8_pieces = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("RR_SCREEN_GUIDED")) h->guided = atoi(e) != 0;
   if (const char* e = getenv("RR_STATIC_SCHEDULE")) h->dyn_sched = atoi(e) == 0;   // (A/B: 1 = rr_set_schedule(0))
   if (const char* e = getenv("RR_SCREEN_FULL_LISTS")) h->full_lists_env = atoi(e) != 0;   // (A/B: start with full lists)

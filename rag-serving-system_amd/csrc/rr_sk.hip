@@ -1970,15 +1970,27 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
     return dyn ? sk::launch_metric<8, 2, 1, 0, 1>(metric, ns8, kt, grid, a, s)
                : sk::launch_metric<8, 2, 1>(metric, ns8, kt, grid, a, s);
   }
-  if (sdt == KDT_SCREEN9) {   // bf16 storage's int8 screen: 64 slots, one query piece (a.q8 [64][d], a.q8s [4][64])
+  if (sdt == KDT_SCREEN9) {   // the int8 screen with ONE query piece (a.q8 [64][d], a.q8s [4][64]): bf16 storage's 64
+                              // slots, or (A/B, RR_SCREEN_I8_PIECES=1) fp32 storage's 32
     const int ns8 = sk_slabs(KDT_SCREEN9, a.d);
-    if (qslots != 64 || ring != 2 || !ns8 || kt > 16 || !a.q8 || !a.q8s || !a.sx8 || !a.e8 ||
-        a.n != (a.rows8 + 1) / 2)
+    if ((qslots != 64 && qslots != 32) || ring != 2 || !ns8 || (qslots == 64 && kt > 16) || !a.q8 || !a.q8s ||
+        !a.sx8 || !a.e8 || a.n != (a.rows8 + 1) / 2)
       return hipErrorInvalidValue;
-    // static schedule with the guided tail only: the 9-wave form's register budget (168) spills 10-39 VGPRs here
-    if (a.full_lists == 2) return sk::launch_metric<9, 2, 2, 0, 0, 2>(metric, ns8, kt, grid, a, s);
-    if (a.full_lists) return sk::launch_metric<9, 2, 2, 0, 0, 1>(metric, ns8, kt, grid, a, s);
-    return sk::launch_metric<9, 2, 2>(metric, ns8, kt, grid, a, s);
+    if (qslots == 64) {
+      // static schedule with the guided tail only: the 9-wave form's register budget (168) spills 10-39 VGPRs here
+      if (a.full_lists == 2) return sk::launch_metric<9, 2, 2, 0, 0, 2>(metric, ns8, kt, grid, a, s);
+      if (a.full_lists) return sk::launch_metric<9, 2, 2, 0, 0, 1>(metric, ns8, kt, grid, a, s);
+      return sk::launch_metric<9, 2, 2>(metric, ns8, kt, grid, a, s);
+    }
+    const bool dyn = a.dyn && a.ctr && kt <= 16;
+    if (a.full_lists == 2)
+      return dyn ? sk::launch_metric<9, 2, 1, 0, 1, 2>(metric, ns8, kt, grid, a, s)
+                 : sk::launch_metric<9, 2, 1, 0, 0, 2>(metric, ns8, kt, grid, a, s);
+    if (a.full_lists)
+      return dyn ? sk::launch_metric<9, 2, 1, 0, 1, 1>(metric, ns8, kt, grid, a, s)
+                 : sk::launch_metric<9, 2, 1, 0, 0, 1>(metric, ns8, kt, grid, a, s);
+    return dyn ? sk::launch_metric<9, 2, 1, 0, 1>(metric, ns8, kt, grid, a, s)
+               : sk::launch_metric<9, 2, 1>(metric, ns8, kt, grid, a, s);
   }
   if (sdt == KDT_SCREEN16) {   // the screen over the f16 copy (a.corpus = that copy)
     const int ns16 = sk_slabs(KDT_SCREEN16, a.d);
