@@ -258,7 +258,8 @@ struct rr_handle {
   int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy); bf16: the int8 one
   int screen_i8 = 1;            // ... and an int8 copy, screened first (rr_screen_int8; RR_SCREEN_I8=0 at creation: off)
   int ct8 = 0;                  // the int8 screen's tiles per chunk (0: by shard size; A/B: RR_SCREEN_CT8)
-  int i8_pieces = 2;            // fp32 storage's int8 screen: query pieces (A/B: RR_SCREEN_I8_PIECES=1, the DT 9 form)
+  int i8_pieces = 0;            // fp32 storage's int8 screen: query pieces, 0 = by shard size (kOnePieceRows), 1 or 2
+                                // (RR_SCREEN_I8_PIECES)
   int guided = 1;               // split-K chunks: 2-tile chunks at the end of a launch (A/B: RR_SCREEN_GUIDED=0)
   int64_t i8_min_rows = 65536;  // ... for shards of at least this many rows (RR_SCREEN_I8_MIN_ROWS): below, a search is
                                 // launch-bound and lists holding a large share of the shard's rows leave the looser
@@ -1042,6 +1043,7 @@ int collect_timing(rr_handle* h) {
 // Measured against one stream and every CU screening (profiles/r02/ab/ab_screen_grid*.txt): +23-45 % per step at
 // 125k-250k rows, +2-5 % at 1M-2M.
 constexpr int kVerifyCUs = 32;
+constexpr int64_t kOnePieceRows = 400000;   // fp32 storage's int8 screen: one query piece from this shard size on
 bool two_streams(const rr_handle* h, const Shard&) { return h->streams == 2; }
 // Screen workgroups on shard s; `alone`: no screened block is in flight on the other stream (its last verify has
 // completed: a single search, or the first of a burst), so nothing overlaps this one and every CU screens.
@@ -1466,7 +1468,15 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       const bool s16 = !bf && s.scr16 && h->screen_copy && rr::sk_slabs(rr::KDT_SCREEN16, d);
       // the int8 copy: a quarter of the fp32 bytes, a bound ~8x looser (more rows reach the verify's wide phase)
       const bool s8 = bf || (s16 && s.scr8 && i8_active(h));
-      const bool one_piece = bf || (s8 && h->i8_pieces == 1);   // (one int8 query piece: DT 9)
+      // one int8 query piece (DT 9) or two (DT 8): one halves the screen's matrix work for a bound ~2x looser (slack
+      // 0.0155 vs 0.0079 on unit-norm rows, tests/test_int8_bound.py), so more query slots need the verify's wide
+      // phase — a longer verify, which the step pays on small shards and hides on large ones. Measured
+      // (profiles/r05/pieces/, window / steady): 1M +15 % / +6 %, 500k +8 % / +11 %, 1.25M k = 10 +14 % / +7 %, 250k
+      // -5 % / +4 %, 125k -12 % / -15 %, 10M k = 10 even: one piece from kOnePieceRows rows on — but not in repair
+      // mode, whose repair pass rescores every chunk the bound cannot exclude: on contiguous SQuAD clusters the looser
+      // bound marked so many that the screen fell to 0.5x the exact kernel (two pieces: 2.0x; profiles/r05/pieces/)
+      const bool one_piece =
+          bf || (s8 && (h->i8_pieces == 1 || (h->i8_pieces == 0 && !h->full_lists && s.rows() >= kOnePieceRows)));
       const int sdt = one_piece ? rr::KDT_SCREEN9 : s8 ? rr::KDT_SCREEN8 : s16 ? rr::KDT_SCREEN16 : rr::KDT_SCREEN;
       const bool alone = !two || s.last_vsi < 0 || s.last_vsi == bsi ||
                          hipEventQuery(s.evq(s.last_vq, s.last_vsi)) == hipSuccess;
@@ -1919,7 +1929,7 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   if (const char* e = getenv("RR_SCREEN_I8")) h->screen_i8 = atoi(e) != 0;         // (A/B: 0 = the f16 copy only)
   if (const char* e = getenv("RR_SCREEN_I8_MIN_ROWS")) h->i8_min_rows = atoll(e);
   if (const char* e = getenv("RR_SCREEN_CT8")) h->ct8 = atoi(e);
-  if (const char* e = getenv("RR_SCREEN_I8_PIECES")) h->i8_pieces = atoi(e) == 1 ? 1 : 2;
+  if (const char* e = getenv("RR_SCREEN_I8_PIECES")) h->i8_pieces = std::min(2, std::max(0, atoi(e)));
   if (const char* e = getenv("RR_SCREEN_GUIDED")) h->guided = atoi(e) != 0;
   if (const char* e = getenv("RR_STATIC_SCHEDULE")) h->dyn_sched = atoi(e) == 0;   // (A/B: 1 = rr_set_schedule(0))
   if (const char* e = getenv("RR_SCREEN_FULL_LISTS")) h->full_lists_env = atoi(e) != 0;   // (A/B: start with full lists)

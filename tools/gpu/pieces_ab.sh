@@ -9,3 +9,6 @@ for rep in 1 2; do
     RR_SCREEN_I8_PIECES=$P timeout -k 10 300 python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --exchange-1rank --docs 125000 --variants "" --no-cpu-baseline --no-pmc --ingest-rows 0 > $O/x125k_p${P}_$rep.json 2> $O/x125k_p${P}_$rep.err || exit 1
   done
 done
+# (kernel-argument placement: the screen's prologue with device-memory kernargs forced)
+timeout -k 10 60 $R/tools/probe_screen 125000 224 2 0 1 > $O/probe_default.jsonl 2>&1 &&
+HIP_FORCE_DEV_KERNARG=1 timeout -k 10 60 $R/tools/probe_screen 125000 224 2 0 1 > $O/probe_devkernarg.jsonl 2>&1
