@@ -35,7 +35,8 @@ sys.path.insert(0, os.path.join(REPO, "rag-serving-system_amd"))
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "retrieval queries/sec + p99 latency, batch=32, 1M docs d=1024, 1/2/4/8 GPU"
 SCORE_KERNEL_DOC = ("the corpus-streaming kernel: sk_score_kernel MODE 0 (split-K, LDS-DMA; for fp32 storage the "
-                    "screened search's screen — DT 8 over the int8 screening copy (d a multiple of 512 up to 1024), "
+                    "screened search's screen — over the int8 screening copy (d a multiple of 512 up to 1024) DT 9 with "
+                    "one int8 query piece on 400k-4M-row shards outside repair mode, else DT 8 with two, "
                     "DT 7 over the f16 copy, else DT 6 over the fp32 rows — whose exact fp32 verify of the candidates "
                     "runs on the other compute stream; for bf16 storage's 64-slot blocks DT 9 over the int8 copy of the "
                     "bf16 rows, verified by the bf16 pass's own arithmetic), else fused_score_kernel")

@@ -1043,7 +1043,9 @@ int collect_timing(rr_handle* h) {
 // Measured against one stream and every CU screening (profiles/r02/ab/ab_screen_grid*.txt): +23-45 % per step at
 // 125k-250k rows, +2-5 % at 1M-2M.
 constexpr int kVerifyCUs = 32;
-constexpr int64_t kOnePieceRows = 400000;   // fp32 storage's int8 screen: one query piece from this shard size on
+constexpr int64_t kOnePieceRows = 400000;   // fp32 storage's int8 screen: one query piece from this shard size on,
+constexpr int64_t kOnePieceMaxRows = 4000000;   // ... below this one (10M rows, k = 10: no faster, and a block flagged
+                                                // in the 20-step window, profiles/r05/final/shard_sweep.jsonl)
 bool two_streams(const rr_handle* h, const Shard&) { return h->streams == 2; }
 // Screen workgroups on shard s; `alone`: no screened block is in flight on the other stream (its last verify has
 // completed: a single search, or the first of a burst), so nothing overlaps this one and every CU screens.
@@ -1476,7 +1478,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       // mode, whose repair pass rescores every chunk the bound cannot exclude: on contiguous SQuAD clusters the looser
       // bound marked so many that the screen fell to 0.5x the exact kernel (two pieces: 2.0x; profiles/r05/pieces/)
       const bool one_piece =
-          bf || (s8 && (h->i8_pieces == 1 || (h->i8_pieces == 0 && !h->full_lists && s.rows() >= kOnePieceRows)));
+          bf || (s8 && (h->i8_pieces == 1 || (h->i8_pieces == 0 && !h->full_lists && s.rows() >= kOnePieceRows &&
+                                               s.rows() < kOnePieceMaxRows)));
       const int sdt = one_piece ? rr::KDT_SCREEN9 : s8 ? rr::KDT_SCREEN8 : s16 ? rr::KDT_SCREEN16 : rr::KDT_SCREEN;
       const bool alone = !two || s.last_vsi < 0 || s.last_vsi == bsi ||
                          hipEventQuery(s.evq(s.last_vq, s.last_vsi)) == hipSuccess;
