@@ -34,13 +34,17 @@ def _spiky_corpus(rng, n, d, q):
     return corpus
 
 
+@pytest.mark.parametrize("pieces", ["2", "1"])
 @pytest.mark.parametrize("n,d,b,k", [(4099, 1024, 32, 5), (70001, 1024, 32, 10), (65536, 512, 20, 1),
                                      (12345, 1024, 7, 16), (33, 1024, 32, 3)])
 @pytest.mark.parametrize("metric", ["cosine", "dot"])
-def test_int8_screen_equals_exact(Index, n, d, b, k, metric):
+def test_int8_screen_equals_exact(Index, monkeypatch, n, d, b, k, metric, pieces):
+    """(pieces "1": the one-query-piece form, DT 9 at 32 slots, which large shards screen with — forced here at every
+    size, RR_SCREEN_I8_PIECES)"""
     rng = np.random.default_rng(n + d + k)
     q = rng.standard_normal((b, d)).astype(np.float32)
     corpus = _spiky_corpus(rng, n, d, q)
+    monkeypatch.setenv("RR_SCREEN_I8_PIECES", pieces)
     ix = Index(dtype="fp32", metric=metric)
     ix.load(corpus)
     assert ix.screen_int8()
