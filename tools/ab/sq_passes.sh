@@ -17,3 +17,6 @@ for P in "$P1" "$P2"; do
   timeout -s KILL 200 rocprofv3 --pmc $P -d "$O/p$i" -o p --output-format csv -- \
     python3 "$R/bench.py" --pmc-child --gpus 1 $W > "$O/p$i.out" 2> "$O/p$i.err" || exit 1
 done
+# per-kernel medians on the box; the raw per-dispatch CSVs can exceed what gpurun copies back
+python3 "$R/tools/ab/sq_summary.py" "$O" > "$O/summary.json" || exit 1
+[ -n "$KEEP_RAW" ] || rm -rf "$O"/p1 "$O"/p2
