@@ -201,6 +201,55 @@ int main() {
     printf("{\"gap_plain_us\": %.2f, \"gap_record_us\": %.2f, \"gap_two_records_us\": %.2f, \"gap_wait_done_event_us\": %.2f, "
            "\"gap_wait_event_done_before_k1_end_us\": %.2f}\n", g[0] / reps, g[1] / reps, g[2] / reps, g[3] / reps, g[4] / reps);
   }
+  // hipDeviceSynchronize (torch.cuda.synchronize) after work that has already completed — seen through an event the
+  // host polled, as rr_synchronize does — on S streams, the last command on each (0) an event record after a launch,
+  // (1) a launch with its stop event in the packet; (2) a plain launch (the host sleeps 200 us instead of polling);
+  // (3) as (1), but the host waits with hipEventSynchronize instead of polling hipEventQuery; (4) as (1), polled, then
+  // hipEventSynchronize of the (complete) stop events; and hipStreamSynchronize of each instead
+  {
+    hipStream_t ss[4];
+    for (auto& s : ss) CK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi));
+    hipEvent_t done[4];
+    for (auto& e : done) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (int mode = 0; mode < 5; ++mode)
+      for (int S = 1; S <= 4; S *= 2) {
+        double t_dev = 0, t_str = 0;
+        const int reps = 100;
+        for (int rep = 0; rep < 2 * reps; ++rep) {
+          for (int i = 0; i < S; ++i) {
+            const bool ext = mode == 1 || mode >= 3;
+            if (ext)
+              hipExtLaunchKernelGGL(empty_kernel, dim3(32), dim3(64), 0, ss[i], nullptr, done[i], 0, nullptr);
+            else
+              hipLaunchKernelGGL(empty_kernel, dim3(32), dim3(64), 0, ss[i], nullptr);
+            if (mode == 0) (void)hipEventRecord(done[i], ss[i]);
+          }
+          if (mode == 2) {
+            const auto ts = std::chrono::steady_clock::now();
+            while (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - ts).count() < 200) {
+            }
+          }
+          for (int i = 0; i < S; ++i) {
+            if (mode == 3) (void)hipEventSynchronize(done[i]);
+            if (mode == 0 || mode == 1 || mode == 4)
+              while (hipEventQuery(done[i]) != hipSuccess) {
+              }
+            if (mode == 4) (void)hipEventSynchronize(done[i]);
+          }
+          const auto t0 = std::chrono::steady_clock::now();
+          if (rep & 1) {
+            (void)hipDeviceSynchronize();
+          } else {
+            for (int i = 0; i < S; ++i) (void)hipStreamSynchronize(ss[i]);
+          }
+          const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+          (rep & 1 ? t_dev : t_str) += us;
+          CK(hipDeviceSynchronize());
+        }
+        printf("{\"sync_after_done_mode\": %d, \"streams\": %d, \"device_sync_us\": %.2f, \"stream_syncs_us\": %.2f}\n",
+               mode, S, t_dev / reps, t_str / reps);
+      }
+  }
   printf("{\"launch_us\": %.2f, \"launch_224x576_us\": %.2f, \"event_record_us\": %.2f, \"stream_wait_event_us\": %.2f, "
          "\"event_query_us\": %.2f, \"set_device_us\": %.2f, \"get_last_error_us\": %.3f, \"record_wait_launch_us\": %.2f}\n",
          t_launch, t_launch_big, t_record, t_wait, t_query, t_setdev, t_lasterr, t_handoff);
