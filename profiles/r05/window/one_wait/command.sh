@@ -1,0 +1,8 @@
+# One wait for the flag word and the counters at the window's end: window fixed cost, the screened-search tests, benches.
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${OUT:-r5cnt}; mkdir -p $O; cd /tmp; export TMPDIR=/tmp
+timeout -k 10 200 python3 $R/tools/window_cost.py 125000 --x > $O/wc_x125k.txt 2>&1 &&
+timeout -k 10 200 python3 $R/tools/window_cost.py 1000000 > $O/wc_h1m.txt 2>&1 &&
+timeout -k 10 900 python3 -u -m pytest -x -v --timeout 150 --timeout-method thread -m gpu $R/tests/test_gpu_api.py $R/tests/test_gpu_robust.py $R/tests/test_gpu_screen.py $R/tests/test_gpu_repair.py $R/tests/test_gpu_bench.py > $O/tests.log 2>&1 &&
+timeout -k 10 300 python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --exchange-1rank --docs 125000 --variants "" --no-cpu-baseline --no-pmc --ingest-rows 0 > $O/x125k.json 2> $O/x125k.err &&
+timeout -k 10 300 python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --variants "" --no-cpu-baseline --no-pmc --ingest-rows 0 > $O/h1m.json 2> $O/h1m.err
