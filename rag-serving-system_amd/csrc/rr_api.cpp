@@ -108,6 +108,11 @@ struct Shard {
   // ev_keys[x] is re-recorded kXSlots blocks later, on the same stream — a later point, which only orders more)
   hipEvent_t evq_alias[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
   hipEvent_t evq(int t, int i) const { return evq_alias[t][i] ? evq_alias[t][i] : ev_q[t][i]; }
+  // rr_screen_counts (a timed window's close) waits on a record at each stream's tail: a later hipStreamSynchronize or
+  // hipDeviceSynchronize (torch.cuda.synchronize) returns at once when a stream's last command is a completed record,
+  // but enqueues and awaits a marker of its own, 11-16 us per stream, when it is a kernel or a copy
+  // (tools/api_cost.hip "sync_after_done")
+  hipEvent_t ev_tail[4] = {};
   bool q_rd[2][2] = {{false, false}, {false, false}};   // ev_q[t][i] recorded, no writer of buffer t waited on it yet
   bool fork_pending = false;   // ev_fork was recorded since cstream2 last waited on it
   bool c2_busy = false;        // cstream2 holds work `stream` has not joined
@@ -451,7 +456,8 @@ int free_shard(Shard& s) {
   if (s.copies_done) hipEventDestroy(s.copies_done);
   if (s.ev_cdone) hipEventDestroy(s.ev_cdone);
   if (s.ev_rcopy) hipEventDestroy(s.ev_rcopy);
-  for (hipEvent_t e : {s.ev_fork, s.ev_join, s.ev_stage, s.ev_q[0][0], s.ev_q[0][1], s.ev_q[1][0], s.ev_q[1][1]})
+  for (hipEvent_t e : {s.ev_fork, s.ev_join, s.ev_stage, s.ev_q[0][0], s.ev_q[0][1], s.ev_q[1][0], s.ev_q[1][1],
+                       s.ev_tail[0], s.ev_tail[1], s.ev_tail[2], s.ev_tail[3]})
     if (e) hipEventDestroy(e);
   if (s.comm2) ncclCommDestroy(s.comm2);
   if (s.comm) ncclCommDestroy(s.comm);
@@ -1912,7 +1918,7 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
       if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev_xdone[x], hipEventDisableTiming);
     }
     for (hipEvent_t* ev : {&s.ev_cdone, &s.ev_rcopy, &s.ev_fork, &s.ev_join, &s.ev_stage, &s.ev_q[0][0], &s.ev_q[0][1],
-                           &s.ev_q[1][0], &s.ev_q[1][1]})
+                           &s.ev_q[1][0], &s.ev_q[1][1], &s.ev_tail[0], &s.ev_tail[1], &s.ev_tail[2], &s.ev_tail[3]})
       if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e != hipSuccess) {
       rr_destroy(h);
@@ -2300,6 +2306,37 @@ int sync_streams(rr_handle* h) {
   return collect_timing(h);
 }
 
+// rr_screen_counts' D2H copies on shard s's `stream`: its counters, and for shard 0 the flag word (`flag`: the last
+// search is unsettled), into its pinned staging
+hipError_t queue_count_copies(const rr_handle* h, Shard& s, bool flag) {
+  if (!s.pin_scount) return hipSuccess;
+  hipError_t e = hipSuccess;
+  if (s.scount) e = hipMemcpyAsync(s.pin_scount, s.scount, 4 * sizeof(int), hipMemcpyDeviceToHost, s.stream);
+  if (e == hipSuccess && flag && &s == &h->shards[0] && s.out_base)
+    e = hipMemcpyAsync(s.pin_scount + 4, s.out_base, sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream);
+  return e;
+}
+// sync_streams through records at every stream's tail (Shard::ev_tail), queued on all of them before the first wait
+// (their markers complete side by side), after each shard's count copies (queue_count_copies)
+int sync_streams_tail(rr_handle* h, bool flag) {
+  if (h->xw)   // every posted exchange issued: its launches precede the records
+    if (int rc = xw_drain(h)) return rc;
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    HIP_TRY(queue_count_copies(h, s, flag));
+    const hipStream_t sts[4] = {s.stream, s.xstream, s.xstream2, s.cstream2};
+    for (int i = 0; i < 4; ++i) HIP_TRY(hipEventRecord(s.ev_tail[i], sts[i]));
+  }
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    for (int i = 0; i < 4; ++i)
+      if (int rc = wait_event(h, s, s.ev_tail[i], "device work (stream tails)")) return rc;
+    s.c2_busy = false;
+    s.rcopy_pending = false;
+  }
+  return collect_timing(h);
+}
+
 // D2H of device bytes on local shard 0's `stream` (never the null stream: it sits in the normal-priority queue pool
 // with RCCL's internal streams, whose barrier packets may wait for an all-gather). The streams are idle.
 int copy_out(rr_handle* h, void* dst, const void* src, size_t bytes) {
@@ -2524,34 +2561,26 @@ int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx) {
   return collect_timing(h);
 }
 
-// As rr_synchronize, then the counters: the last search's flag word and shard 0's counters come back in one wait
-// (two copies queued together; the end of a timed window pays this call, bench.py timed_steps). A re-run the flag
-// asks for counts nothing (the exact kernel does not screen); settle_screen waits for it.
+// As rr_synchronize, then the counters: the last search's flag word and every shard's counters come back in the same
+// wait as the streams' work (sync_streams_tail; the end of a timed window pays this call, bench.py timed_steps). A
+// re-run the flag asks for counts nothing (the exact kernel does not screen); settle_screen waits for it.
 int rr_screen_counts(rr_handle* h, int64_t* blocks, int64_t* flagged, int64_t* reruns, int64_t* wide_slots) {
   if (!h) return fail(RR_E_INVALID, "null handle");
   if (h->failed) return failed_handle();
-  if (int rc = sync_streams(h)) return rc;
   const bool unsettled = h->last_screened && !h->last_settled;
+  // every stream idle, with shard 0's flag word (pinned) and each shard's counters copied behind its work
+  if (int rc = sync_streams_tail(h, unsettled)) return rc;
   int64_t fb = 0, ws = 0;
   uint64_t flag = 0;
   for (Shard& s : h->shards) {
-    const bool head = &s == &h->shards[0] && unsettled && s.out_base;
-    if (!s.scount && !head) continue;
-    HIP_TRY(hipSetDevice(s.dev));
-    if (head && !s.pin_scount) {   // (no screened-search buffers yet: the flag alone)
-      if (int rc = read_flag(h, &flag)) return rc;
-      continue;
-    }
-    if (s.scount) HIP_TRY(hipMemcpyAsync(s.pin_scount, s.scount, 4 * sizeof(int), hipMemcpyDeviceToHost, s.stream));
-    if (head) HIP_TRY(hipMemcpyAsync(s.pin_scount + 4, s.out_base, sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream));
-    if (int rc = wait_stream(h, s, s.stream, "the screened-search counts")) return rc;
-    if (s.scount) {
-      fb += ((volatile int*)s.pin_scount)[0];
-      ws += ((volatile int*)s.pin_scount)[2];   // (wcount = scount + 2)
-    }
-    if (head) memcpy(&flag, (const void*)(s.pin_scount + 4), sizeof flag);
+    if (!s.scount || !s.pin_scount) continue;
+    fb += ((volatile int*)s.pin_scount)[0];
+    ws += ((volatile int*)s.pin_scount)[2];   // (wcount = scount + 2)
   }
   if (unsettled) {
+    Shard& s0 = h->shards[0];
+    if (s0.out_base && s0.pin_scount) memcpy(&flag, (const void*)(s0.pin_scount + 4), sizeof flag);
+    else if (int rc = read_flag(h, &flag)) return rc;
     bool rerun = false;
     if (int rc = settle_screen(h, flag, &rerun)) return rc;
   }
