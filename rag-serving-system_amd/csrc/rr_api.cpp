@@ -2316,21 +2316,26 @@ hipError_t queue_count_copies(const rr_handle* h, Shard& s, bool flag) {
     e = hipMemcpyAsync(s.pin_scount + 4, s.out_base, sizeof(uint64_t), hipMemcpyDeviceToHost, s.stream);
   return e;
 }
-// sync_streams through records at every stream's tail (Shard::ev_tail), queued on all of them before the first wait
-// (their markers complete side by side), after each shard's count copies (queue_count_copies)
+// sync_streams ending on records at every stream's tail (Shard::ev_tail): the other streams' records are queued
+// together and waited on together with `stream`'s work; then, every stream idle (the flag word and the counters may
+// be written on any of them), the count copies on `stream` (queue_count_copies) and its own tail record.
 int sync_streams_tail(rr_handle* h, bool flag) {
   if (h->xw)   // every posted exchange issued: its launches precede the records
     if (int rc = xw_drain(h)) return rc;
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
-    HIP_TRY(queue_count_copies(h, s, flag));
-    const hipStream_t sts[4] = {s.stream, s.xstream, s.xstream2, s.cstream2};
-    for (int i = 0; i < 4; ++i) HIP_TRY(hipEventRecord(s.ev_tail[i], sts[i]));
+    for (int i = 1; i < 4; ++i) HIP_TRY(hipEventRecord(s.ev_tail[i], i == 1 ? s.xstream : i == 2 ? s.xstream2 : s.cstream2));
   }
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
-    for (int i = 0; i < 4; ++i)
+    for (int i = 1; i < 4; ++i)
       if (int rc = wait_event(h, s, s.ev_tail[i], "device work (stream tails)")) return rc;
+    HIP_TRY(queue_count_copies(h, s, flag));
+    HIP_TRY(hipEventRecord(s.ev_tail[0], s.stream));
+  }
+  for (Shard& s : h->shards) {
+    HIP_TRY(hipSetDevice(s.dev));
+    if (int rc = wait_event(h, s, s.ev_tail[0], "device work and the screened-search counts")) return rc;
     s.c2_busy = false;
     s.rcopy_pending = false;
   }
