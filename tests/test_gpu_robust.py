@@ -156,6 +156,36 @@ def test_growing_batch_settles_the_last_search_first(Index):
     ex.close()
 
 
+@pytest.mark.parametrize("exchange", [False, True])
+def test_counts_right_after_a_burst_see_every_flag(Index, exchange):
+    """rr_screen_counts straight after a burst of staged searches (bench.py's window close) copies the counters and the
+    last search's flag word only once every stream is idle — the flag is written by the exchange lane's merge
+    (1-rank RCCL) or the last verify, on either compute stream. Every block flagged (screen-fallback): all of them are
+    counted, the last search is settled (one re-run) and its results equal the exact kernel's."""
+    from rag_service_amd import get_unique_id
+    corpus = synth.unit_norm_gaussian(91, 125000, 1024)
+    q = synth.unit_norm_gaussian(92, 32, 1024)
+    ex = _exact(Index, corpus)
+    ix = Index(dtype="fp32", metric="cosine")
+    if exchange:
+        ix.init_dist(1, 0, get_unique_id())
+    ix.load(corpus)
+    ix.set_queries(q)
+    for _ in range(3):
+        ix.search_staged(5)
+    ix.synchronize()
+    ix.set_kernel("screen-fallback")
+    for rnd in range(3):
+        b0, f0, r0, _ = ix.screen_counts_all()
+        for _ in range(7):
+            ix.search_staged(5)
+        b1, f1, r1, _ = ix.screen_counts_all()                 # no synchronize before it
+        assert (b1 - b0, f1 - f0, r1 - r0) == (7, 7, 1), (rnd, b1 - b0, f1 - f0, r1 - r0)
+        assert _same(ix.fetch(), ex.search(q, 5))
+    ix.close()
+    ex.close()
+
+
 def test_dist_deadline_fails_loudly(Index, monkeypatch):
     """The multi-process deadline (rr_set_timeout): device work that does not finish in time makes the wait return
     RR_E_TIMEOUT naming the rank, and fails the handle (later calls: RR_E_STATE). The stall is a stand-in kernel
