@@ -160,15 +160,33 @@ __device__ __forceinline__ void q8_prep_slot(const float* __restrict__ q, int b,
   }
   (void)p2;
   const f32x4* src = (const f32x4*)(q + (size_t)slot * d);
+  // d <= 1024 (every d the int8 copy serves): the lane's <= 4 float4 loaded once, all issued before the first use —
+  // one memory latency for both passes instead of one per float4 per pass (the same values in the same order)
+  constexpr int kRegC = 4;
+  const bool in_regs = d <= 64 * 4 * kRegC;
+  f32x4 vr[kRegC];
+  if (in_regs) {
+#pragma unroll
+    for (int i = 0; i < kRegC; ++i) {
+      const int c = lane + 64 * i;
+      vr[i] = c < (d >> 2) ? src[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
   float m = 0.f, s2 = 0.f, s1 = 0.f;
-  for (int c = lane; c < (d >> 2); c += 64) {
-    const f32x4 v = src[c];
+  auto pass1 = [&](const f32x4 v) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       m = fmaxf(m, fabsf(v[j]));
       s2 = fmaf(v[j], v[j], s2);
       s1 += fabsf(v[j]);
     }
+  };
+  if (in_regs) {
+#pragma unroll
+    for (int i = 0; i < kRegC; ++i)
+      if (lane + 64 * i < (d >> 2)) pass1(vr[i]);
+  } else {
+    for (int c = lane; c < (d >> 2); c += 64) pass1(src[c]);
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
@@ -178,8 +196,7 @@ __device__ __forceinline__ void q8_prep_slot(const float* __restrict__ q, int b,
   }
   const float s = m > 0.f ? m / 127.0f : 0.f;
   float se = 0.f;
-  for (int c = lane; c < (d >> 2); c += 64) {
-    const f32x4 v = src[c];
+  auto pass2 = [&](const f32x4 v, int c) {
     uint32_t w1 = 0, w2 = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -201,6 +218,13 @@ __device__ __forceinline__ void q8_prep_slot(const float* __restrict__ q, int b,
     }
     *(uint32_t*)(p1 + 4 * c) = w1;
     if constexpr (PIECES == 2) *(uint32_t*)(p2 + 4 * c) = w2;
+  };
+  if (in_regs) {
+#pragma unroll
+    for (int i = 0; i < kRegC; ++i)
+      if (lane + 64 * i < (d >> 2)) pass2(vr[i], lane + 64 * i);
+  } else {
+    for (int c = lane; c < (d >> 2); c += 64) pass2(src[c], c);
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) se += __shfl_xor(se, off, 64);
