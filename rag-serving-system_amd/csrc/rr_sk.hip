@@ -350,9 +350,18 @@ __device__ __forceinline__ void merge_lists_for_query(const uint64_t* __restrict
   // per head, each scanning half of them (every wave busy), their counts added through LDS
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
   const u64x2* hv = (const u64x2*)heads;
+  // (16 heads per step while the range allows — eight reads in flight per LDS latency — then 8)
   auto count_above = [&](uint64_t me, int j0, int j1) {
     int rank = 0;
-    for (int j = j0; j < j1; j += 4) {
+    int j = j0;
+    for (; j + 8 <= j1; j += 8) {
+      u64x2 x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = hv[j + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) rank += (x[u][0] > me ? 1 : 0) + (x[u][1] > me ? 1 : 0);
+    }
+    if (j < j1) {   // (j1 - j0 is a multiple of 4)
       u64x2 x[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) x[u] = hv[j + u];
