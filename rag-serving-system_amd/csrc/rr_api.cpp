@@ -2324,7 +2324,8 @@ int sync_streams_tail(rr_handle* h, bool flag) {
     if (int rc = xw_drain(h)) return rc;
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
-    for (int i = 1; i < 4; ++i) HIP_TRY(hipEventRecord(s.ev_tail[i], i == 1 ? s.xstream : i == 2 ? s.xstream2 : s.cstream2));
+    const hipStream_t others[3] = {s.xstream, s.xstream2, s.cstream2};
+    for (int i = 1; i < 4; ++i) HIP_TRY(hipEventRecord(s.ev_tail[i], others[i - 1]));
   }
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
