@@ -140,8 +140,8 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
 // residual's norm (real arithmetic), in the scale's units as f32_to_i8_kernel: t - p1 - p2 / 64 is exact (each step
 // by Sterbenz), so |q - s (p1 + p2 / 64)|_2 <= s |t - p1 - p2/64|_2 (x 1 + 2^-12) + 2^-21 sqrt(d) max|q| + 2^-140.
 // |q| and sum|q| in fp32 (the bound bumps for their summation order). One wave (64 lanes) per query slot `slot`;
-// slots >= b get zero pieces and scalars. Run by the screen launch's joiner workgroups (rr_sk.hip, one slot each) or
-// by q8_prep_kernel (rr_kernels.hip). (Quantising in every screen workgroup instead — each redoing all 32 queries,
+// slots >= b get zero pieces and scalars. Run by q8_prep_kernel / q9_prep_kernel (rr_kernels.hip) in front of the
+// screen on its stream. (Quantising in every screen workgroup instead — each redoing all 32 queries,
 // two L2 passes — measured 8-13 us longer per launch: profiles/r04/ab/int8/.)
 // PIECES = 1 (the bf16-storage screen, DT 9: q ~ s p1, pieces [QS][d], scalars [4][QS] with the scale s itself; up to 64
 // slots) or 2 (DT 8: q ~ s (p1 + p2 / 64), pieces [2][32][d], scale s / 64).
