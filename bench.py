@@ -38,8 +38,8 @@ SCORE_KERNEL_DOC = ("the corpus-streaming kernel: sk_score_kernel MODE 0 (split-
                     "screened search's screen — over the int8 screening copy (d a multiple of 512 up to 1024) DT 9 with "
                     "one int8 query piece on 400k-4M-row shards outside repair mode, else DT 8 with two, "
                     "DT 7 over the f16 copy, else DT 6 over the fp32 rows — whose exact fp32 verify of the candidates "
-                    "runs on the other compute stream; for bf16 storage's 64-slot blocks DT 9 over the int8 copy of the "
-                    "bf16 rows, verified by the bf16 pass's own arithmetic), else fused_score_kernel")
+                    "runs on the other compute stream; for bf16 storage DT 9 over the int8 copy of the bf16 rows, verified by "
+                    "the bf16 pass's own arithmetic), else fused_score_kernel")
 
 
 def is_score_kernel(name: str) -> bool:
@@ -115,7 +115,7 @@ def algorithmic_bytes(rows: int, d: int, batch: int, dtype: str, metric: str, sc
     for cosine, row scale for fp32-split; the int8 copy's norm, scale and error norm), the queries once (fp32; the
     int8 screen's two int8 pieces of 32 slots, or bf16 storage's one piece of 64 slots) and their 4 scalars."""
     if screen8:
-        slots = 64 if dtype == "bf16" else 32
+        slots = 64 if dtype == "bf16" and batch > 32 else 32
         return rows * (d + 12) + 64 * d + 4 * slots * 4
     elem = 2 if dtype == "bf16" or screen16 else 4
     # per-row factors: the norm (cosine; and the fp32 screen's error bound for either metric), the split scale
@@ -292,7 +292,14 @@ def main() -> None:
                          "third of it, at most 120 s) the library's waits on RCCL work; a miss ends the rank with a "
                          "JSON error line naming the rank and stage, and a non-zero exit status")
     ap.add_argument("--dry-run-stall-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="a path setting of the measured handle (rr_set_option: screen_grid, verify_cus, x_slots, "
+                         "x_host_wait_us, screen_i8_pieces, ...; results are the same under every value); repeatable")
     args = ap.parse_args()
+    args.options = {}
+    for o in args.opt:
+        name, _, value = o.partition("=")
+        args.options[name.strip()] = int(value)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
     from rag_service_amd.dist import env_rank_world
@@ -347,7 +354,7 @@ def run(args, stage: dict) -> None:
             return None
 
     stage["stage"] = "handle + RCCL communicator"
-    ix = Index(devices=[local], dtype=args.dtype, metric=args.metric)
+    ix = Index(devices=[local], dtype=args.dtype, metric=args.metric, options=args.options)
     rccl_ranks = 0
     if world > 1:
         uid = broadcast_bytes(dist, get_unique_id() if rank == 0 else None)
@@ -415,8 +422,9 @@ def run(args, stage: dict) -> None:
     n_local = se - sb
     # the fp32 screened search (k <= 29) streams the f16 screening copy when the handle keeps one
     screen16 = args.dtype == "fp32" and args.k <= 29 and args.kernel == "auto" and ix.screen_copy()
-    # bf16 storage: 64-slot blocks (batch > 32) with 16-entry lists (k <= 13) screen its int8 copy (DT 9)
-    screen_bf = (args.dtype == "bf16" and args.batch > 32 and args.k <= 13 and args.kernel == "auto" and
+    # bf16 storage screens its int8 copy (DT 9): 32-slot blocks (batch <= 32, k <= 29) and 64-slot ones (16-entry
+    # lists: k <= 13)
+    screen_bf = (args.dtype == "bf16" and args.k <= (13 if args.batch > 32 else 29) and args.kernel == "auto" and
                  ix.screen_int8())
     screen8 = (screen16 and ix.screen_int8()) or screen_bf   # the int8 copy, unless the adaptive screen gave it up
     alg_bytes = algorithmic_bytes(n_local, args.dim, args.batch, args.dtype, args.metric, screen16, screen8)
@@ -493,16 +501,28 @@ def run(args, stage: dict) -> None:
             vx = Index(devices=[local], dtype=vd, metric=args.metric)
             vx.fill_synthetic(_lib.RR_SYNTH_UNIT_NORM, 1234, args.docs, args.dim)
             vx.set_queries(q)
-            v_el, v_ms, v_n = timed_steps(vx, args.k, args.variant_steps, args.warmup, dist, cuda_sync, 10)
+            v_acct = {}
+            v_el, v_ms, v_n = timed_steps(vx, args.k, args.variant_steps, args.warmup, dist, cuda_sync, 10, v_acct)
             _, v_idx = vx.search(q, args.k)
+            # bf16 storage screens its int8 copy (DT 9, verified by the bf16 pass's own arithmetic): the screen streams
+            # that copy, so its bytes are the launch's algorithmic bytes; the screened steps overlap on two streams
+            v_scr = vd == "bf16" and args.k <= (13 if args.batch > 32 else 29) and vx.screen_int8()
+            v_bytes = algorithmic_bytes(n_local, args.dim, args.batch, vd, args.metric, screen8=v_scr)
             vx.close()
             v_kern = v_ms / max(v_n, 1) / 1e3
-            v_ach = algorithmic_bytes(n_local, args.dim, args.batch, vd, args.metric) / v_kern / 1e9
+            v_step = v_el / args.variant_steps
+            v_ach = v_bytes / (v_step if v_scr else v_kern) / 1e9
             variants[vd] = {"value": round(args.batch * args.variant_steps / v_el, 2), "unit": "queries/s",
-                            "ms_per_step": round(v_el / args.variant_steps * 1e3, 4),
+                            "ms_per_step": round(v_step * 1e3, 4),
                             "kernel_avg_us": round(v_kern * 1e6, 2), "achieved_GBps": round(v_ach, 1),
                             "frac": round(v_ach / HBM_PEAK_GBS, 4), "steps": args.variant_steps,
+                            "alg_bytes_per_launch": v_bytes, "screened": bool(v_scr),
+                            "screen_fallbacks_timed": v_acct.get("flagged"), "reruns_paid": v_acct.get("reruns_paid"),
                             "index_agreement_with_headline": round(float(np.mean(v_idx == head_idx)), 4)}
+            if v_scr:
+                variants[vd]["note"] = ("the screened search over the int8 copy of the bf16 rows (DT 9, one query piece), "
+                                        "verified by the bf16 pass's own arithmetic; frac = its bytes / step time (two "
+                                        "compute streams overlap the launches), every flagged block's exact re-run paid")
 
     clustered = None
     if world == 1 and args.dtype == "fp32" and not args.no_clustered and args.variants:
@@ -558,6 +578,9 @@ def run(args, stage: dict) -> None:
             "exchange": ("rccl ncclAllGather of per-shard top-k keys, device merge on every rank"
                          if world > 1 or rccl_ranks else "none (one shard)"),
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default (4)"),
+            "library_build": _lib.build_info(),
+            "options": args.options,
+            "rr_env": {k: v for k, v in sorted(os.environ.items()) if k.startswith("RR_")},
             "stream_queues_distinct": len(set(queues)),
             "rccl_ranks": rccl_ranks,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
@@ -646,7 +669,7 @@ def pmc_counters(args, kernel_s):
            sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "3", "--warmup", "1",
            "--latency-steps", "1", "--no-cpu-baseline", "--docs", str(args.docs), "--dim", str(args.dim),
            "--batch", str(args.batch), "--k", str(args.k), "--dtype", args.dtype, "--metric", args.metric,
-           "--variants", "", "--kernel", args.kernel]
+           "--variants", "", "--kernel", args.kernel] + [a for o in args.opt for a in ("--opt", o)]
     try:
         subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
         vals = {}

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RR_ABI_VERSION 8
+#define RR_ABI_VERSION 9
 
 /* error codes */
 #define RR_OK             0
@@ -150,6 +150,13 @@ int rr_update_rows(rr_handle* h, const float* host_rows, const int64_t* row_idx,
  * (bf16 corpora are widened). The rows must lie in local shards. Test/diagnostic use. */
 int rr_read_rows(const rr_handle* h, int64_t row_begin, int64_t n_rows, float* host_out);
 
+/* The per-row factors the screens read, for rows [row_begin, row_begin + n_rows) of local shards (diagnostic; the GPU
+ * tests compare them with NumPy): norms = |x| of the stored values (fp32 sum of squares; cosine, and every screen's
+ * bound for either metric), scales / err_norms = the int8 copy's per-row scale max|x| / 127 and rounding-error norm
+ * (RR_E_STATE when a shard holding the rows has no int8 copy). Any output may be null. Synchronises the handle. */
+int rr_screen_factors(rr_handle* h, int64_t row_begin, int64_t n_rows, float* norms, float* scales,
+                      float* err_norms);
+
 /* ---- search ------------------------------------------------------------------------------------ */
 
 /* Synchronous batched search: host queries (b x d fp32, row-major) -> host results
@@ -232,15 +239,16 @@ int rr_screen_copy(rr_handle* h, int32_t use, int32_t* present);
  * scale and the rounding error's norm, the rows as int8 — a quarter of the fp32 bytes per screen — against two int8
  * pieces of each query (v_mfma_i32_32x32x32_i8). Its upper bound (exact integer sums + the error norms, Cauchy-
  * Schwarz) is ~8x looser than the f16 copy's, so more rows reach the verify; results are bit-identical either way.
- * Adaptive: when more than 1 in 32 settled blocks of a window re-run, the handle screens the f16 copy instead (reset
- * at every load). Made at load time for shards of at least 65536 rows when it fits (default; RR_SCREEN_I8=0 at
+ * Corpora whose blocks re-run switch the handle to repair mode (rr_screen_state), which keeps screening this copy.
+ * Made at load time for shards of at least 65536 rows when it fits (default; RR_SCREEN_I8=0 at
  * creation: not made; RR_SCREEN_I8_MIN_ROWS: another row minimum). use = 1: screen it
  * (re-armed; from the next load if none was made), 0: screen the f16 copy, -1: leave as is. *active (may be null):
  * the next search screens the int8 copy on every local shard.
- * bf16 storage: an int8 copy of the bf16 rows (half their bytes), screened against ONE int8 piece per query so that
- * 64 query slots fit a pass, and verified by the bf16 pass's own arithmetic (DT 9 / DT 1 in rr_sk.hip); it is bf16's
- * only screen (no f16 copy), so use = 0 (or the adaptive pause) leaves bf16 on the exact pass. Made for shards of at
- * least 65536 rows (as above) when every row is finite. */
+ * bf16 storage: an int8 copy of the bf16 rows (half their bytes), screened against ONE int8 piece per query (32- and
+ * 64-query blocks), and verified by the bf16 pass's own arithmetic (DT 9 / DT 1 in rr_sk.hip); it is bf16's only
+ * screen (no f16 copy), so use = 0 (or the adaptive pause) leaves bf16 on the exact pass. Made for shards of at least
+ * 65536 rows (as above); screened when every row is finite with a norm of at most 2^60 (the bound's arithmetic then
+ * stays finite; a larger row leaves the handle on the exact pass). */
 int rr_screen_int8(rr_handle* h, int32_t use, int32_t* active);
 
 /* Repair mode (the adaptive screen's answer to corpora whose near-duplicate clusters defeat the screen's lists; see
@@ -270,6 +278,32 @@ int rr_screen_counts(rr_handle* h, int64_t* blocks, int64_t* flagged, int64_t* r
  * Any pointer may be null. */
 int rr_screen_state(rr_handle* h, int32_t* full_lists, int64_t* pause_left, int64_t* pauses);
 
+/* ---- path settings ------------------------------------------------------------------------------------ */
+
+/* Named settings of HOW searches run — never of their results (every path is exact by construction; the GPU tests
+ * check each against RR_KERNEL_EXACT). The defaults are the measured best; the options serve measurements and tests
+ * that must reach a path on small inputs. Synchronises the handle first. RR_E_INVALID for an unknown name or a value
+ * out of range.
+ *   screen_grid          screen workgroups at most (default: one per CU)
+ *   verify_cus           CUs an overlapping screen leaves to the other compute stream's verify (32)
+ *   x_slots              pipelined-exchange buffer sets, 2 or 4 (4)
+ *   x_exchange_delay_us  a one-workgroup delay kernel before each exchange's merge, 0..1000 us (0; a stand-in for a
+ *                        slower all-gather)
+ *   x_host_wait_us       multi-process mode: host wait for a buffer set's previous exchange before a block (500)
+ *   x_thread             multi-process mode: issue the exchanges from a second host thread (1; read by rr_init_dist)
+ *   wide_verify          the verify's wide phase (1)
+ *   screen_ct8           the int8 screen's tiles per chunk: 0 (by shard size), 2 or 4
+ *   screen_i8_pieces     fp32 storage's int8 screen: query pieces, 0 (by shard size), 1 or 2
+ *   screen_guided        2-tile chunks at the end of a screen launch (1)
+ *   screen_full_lists    repair mode from the start and from every load on (0)
+ *   screen_i8_min_rows   the int8 copy is made for shards of at least this many rows (65536; the next load) */
+int rr_set_option(rr_handle* h, const char* name, int64_t value);
+int rr_get_option(const rr_handle* h, const char* name, int64_t* value);
+
+/* "gfx950; product build", or the A/B build's description (RR_AB_ENV: options read from RR_<NAME> environment
+ * variables, and RR_AB_NO_VERIFY, which skips the verify and INVALIDATES results — never set by the product Makefile). */
+const char* rr_build_info(void);
+
 /* ---- deadline ---------------------------------------------------------------------------------------- */
 
 /* Deadline (milliseconds, 0 = the runtime's unbounded blocking waits) of every host wait on this handle's device
@@ -277,7 +311,11 @@ int rr_screen_state(rr_handle* h, int32_t* full_lists, int64_t* pause_left, int6
  * load-time agreement between ranks. Device work that does not complete in time — an all-gather whose peers never
  * arrive, a stream that never drains — makes the call return RR_E_TIMEOUT naming the rank (multi-process) or the
  * local shard, its device, the stream and the newest search block, and fails the handle. Default 120000; the
- * environment variable RR_TIMEOUT_MS (or its round-3 name RR_DIST_TIMEOUT_MS) overrides it at rr_create. */
+ * environment variable RR_TIMEOUT_MS (or its round-3 name RR_DIST_TIMEOUT_MS) overrides it at rr_create.
+ * Multi-process mode with the exchange issue thread (x_thread, the default): the caller's wait for that thread to
+ * ISSUE its posted exchanges (host work: the all-gather and merge enqueues) is bounded by max(30 s, this deadline),
+ * not by a shorter one — the thread's own wake-up can take milliseconds on a loaded host; device work is bounded as
+ * above. */
 int rr_set_timeout(rr_handle* h, int32_t ms);
 
 /* Diagnostic: the hardware (AQL) queue each of local shard `i`'s four streams dispatches to — out[0] compute

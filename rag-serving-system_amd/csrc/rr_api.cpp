@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cctype>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -256,21 +257,23 @@ struct rr_handle {
   int qpar = 0;                 // the staged queries live in every shard's qbuf[qpar]
   int dyn_sched = 1;            // split-K kernels: dynamic chunk schedule (rr_set_schedule)
   int streams = 2;              // compute streams for screened blocks (rr_set_compute_streams)
-  int screen_grid = 1 << 30;    // screen workgroups at most (A/B: RR_SCREEN_GRID)
-  int verify_cus = 32;           // (kVerifyCUs) CUs an overlapping screen leaves to the other stream's verify (A/B: RR_VERIFY_CUS)
-  int xslots = kXSlots;         // pipelined-exchange buffer sets in use (A/B: RR_X_SLOTS, 2..kXSlots)
-  int x_delay_us = 0;           // A/B: RR_X_EXCHANGE_DELAY_US, a stand-in for a slower exchange
-  int x_host_wait_us = 500;     // exchange issue thread: host wait for a px slot's previous exchange (RR_X_HOST_WAIT_US)
+  // (path settings: rr_set_option, kOptions below; results are the same under every value)
+  int screen_grid = 1 << 30;    // screen workgroups at most (screen_grid)
+  int verify_cus = 32;           // (kVerifyCUs) CUs an overlapping screen leaves to the other stream's verify (verify_cus)
+  int xslots = kXSlots;         // pipelined-exchange buffer sets in use (x_slots: 2 or kXSlots)
+  int x_delay_us = 0;           // x_exchange_delay_us: a one-workgroup delay kernel on the exchange lane (a stand-in for
+                                // a slower all-gather, for measurements and the deadline tests)
+  int x_host_wait_us = 500;     // exchange issue thread: host wait for a px slot's previous exchange (x_host_wait_us)
+  int x_thread = 1;             // multi-process mode: the exchange issue thread (x_thread; read at rr_init_dist)
   int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy); bf16: the int8 one
   int screen_i8 = 1;            // ... and an int8 copy, screened first (rr_screen_int8; RR_SCREEN_I8=0 at creation: off)
-  int ct8 = 0;                  // the int8 screen's tiles per chunk (0: by shard size; A/B: RR_SCREEN_CT8)
+  int ct8 = 0;                  // the int8 screen's tiles per chunk (0: by shard size; screen_ct8)
   int i8_pieces = 0;            // fp32 storage's int8 screen: query pieces, 0 = by shard size (kOnePieceRows), 1 or 2
-                                // (RR_SCREEN_I8_PIECES)
-  int guided = 1;               // split-K chunks: 2-tile chunks at the end of a launch (A/B: RR_SCREEN_GUIDED=0)
-  int64_t i8_min_rows = 65536;  // ... for shards of at least this many rows (RR_SCREEN_I8_MIN_ROWS): below, a search is
+                                // (screen_i8_pieces)
+  int guided = 1;               // split-K chunks: 2-tile chunks at the end of a launch (screen_guided)
+  int64_t i8_min_rows = 65536;  // ... for shards of at least this many rows (screen_i8_min_rows, RR_SCREEN_I8_MIN_ROWS): below, a search is
                                 // launch-bound and lists holding a large share of the shard's rows leave the looser
                                 // bound little to prove with (a 1000-row corpus of real embeddings re-ran blocks)
-  bool i8_off = false;          // adaptive: the int8 screen re-ran too often on this corpus, the f16 copy screens
   bool i8_all = false;          // every shard of the world holds an int8 copy (agreed across ranks at load: finish_all)
   bool last_i8 = false;         // the last search screened the int8 copy
   int64_t narrow_settled = 0;   // settled screened blocks run with 16-entry lists where 2k + 2 wanted 32 (screen_kt)
@@ -283,17 +286,18 @@ struct rr_handle {
   bool last_scr_block = false;  // the last block enqueued was a screened one
   // deadline (rr_set_timeout): every host wait on device work polls against it; a miss fails the handle
   int timeout_ms = 120000;
-  bool stream_prio = true;      // streams at the runtime's greatest priority (A/B: RR_STREAM_PRIORITY=0)
+  bool stream_prio = true;      // streams at the runtime's greatest priority (A/B builds: RR_STREAM_PRIORITY=0)
   bool failed = false;
-  int wide_verify = 1;          // the verify's wide phase (A/B: RR_WIDE_VERIFY=0)
+  int wide_verify = 1;          // the verify's wide phase (wide_verify)
   bool host_prof = false;       // RR_HOST_PROF=1 (diagnostics)
   HostProf hp;
-  bool ab_no_verify = false;    // A/B only (RR_AB_NO_VERIFY=1): skip the screened search's verify launch — results
-                                // invalid; measures what the verify's launch costs the step
+  bool ab_no_verify = false;    // A/B builds only (RR_AB_ENV, RR_AB_NO_VERIFY=1): skip the screened search's verify
+                                // launch — results invalid; measures what the verify's launch costs the step. The
+                                // product library never sets it.
   // adaptive screen (observe_settled): the screen's per-lane lists grow from 4 keys to KT once blocks flag, and
   // screening pauses when even that leaves most blocks to the exact pass — decided from settled searches only
   bool full_lists = false;
-  bool full_lists_env = false;              // (A/B: RR_SCREEN_FULL_LISTS=1, full lists from every load)
+  bool full_lists_env = false;              // (screen_full_lists = 1: repair mode from every load on)
   int64_t win_nb = 0, win_nf = 0;           // settled screened blocks of the current window, and re-run ones
   int64_t screen_pause = 0;                 // search blocks still to run without the screen
   int64_t pauses = 0;                       // statistics: pauses so far (since the load)
@@ -535,13 +539,27 @@ int alloc_corpus(rr_handle* h, Shard& s) {
   return RR_OK;
 }
 
-// Per-row norms (cosine, and the screened search's bound for fp32 storage) and, for fp32 storage, whether
-// every value fits the screen's f16 reading (|x| < 2^15). Returns the shard's verdict in *screen_ok.
+// Whether the handle keeps per-row norms: cosine (the denominator), and every screen's bound for either metric — the
+// fp32 screens' eps and the int8 screens' eq |x| and eps terms read |x| (rr_sk.hip epilogue). bf16 storage therefore
+// keeps them for dot too (bf16 + dot left them at the 1.0 placeholder, which the int8 bound read).
+// Split-f16 rows get theirs (of the fp32 values) during the split.
+bool keeps_norms(const rr_handle* h) {
+  return h->metric == RR_METRIC_COSINE || h->dtype == RR_DTYPE_F32 || h->dtype == RR_DTYPE_BF16;
+}
+
+// bf16 storage's int8 screen: rows of norm at most kBf16ScreenNorm (and queries inside the verify's range check,
+// max|q| < 2^15) keep every quantity of the bound finite: |x||q| <= 2^60 2^15 sqrt(d) < 2^81, the estimate and the
+// error terms alike, and the cosine denominator. A larger (or overflowing) row norm turns the screen off for the
+// handle: the exact pass serves it, which divides by the same fp32 norm.
+constexpr float kBf16ScreenNorm = 0x1p60f;
+
+// Per-row norms (keeps_norms) and whether the shard's rows allow the screened search: fp32 storage, every value inside
+// the f16 screens' reading (|x| < 2^15); bf16 storage, every int8 error norm finite and every row norm at most
+// kBf16ScreenNorm. Returns the shard's verdict in *screen_ok.
 int finish_corpus(rr_handle* h, Shard& s, bool* screen_ok) {
   HIP_TRY(hipSetDevice(s.dev));
   const bool f32 = kdt_of(h->dtype) == rr::KDT_F32_MFMA;
-  // split-f16 rows got their norms (of the fp32 values) during the split
-  if ((h->metric == RR_METRIC_COSINE || f32) && s.rows() > 0 && kdt_of(h->dtype) != rr::KDT_F32_SPLIT)
+  if (keeps_norms(h) && s.rows() > 0 && kdt_of(h->dtype) != rr::KDT_F32_SPLIT)
     HIP_TRY(rr::launch_row_norms(h->dtype == RR_DTYPE_BF16 ? 1 : 0, s.corpus, s.rows(), h->d, s.norms, s.stream));
   *screen_ok = false;
   if (f32) {
@@ -559,23 +577,24 @@ int finish_corpus(rr_handle* h, Shard& s, bool* screen_ok) {
     hipFree(dmax);
     *screen_ok = m < 32768.0f;   // also false for NaN
   } else if (h->dtype == RR_DTYPE_BF16) {
-    // the bf16 screen's bound holds for finite rows: every error norm finite (a NaN or infinite value makes its row's
-    // NaN or infinite)
+    // the bf16 screen's bound holds for finite rows (every error norm finite: a NaN or infinite value makes its row's
+    // NaN or infinite) whose norm keeps its arithmetic finite (kBf16ScreenNorm; an overflowing norm reads +inf)
     *screen_ok = true;
     if (s.scr8 && s.rows() > 0) {
       float* dmax = nullptr;
-      HIP_TRY(hipMalloc((void**)&dmax, sizeof(float)));
-      hipError_t e = hipMemsetAsync(dmax, 0, sizeof(float), s.stream);
+      HIP_TRY(hipMalloc((void**)&dmax, 2 * sizeof(float)));
+      hipError_t e = hipMemsetAsync(dmax, 0, 2 * sizeof(float), s.stream);
       if (e == hipSuccess) e = rr::launch_absmax(s.e8, s.rows(), dmax, s.stream);
-      float m = 0.f;
-      if (e == hipSuccess) e = hipMemcpyAsync(&m, dmax, sizeof(float), hipMemcpyDeviceToHost, s.stream);
+      if (e == hipSuccess) e = rr::launch_absmax(s.norms, s.rows(), dmax + 1, s.stream);
+      float m[2] = {0.f, 0.f};
+      if (e == hipSuccess) e = hipMemcpyAsync(m, dmax, 2 * sizeof(float), hipMemcpyDeviceToHost, s.stream);
       if (e != hipSuccess) {
         hipFree(dmax);
         return fail(RR_E_HIP, "corpus range check failed: %s", hipGetErrorString(e));
       }
       if (int rc = wait_stream(h, s, s.stream, "the corpus range check")) return rc;
       hipFree(dmax);
-      *screen_ok = m <= 3.0e38f;   // (false for NaN and infinity)
+      *screen_ok = m[0] <= 3.0e38f && m[1] <= kBf16ScreenNorm;   // (false for NaN and infinity)
     }
   }
   return wait_stream(h, s, s.stream, "the corpus norms");
@@ -763,7 +782,6 @@ int drop_work_buffers(rr_handle* h) {
   h->narrow_settled = h->narrow_reruns = 0;
   h->screen_wide = false;
   h->full_lists = h->full_lists_env;
-  h->i8_off = false;
   h->win_nb = h->win_nf = 0;
   h->screen_pause = h->pauses = 0;
   h->last_screened = false;
@@ -933,13 +951,17 @@ constexpr float kScreen16EpsB = 7.5e-8f;
 constexpr float kScreen8EpsA = 6.0e-5f;
 constexpr float kScreen8EpsB = 4.0e-8f;
 
-// The int8 copy screens (shards that hold one) unless turned off or given way to the f16 copy (observe_settled).
-bool i8_active(const rr_handle* h) { return h->screen_i8 && !h->i8_off && h->screen_copy; }
+// The int8 copy screens (shards that hold one) unless turned off (rr_screen_int8, rr_screen_copy). (Round 4 gave it up
+// for the f16 copy on corpora where blocks re-ran; since r5 repair mode keeps it screening there: observe_settled.)
+bool i8_active(const rr_handle* h) { return h->screen_i8 && h->screen_copy; }
 
-// fp32 storage: 32-slot blocks (the int8, f16-copy or fp32-reading screen, DT 3 verify); bf16 storage: 64-slot blocks
-// over the int8 copy on every shard (DT 9 screen, DT 1 verify: the bf16 pass's own arithmetic), 16-entry lists at most.
+// fp32 storage: 32-slot blocks (the int8, f16-copy or fp32-reading screen, DT 3 verify); bf16 storage: 32- and 64-slot
+// blocks over the int8 copy on every shard (DT 9 screen with one query piece, DT 1 verify: the bf16 pass's own
+// arithmetic), 16-entry lists at most in 64-slot blocks (r6: the 32-slot blocks too — bf16 at the headline batch ran
+// the exact pass before, 104 k q/s against fp32 storage's screened 183 k on the same int8 bytes).
 bool screened_bf16(const rr_handle* h, int k, int slots) {
-  return h->dtype == RR_DTYPE_BF16 && slots == kMaxSlots && i8_active(h) && h->i8_all && screen_kt(h, k) <= 16;
+  return h->dtype == RR_DTYPE_BF16 && i8_active(h) && h->i8_all &&
+         (slots == rr::kQSlots || (slots == kMaxSlots && screen_kt(h, k) <= 16));
 }
 bool screened(const rr_handle* h, int k, int slots) {
   return (h->kernel == RR_KERNEL_AUTO || h->kernel == RR_KERNEL_SCREEN_FALLBACK) &&
@@ -985,7 +1007,6 @@ void observe_settled(rr_handle* h, int blocks, bool narrow, bool full, bool wide
   h->win_nb += blocks;
   h->win_nf += nre;
   if (h->win_nb < 32) return;
-  (void)i8;
   if (!h->full_lists) {
     if (h->win_nf * 32 > h->win_nb) {
       h->full_lists = true;   // repair mode; the narrow lists are judged afresh in it (they no longer re-run)
@@ -1147,7 +1168,7 @@ int local_gather(rr_handle* h, size_t per) {
 // call, the merge launch, two event records and two waits on pending events, each ~3.6 us (tools/api_cost.hip). The
 // caller now records the block's keys-ready event and posts the exchange; this thread issues it (issue_exchange, in
 // post order: the communicators' collectives keep one order on every rank). The caller never runs ahead of it by more
-// than kXLag blocks (px_keys slot reuse, enqueue_block), and drains it (every posted exchange issued) before any host
+// than x_lag blocks (px_keys slot reuse, enqueue_block), and drains it (every posted exchange issued) before any host
 // wait, any collective of its own and any read of the exchange state (last_x, rcopy): a drained worker is idle, so
 // the two threads never touch that state or a communicator at the same time. (r4 measured an issue thread 2-6 %
 // slower while the device set the step; RR_X_THREAD=0: inline.)
@@ -1165,7 +1186,11 @@ struct XWorker {
   std::string errmsg;   // written by the worker before err (release), read by the caller after it (acquire)
   XJob ring[kRing];
 };
-constexpr int kXLag = 2;   // posted exchanges not yet issued, at most, when a block is enqueued (kXSlots - 2)
+// Posted exchanges not yet issued, at most, when a block is enqueued: block i rewrites the px slot of block i - xslots,
+// whose exchange must be issued (its ev_xdone recorded) before block i waits on it — so at most xslots - 1 may be
+// pending; xslots - 2 keeps one block of slack (2 with the default 4 sets, 0 with RR_X_SLOTS = 2: ADVICE r5, with 2
+// sets and a fixed lag of 2 block i waited on a stale ev_xdone and overwrote keys block i - 2's exchange had not read).
+int x_lag(const rr_handle* h);
 
 int issue_exchange(rr_handle* h, int x, int q0, int bb, int k, int kt, int slots, int64_t* ns_gather);
 
@@ -1231,6 +1256,7 @@ int xw_wait(rr_handle* h, int64_t lag) {
   return xw_check(h);
 }
 int xw_drain(rr_handle* h) { return xw_wait(h, 0); }
+int x_lag(const rr_handle* h) { return std::max(0, h->xslots - 2); }
 int xw_post(rr_handle* h, const XJob& j) {
   XWorker* w = h->xw;
   if (int rc = xw_wait(h, XWorker::kRing - 1)) return rc;
@@ -1244,9 +1270,7 @@ int xw_post(rr_handle* h, const XJob& j) {
   return RR_OK;
 }
 void xw_start(rr_handle* h) {
-  if (h->xw) return;
-  if (const char* e = getenv("RR_X_THREAD"))
-    if (atoi(e) == 0) return;
+  if (h->xw || !h->x_thread) return;
   h->xw = new XWorker();
   h->xw->th = std::thread(xw_main, h, h->xw);
 }
@@ -1473,7 +1497,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       }
       uint64_t* candp = s.cand + (size_t)p * cand_half(s);
       // the f16 copy holds exactly the values the fp32-reading screen rounds to: half the bytes
-      const bool bf = h->dtype == RR_DTYPE_BF16;   // (bf16: the int8 copy, DT 9, 64 slots; verified by the bf16 pass)
+      const bool bf = h->dtype == RR_DTYPE_BF16;   // (bf16: the int8 copy, DT 9, 32 or 64 slots; verified by the bf16 pass)
       const bool s16 = !bf && s.scr16 && h->screen_copy && rr::sk_slabs(rr::KDT_SCREEN16, d);
       // the int8 copy: a quarter of the fp32 bytes, a bound ~8x looser (more rows reach the verify's wide phase)
       const bool s8 = bf || (s16 && s.scr8 && i8_active(h));
@@ -1810,8 +1834,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
 // Enqueue one block: a screened block goes on its parity's compute stream; any other block runs on `stream`
 // after everything on cstream2, and later cstream2 blocks follow it.
 int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
-  if (h->xw)   // the exchange of the block kXSlots back (its px slot's last reader) must be issued
-    if (int rc = xw_wait(h, kXLag)) return rc;
+  if (h->xw)   // the exchange of the block xslots back (its px slot's last reader) must be issued
+    if (int rc = xw_wait(h, x_lag(h))) return rc;
   const bool scr = screened(h, k, slots);
   if (!scr)
     for (Shard& s : h->shards) {
@@ -1835,6 +1859,66 @@ int begin_stage(rr_handle* h, int* nq) {
 
   *nq = t;
   return RR_OK;
+}
+
+// ---- path settings (rr_set_option) -----------------------------------------------------------------------------
+// Every option picks HOW a search runs — grid sizes, list widths, query pieces, the exchange's buffering — never its
+// results: each path is exact by construction and the GPU tests check them against the exact kernel. Defaults are the
+// measured best; the options exist for measurements and for tests that reach a path on small inputs.
+struct OptionDesc {
+  const char* name;
+  int64_t lo, hi;
+};
+const OptionDesc kOptions[] = {
+    {"screen_grid", 1, 1 << 30},        // screen workgroups at most
+    {"verify_cus", 0, 256},             // CUs an overlapping screen leaves to the other stream's verify
+    {"x_slots", 2, kXSlots},            // pipelined-exchange buffer sets: 2 or 4 (even: each slot stays on one
+                                        // compute stream, which ev_keys' use as ev_q's stand-in assumes)
+    {"x_exchange_delay_us", 0, 1000},   // a delay kernel on the exchange lane per exchange (a slower all-gather)
+    {"x_host_wait_us", 0, 100000},      // exchange issue thread: host wait for a slot's previous exchange
+    {"x_thread", 0, 1},                 // multi-process mode: the exchange issue thread (before rr_init_dist)
+    {"wide_verify", 0, 1},              // the verify's wide phase
+    {"screen_ct8", 0, 8},               // the int8 screen's tiles per chunk (0: by shard size; 2 or 4)
+    {"screen_i8_pieces", 0, 2},         // fp32 storage's int8 screen: query pieces (0: by shard size)
+    {"screen_guided", 0, 1},            // 2-tile chunks at the end of a screen launch
+    {"screen_full_lists", 0, 1},        // repair mode from the start (and from every load on)
+    {"screen_i8_min_rows", 0, INT64_MAX / 2},   // the int8 copy for shards of at least this many rows (next load)
+};
+
+int64_t* option_field64(rr_handle* h, const std::string& n) { return n == "screen_i8_min_rows" ? &h->i8_min_rows : nullptr; }
+int* option_field(rr_handle* h, const std::string& n) {
+  if (n == "screen_grid") return &h->screen_grid;
+  if (n == "verify_cus") return &h->verify_cus;
+  if (n == "x_slots") return &h->xslots;
+  if (n == "x_exchange_delay_us") return &h->x_delay_us;
+  if (n == "x_host_wait_us") return &h->x_host_wait_us;
+  if (n == "x_thread") return &h->x_thread;
+  if (n == "wide_verify") return &h->wide_verify;
+  if (n == "screen_ct8") return &h->ct8;
+  if (n == "screen_i8_pieces") return &h->i8_pieces;
+  if (n == "screen_guided") return &h->guided;
+  return nullptr;
+}
+int set_option(rr_handle* h, const OptionDesc& o, int64_t v) {
+  const std::string n = o.name;
+  if (v < o.lo || v > o.hi || (n == "x_slots" && v != 2 && v != kXSlots) ||
+      (n == "screen_ct8" && v != 0 && v != 2 && v != 4))
+    return fail(RR_E_INVALID, "option %s = %lld out of range", o.name, (long long)v);
+  if (n == "x_slots") h->xslot = 0;   // (the caller synchronised: no slot in use)
+  if (n == "screen_full_lists") {
+    h->full_lists_env = v != 0;
+    h->full_lists = v != 0;
+    h->win_nb = h->win_nf = 0;
+    return RR_OK;
+  }
+  if (int64_t* f = option_field64(h, n)) *f = v;
+  else *option_field(h, n) = (int)v;
+  return RR_OK;
+}
+const OptionDesc* find_option(const char* name) {
+  for (const OptionDesc& o : kOptions)
+    if (name && strcmp(o.name, name) == 0) return &o;
+  return nullptr;
 }
 
 }  // namespace
@@ -1868,7 +1952,9 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
   h->metric = metric;
   h->world = n_dev;
   h->shards.resize(n_dev);
-  if (const char* e = getenv("RR_STREAM_PRIORITY")) h->stream_prio = atoi(e) != 0;   // (A/B)
+#ifdef RR_AB_ENV
+  if (const char* e = getenv("RR_STREAM_PRIORITY")) h->stream_prio = atoi(e) != 0;   // (A/B builds only)
+#endif
   for (int i = 0; i < n_dev; ++i) {
     Shard& s = h->shards[i];
     if (devices[i] < 0 || devices[i] >= ndev_avail) {
@@ -1925,24 +2011,26 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
       return fail(RR_E_HIP, "event setup failed: %s", hipGetErrorString(e));
     }
   }
-  if (const char* e = getenv("RR_COMPUTE_STREAMS")) h->streams = atoi(e) == 1 ? 1 : 2;   // (A/B)
-  if (const char* e = getenv("RR_SCREEN_GRID")) h->screen_grid = std::max(1, atoi(e));               // (A/B)
-  if (const char* e = getenv("RR_VERIFY_CUS")) h->verify_cus = std::max(0, atoi(e));                 // (A/B)
-  if (const char* e = getenv("RR_X_SLOTS")) h->xslots = std::min(kXSlots, std::max(2, atoi(e)));     // (A/B)
-  if (const char* e = getenv("RR_X_EXCHANGE_DELAY_US")) h->x_delay_us = std::min(1000, std::max(0, atoi(e)));
-  if (const char* e = getenv("RR_X_HOST_WAIT_US")) h->x_host_wait_us = std::max(0, atoi(e));
+  // Environment read by the product library: the deadline (RR_TIMEOUT_MS, or its round-3 name RR_DIST_TIMEOUT_MS), the
+  // int8 copy's switch and row minimum (RR_SCREEN_I8, RR_SCREEN_I8_MIN_ROWS; include/rag_retrieval.h rr_screen_int8)
+  // and RR_HOST_PROF (host-side call timings printed at rr_destroy). Every path setting is an rr_set_option (results
+  // unchanged by any of them); the A/B environment (RR_AB_ENV builds only) is below.
   if (const char* e = getenv("RR_DIST_TIMEOUT_MS")) h->timeout_ms = std::max(0, atoi(e));   // (the round-3 name)
   if (const char* e = getenv("RR_TIMEOUT_MS")) h->timeout_ms = std::max(0, atoi(e));
-  if (const char* e = getenv("RR_WIDE_VERIFY")) h->wide_verify = atoi(e) ? 1 : 0;   // (A/B)
-  if (const char* e = getenv("RR_AB_NO_VERIFY")) h->ab_no_verify = atoi(e) != 0;    // (A/B only: invalid results)
   if (const char* e = getenv("RR_HOST_PROF")) h->host_prof = atoi(e) != 0;
-  if (const char* e = getenv("RR_SCREEN_I8")) h->screen_i8 = atoi(e) != 0;         // (A/B: 0 = the f16 copy only)
-  if (const char* e = getenv("RR_SCREEN_I8_MIN_ROWS")) h->i8_min_rows = atoll(e);
-  if (const char* e = getenv("RR_SCREEN_CT8")) h->ct8 = atoi(e);
-  if (const char* e = getenv("RR_SCREEN_I8_PIECES")) h->i8_pieces = std::min(2, std::max(0, atoi(e)));
-  if (const char* e = getenv("RR_SCREEN_GUIDED")) h->guided = atoi(e) != 0;
-  if (const char* e = getenv("RR_STATIC_SCHEDULE")) h->dyn_sched = atoi(e) == 0;   // (A/B: 1 = rr_set_schedule(0))
-  if (const char* e = getenv("RR_SCREEN_FULL_LISTS")) h->full_lists_env = atoi(e) != 0;   // (A/B: start with full lists)
+  if (const char* e = getenv("RR_SCREEN_I8")) h->screen_i8 = atoi(e) != 0;
+  if (const char* e = getenv("RR_SCREEN_I8_MIN_ROWS")) h->i8_min_rows = std::max<int64_t>(0, atoll(e));
+#ifdef RR_AB_ENV
+  // A/B builds (tools/ab/build_rev.sh ... "-DRR_AB_ENV=1"; never the product Makefile): every option from RR_<NAME>,
+  // and RR_AB_NO_VERIFY, which skips the screened search's verify — INVALID results, for pricing the verify's launch
+  for (const OptionDesc& o : kOptions) {
+    std::string env = "RR_";
+    for (const char* c = o.name; *c; ++c) env += (char)toupper(*c);
+    if (const char* e = getenv(env.c_str())) set_option(h, o, atoll(e));
+  }
+  if (const char* e = getenv("RR_STATIC_SCHEDULE")) h->dyn_sched = atoi(e) == 0;
+  if (const char* e = getenv("RR_AB_NO_VERIFY")) h->ab_no_verify = atoi(e) != 0;
+#endif
   *out = h;
   return RR_OK;
 }
@@ -2101,29 +2189,48 @@ int rr_shard_range(const rr_handle* h, int i, int64_t* begin, int64_t* end) {
 }
 
 int rr_update_rows(rr_handle* h, const float* host_rows, const int64_t* row_idx, int64_t n_rows, int32_t d) {
-  if (!h || ((!host_rows || !row_idx) && n_rows > 0)) return fail(RR_E_INVALID, "null argument");
+  if (!h) return fail(RR_E_INVALID, "null handle");
   if (h->failed) return failed_handle();
-  if (!h->loaded) return fail(RR_E_STATE, "no corpus loaded");
-  if (d != h->d) return fail(RR_E_INVALID, "row dim %d != corpus dim %d", d, h->d);
-  if (n_rows < 0) return fail(RR_E_INVALID, "n_rows=%lld", (long long)n_rows);
-  for (int64_t i = 0; i < n_rows; ++i)
+  // Under rr_init_dist this call is a collective (the range agreement below): every rank reaches it, with its own
+  // argument checks folded into the agreed value, so a rank that rejects its arguments fails together with its peers
+  // instead of leaving them in the allreduce until the deadline.
+  int ok = 1;
+  if ((!host_rows || !row_idx) && n_rows > 0) ok = fail(RR_E_INVALID, "null argument");
+  else if (!h->loaded) ok = fail(RR_E_STATE, "no corpus loaded");
+  else if (d != h->d) ok = fail(RR_E_INVALID, "row dim %d != corpus dim %d", d, h->d);
+  else if (n_rows < 0) ok = fail(RR_E_INVALID, "n_rows=%lld", (long long)n_rows);
+  for (int64_t i = 0; ok == 1 && i < n_rows; ++i)
     if (row_idx[i] < 0 || row_idx[i] >= h->n_total)
-      return fail(RR_E_INVALID, "row index %lld outside [0, %lld)", (long long)row_idx[i], (long long)h->n_total);
-  // the screen reads fp32 rows as f16 (|x| < 2^15): decided over every given row, on the host, then agreed across the
-  // ranks (an RCCL min: a rank given other rows than its peers must not keep screening while they stop — the list
-  // width sizes the all-gather)
-  // (bf16 storage's int8 screen: finite rows, |x| < 2^100 here)
-  const float lim = h->dtype == RR_DTYPE_BF16 ? 0x1p100f : 32768.0f;
-  bool in_range = true;
-  for (int64_t e = 0; e < n_rows * (int64_t)d && in_range; ++e) in_range = fabsf(host_rows[e]) < lim;   // NaN: no
+      ok = fail(RR_E_INVALID, "row index %lld outside [0, %lld)", (long long)row_idx[i], (long long)h->n_total);
+  const int local_rc = ok == 1 ? RR_OK : ok;
+  // Whether the rows keep the screen's bound valid (finish_corpus), decided over every given row on the host:
+  // fp32 storage, every |x| < 2^15 (the f16 screens' reading); bf16 storage, finite rows of norm < 2^59 (its int8
+  // screen's kBf16ScreenNorm, with a margin for the bf16 rounding and the fp32 norm the device computes).
+  bool in_range = local_rc == RR_OK;
+  if (in_range && h->dtype == RR_DTYPE_BF16) {
+    for (int64_t r = 0; r < n_rows && in_range; ++r) {
+      double ss = 0.0;
+      for (int j = 0; j < d; ++j) ss += (double)host_rows[r * d + j] * host_rows[r * d + j];
+      in_range = ss < 0x1p118;   // (NaN: no)
+    }
+  } else if (in_range) {
+    for (int64_t e = 0; e < n_rows * (int64_t)d && in_range; ++e) in_range = fabsf(host_rows[e]) < 32768.0f;   // NaN: no
+  }
   // the last search may still be re-run from the rows about to change: settle it, and let every stream drain
-  if (int rc = rr_synchronize(h)) return rc;
-  int agreed = in_range ? 1 : 0;
-  if (int rc = agree_min(h, &agreed, 1, "the ranks' row-update range agreement", 10)) return rc;
-  in_range = agreed != 0;
+  if (local_rc == RR_OK)
+    if (int rc = rr_synchronize(h)) return rc;   // (a failed handle: its peers meet the deadline below)
+  // agreed across the ranks (an RCCL min): the arguments were valid everywhere, and whether the screen still holds —
+  // a rank given other rows than its peers must not keep screening while they stop (the list width sizes the
+  // all-gather)
+  int agreed[2] = {local_rc == RR_OK ? 1 : 0, in_range ? 1 : 0};
+  const std::string why = g_err;
+  if (int rc = agree_min(h, agreed, 2, "the ranks' row-update agreement", 10)) return rc;
+  if (local_rc != RR_OK) return fail(local_rc, "%s", why.c_str());
+  if (!agreed[0]) return fail(RR_E_INVALID, "rank %d of %d: a peer rank rejected its row update arguments",
+                              h->shard_base, h->world);
+  in_range = agreed[1] != 0;
   const size_t eb = elem_bytes(h->dtype);
-  const bool norms = (h->metric == RR_METRIC_COSINE || kdt_of(h->dtype) == rr::KDT_F32_MFMA) &&
-                     kdt_of(h->dtype) != rr::KDT_F32_SPLIT;   // (the split computes its own)
+  const bool norms = keeps_norms(h) && kdt_of(h->dtype) != rr::KDT_F32_SPLIT;   // (the split computes its own)
   for (Shard& s : h->shards) {
     std::vector<int64_t> mine;
     for (int64_t i = 0; i < n_rows; ++i)
@@ -2185,6 +2292,33 @@ int rr_read_rows(const rr_handle* h, int64_t row_begin, int64_t n_rows, float* h
       hipFree(tmp);
       if (e != hipSuccess) return fail(RR_E_HIP, "read_rows failed: %s", hipGetErrorString(e));
     }
+    done += nr;
+  }
+  return RR_OK;
+}
+
+int rr_screen_factors(rr_handle* h, int64_t row_begin, int64_t n_rows, float* norms, float* scales,
+                      float* err_norms) {
+  if (!h) return fail(RR_E_INVALID, "null handle");
+  if (h->failed) return failed_handle();
+  if (!h->loaded) return fail(RR_E_STATE, "no corpus loaded");
+  if (n_rows < 0) return fail(RR_E_INVALID, "n_rows=%lld", (long long)n_rows);
+  if (int rc = rr_synchronize(h)) return rc;   // (a row update or a load may still be writing them)
+  int64_t done = 0;
+  while (done < n_rows) {
+    const int64_t row = row_begin + done;
+    Shard* sp = nullptr;
+    for (Shard& s : h->shards)
+      if (row >= s.row_begin && row < s.row_end) sp = &s;
+    if (!sp) return fail(RR_E_INVALID, "row %lld is not held locally", (long long)row);
+    if ((scales || err_norms) && !sp->scr8)
+      return fail(RR_E_STATE, "the shard holding row %lld has no int8 copy", (long long)row);
+    const int64_t nr = std::min(n_rows - done, sp->row_end - row);
+    const int64_t lr = row - sp->row_begin;
+    HIP_TRY(hipSetDevice(sp->dev));
+    if (norms) HIP_TRY(hipMemcpy(norms + done, sp->norms + lr, (size_t)nr * 4, hipMemcpyDeviceToHost));
+    if (scales) HIP_TRY(hipMemcpy(scales + done, sp->sx8 + lr, (size_t)nr * 4, hipMemcpyDeviceToHost));
+    if (err_norms) HIP_TRY(hipMemcpy(err_norms + done, sp->e8 + lr, (size_t)nr * 4, hipMemcpyDeviceToHost));
     done += nr;
   }
   return RR_OK;
@@ -2704,7 +2838,7 @@ int rr_screen_int8(rr_handle* h, int32_t use, int32_t* active) {
   if (h->failed) return failed_handle();
   if (use >= 0) {
     h->screen_i8 = use ? 1 : 0;
-    if (use) h->i8_off = false;   // re-armed (a copy exists only if the handle loaded with it on)
+    // (a copy exists only if the handle loaded with it on)
   }
   if (active) {
     bool all = !h->shards.empty();
@@ -2714,6 +2848,34 @@ int rr_screen_int8(rr_handle* h, int32_t use, int32_t* active) {
     *active = all && i8_active(h) && h->loaded ? 1 : 0;
   }
   return RR_OK;
+}
+
+int rr_set_option(rr_handle* h, const char* name, int64_t value) {
+  if (!h || !name) return fail(RR_E_INVALID, "null argument");
+  if (h->failed) return failed_handle();
+  const OptionDesc* o = find_option(name);
+  if (!o) return fail(RR_E_INVALID, "unknown option '%s'", name);
+  if (int rc = rr_synchronize(h)) return rc;   // no search in flight runs under the old setting
+  return set_option(h, *o, value);
+}
+
+int rr_get_option(const rr_handle* h, const char* name, int64_t* value) {
+  if (!h || !name || !value) return fail(RR_E_INVALID, "null argument");
+  const OptionDesc* o = find_option(name);
+  if (!o) return fail(RR_E_INVALID, "unknown option '%s'", name);
+  rr_handle* m = const_cast<rr_handle*>(h);   // (the accessors are shared with the setter; nothing is written)
+  if (strcmp(name, "screen_full_lists") == 0) *value = h->full_lists_env ? 1 : 0;
+  else if (int64_t* f = option_field64(m, name)) *value = *f;
+  else *value = *option_field(m, name);
+  return RR_OK;
+}
+
+const char* rr_build_info(void) {
+#ifdef RR_AB_ENV
+  return "gfx950; A/B build (RR_AB_ENV: options from RR_<NAME>, RR_AB_NO_VERIFY)";
+#else
+  return "gfx950; product build";
+#endif
 }
 
 int rr_set_timing(rr_handle* h, int enable) {

@@ -1151,7 +1151,10 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           if constexpr (COS) {
             u = v * __builtin_amdgcn_rcpf(cos_den(qn, nd));
             u += fabsf(u) * 0x1p-18f + 0x1p-126f;   // (+ |q| in another summation order than the exact path's)
-            u = fminf(fmaxf(u, -1.0f), 1.0f);   // the exact score is clipped to [-1, 1] (retriever.py:609)
+            // the exact score is clipped to [-1, 1] (retriever.py:609). The min comes first: a NaN bound (inf * 0 or
+            // inf - inf in the bound's own arithmetic) becomes +1, never a value below the exact score. (rr_api.cpp
+            // keeps rows and queries where that arithmetic stays finite; this is the kernel's own guard.)
+            u = fmaxf(fminf(u, 1.0f), -1.0f);
           } else {
             u = v;
           }
@@ -1665,7 +1668,9 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     // bound >= its exact score >= the true k-th score >= ek's; they are marked in rbits (mark, every thread, below) and
     // the repair pass merges their exact keys with xk (written to out_keys). Returns whether the slot needs it.
     auto finish = [&](bool complete) -> bool {
-      const bool range = qinfo[QS + vql] < 32768.0f && !a.force_incomplete;   // f16 range of the screen
+      // the query inside the screen's range: max|q| < 2^15 (the f16 screens read q as f16; with it |q| <= 2^15 sqrt(d)
+      // keeps every screen's bound arithmetic finite) and |q| finite (false for a NaN element, which max|q| drops)
+      const bool range = qinfo[QS + vql] < 32768.0f && qinfo[vql] <= 3.0e38f && !a.force_incomplete;
       const bool repair = a.rbits != nullptr && !complete && range;
       complete = complete && range;
       if (!complete && !repair) {   // the first query slot to flag the block also counts it
@@ -1704,6 +1709,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       const uint64_t tb = *vtail;
       const uint32_t rbar = wide_bar(ek, tb);
       const bool wide = !complete && a.wide_verify && !a.force_incomplete && qinfo[QS + vql] < 32768.0f &&
+                        qinfo[vql] <= 3.0e38f &&
                         ((uint32_t)(ek >> 32) > (uint32_t)(tb >> 32) ||
                          (uint32_t)(akeys[a.k_out - 1] >> 32) > (uint32_t)(tb >> 32));
       vstate[0] = wide ? 1 : 0;

@@ -42,7 +42,7 @@ RR_KERNEL_AUTO = 0
 RR_KERNEL_FUSED = 1
 RR_KERNEL_EXACT = 2
 RR_KERNEL_SCREEN_FALLBACK = 3
-RR_ABI_VERSION = 8
+RR_ABI_VERSION = 9
 
 DTYPES = {"fp32": RR_DTYPE_F32, "float32": RR_DTYPE_F32, "f32": RR_DTYPE_F32,
           "bf16": RR_DTYPE_BF16, "bfloat16": RR_DTYPE_BF16, "fp32-split": RR_DTYPE_F32_SPLIT}
@@ -88,6 +88,10 @@ SIGNATURES = {
     "rr_update_rows": (_c_int, [_vp, _fp, _i64p, _c_i64, _c_i32]),
     "rr_screen_state": (_c_int, [_vp, ctypes.POINTER(_c_i32), _i64p, _i64p]),
     "rr_screen_repairs": (_c_int, [_vp, _i64p]),
+    "rr_screen_factors": (_c_int, [_vp, _c_i64, _c_i64, _fp, _fp, _fp]),
+    "rr_set_option": (_c_int, [_vp, ctypes.c_char_p, _c_i64]),
+    "rr_get_option": (_c_int, [_vp, ctypes.c_char_p, _i64p]),
+    "rr_build_info": (ctypes.c_char_p, []),
 }
 
 
@@ -159,6 +163,11 @@ def _i64ptr(a: np.ndarray):
     return a.ctypes.data_as(_i64p)
 
 
+def build_info() -> str:
+    """The library's build: "gfx950; product build", or an A/B build's description (RR_AB_ENV)."""
+    return load_library().rr_build_info().decode()
+
+
 def get_unique_id() -> bytes:
     lib = load_library()
     buf = ctypes.create_string_buffer(RR_UNIQUE_ID_BYTES)
@@ -173,7 +182,9 @@ class Index:
     the corpus size hold (-inf, -1).
     """
 
-    def __init__(self, devices: Optional[Sequence[int]] = None, dtype: str = "fp32", metric: str = "cosine"):
+    def __init__(self, devices: Optional[Sequence[int]] = None, dtype: str = "fp32", metric: str = "cosine",
+                 options: Optional[dict] = None):
+        """options: path settings applied right after creation (rr_set_option; results are the same under any)."""
         self._lib = load_library()
         if dtype not in DTYPES:
             raise ValueError(f"dtype must be one of {sorted(DTYPES)}")
@@ -191,6 +202,8 @@ class Index:
         self.d = 0
         self.kernel = "auto"
         self._tickets = {}
+        for name, value in (options or {}).items():
+            self.set_option(name, value)
 
     # -- lifecycle ---------------------------------------------------------------------------------
     def close(self) -> None:
@@ -378,6 +391,27 @@ class Index:
         f, p, n = _c_i32(), _c_i64(), _c_i64()
         _check(self._lib.rr_screen_state(self._h, ctypes.byref(f), ctypes.byref(p), ctypes.byref(n)))
         return bool(f.value), p.value, n.value
+
+    def set_option(self, name: str, value: int) -> None:
+        """A path setting (rr_set_option: screen_grid, verify_cus, x_slots, x_exchange_delay_us, x_host_wait_us,
+        x_thread, wide_verify, screen_ct8, screen_i8_pieces, screen_guided, screen_full_lists, screen_i8_min_rows).
+        Results are the same under every value."""
+        _check(self._lib.rr_set_option(self._h, name.encode(), int(value)))
+
+    def get_option(self, name: str) -> int:
+        v = _c_i64()
+        _check(self._lib.rr_get_option(self._h, name.encode(), ctypes.byref(v)))
+        return v.value
+
+    def screen_factors(self, row_begin: int, n_rows: int, int8: bool = True):
+        """(norms, int8 scales, int8 error norms) of rows [row_begin, row_begin + n_rows): the per-row factors the
+        screens read (the last two None when int8 is False)."""
+        nrm = np.empty(n_rows, dtype=np.float32)
+        sc = np.empty(n_rows, dtype=np.float32) if int8 else None
+        er = np.empty(n_rows, dtype=np.float32) if int8 else None
+        _check(self._lib.rr_screen_factors(self._h, row_begin, n_rows, _fptr(nrm), _fptr(sc) if int8 else None,
+                                           _fptr(er) if int8 else None))
+        return nrm, sc, er
 
     def set_timeout(self, ms: int) -> None:
         """Deadline of every host wait on device work, both modes (0 = unbounded); a miss raises

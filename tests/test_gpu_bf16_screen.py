@@ -1,8 +1,8 @@
 """The bf16 storage's screened search (rr_sk.hip DT 9 + the DT 1 verify): the screen reads an int8 copy of the bf16 rows
 (per-row scale and error norm, half the bf16 bytes) against ONE int8 piece per query — 64 query slots per pass, the
 batch-64 configs' block — and the verify rescores the candidates with the bf16 pass's own arithmetic (the same K split,
-MFMA order, wave order and epilogue), so results must be BIT-IDENTICAL to the one-pass 64-slot bf16 kernel's. Blocks
-of <= 32 queries keep the exact 32-slot pass (the screen serves 64-slot blocks)."""
+MFMA order, wave order and epilogue), so results must be BIT-IDENTICAL to the one-pass bf16 kernel's. Blocks of <= 32
+queries are screened in 32-slot blocks (r6; round 5 kept them on the exact 32-slot pass)."""
 import numpy as np
 import pytest
 
@@ -46,7 +46,9 @@ def _same(a, b):
 
 
 @pytest.mark.parametrize("n,d,b,k", [(70001, 1024, 64, 10), (4099, 1024, 64, 5), (12345, 512, 40, 13),
-                                     (65536, 1024, 33, 1), (257, 1024, 64, 4)])
+                                     (65536, 1024, 33, 1), (257, 1024, 64, 4),
+                                     # 32-slot blocks (r6): the headline batch, small batches, k up to 29 (32-entry lists)
+                                     (70001, 1024, 32, 5), (12345, 512, 7, 16), (4099, 1024, 32, 29), (257, 1024, 1, 1)])
 @pytest.mark.parametrize("metric", ["cosine", "dot"])
 def test_bf16_screen_equals_exact(Index, n, d, b, k, metric):
     rng = np.random.default_rng(n + d + k + b)
@@ -68,19 +70,26 @@ def test_bf16_screen_equals_exact(Index, n, d, b, k, metric):
     ix.close()
 
 
-def test_bf16_screen_only_for_64_slot_blocks(Index):
-    """32 queries or fewer: the exact 32-slot pass (no screened block); 33-64: one screened 64-slot block; 100: two."""
+def test_bf16_screen_block_shapes(Index):
+    """32 queries or fewer: one screened 32-slot block (r6); 33-64: one screened 64-slot block; 100: two 64-slot
+    blocks; k = 20 (32-entry lists) at 32 queries: a 32-slot block too."""
     rng = np.random.default_rng(3)
     corpus = rng.standard_normal((20000, 1024)).astype(np.float32)
     ix = Index(dtype="bf16", metric="cosine")
     ix.load(corpus)
-    ix.search(rng.standard_normal((32, 1024)).astype(np.float32), 10)
-    assert ix.screen_counts_all()[0] == 0
-    ix.search(rng.standard_normal((64, 1024)).astype(np.float32), 10)
+    q32 = rng.standard_normal((32, 1024)).astype(np.float32)
+    got32 = ix.search(q32, 10)
     assert ix.screen_counts_all()[0] == 1
+    ix.search(rng.standard_normal((64, 1024)).astype(np.float32), 10)
+    assert ix.screen_counts_all()[0] == 2
     q = rng.standard_normal((100, 1024)).astype(np.float32)
     got = ix.search(q, 10)
-    assert ix.screen_counts_all()[0] == 3
+    assert ix.screen_counts_all()[0] == 4
+    got20 = ix.search(q32, 20)
+    assert ix.screen_counts_all()[0] == 5
+    ix.set_kernel("exact")
+    _same(got32, ix.search(q32, 10))
+    _same(got20, ix.search(q32, 20))
     ix.set_kernel("exact")
     _same(got, ix.search(q, 10))
     ix.close()
@@ -187,23 +196,25 @@ def test_non_finite_row_turns_the_screen_off(Index, bad, dtype):
     ix.close()
 
 
-@pytest.mark.parametrize("kind", ["tiny", "huge_row"])
+@pytest.mark.parametrize("kind", ["tiny", "huge_row", "overflow_row"])
 def test_bf16_screen_extreme_magnitudes(Index, kind):
-    """Rows near bf16's range ends: tiny rows (2^-60 scale: squares underflow, the bound's absolute terms carry them) and
-    one huge row (2^60: its bound stays finite and it is found)."""
+    """Rows near bf16's range ends: tiny rows (2^-60 scale: squares underflow, the bound's absolute terms carry them),
+    one huge row (2^40: norm 2^45, its bound stays finite) and one whose norm overflows fp32 (2^60 x a Gaussian row:
+    |x| ~ 2^65 > kBf16ScreenNorm, so the handle leaves bf16 on the exact pass — round 5 screened it with a NaN bound
+    clipped to -1; tests/test_gpu_bound_inputs.py makes that row the true top-1)."""
     rng = np.random.default_rng(13)
     n, d = 20000, 1024
     corpus = rng.standard_normal((n, d)).astype(np.float32)
     if kind == "tiny":
         corpus *= np.float32(2.0 ** -60)
     else:
-        corpus[777] *= np.float32(2.0 ** 60)
+        corpus[777] *= np.float32(2.0 ** (40 if kind == "huge_row" else 60))
     q = rng.standard_normal((64, d)).astype(np.float32)
     for metric in ("dot", "cosine"):
         ix = Index(dtype="bf16", metric=metric)
         ix.load(corpus)
         got = ix.search(q, 10)
-        assert ix.screen_counts_all()[0] == 1
+        assert ix.screen_counts_all()[0] == (0 if kind == "overflow_row" else 1)
         ix.set_kernel("exact")
         _same(got, ix.search(q, 10))
         ix.close()

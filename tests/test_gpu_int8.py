@@ -40,12 +40,11 @@ def _spiky_corpus(rng, n, d, q):
 @pytest.mark.parametrize("metric", ["cosine", "dot"])
 def test_int8_screen_equals_exact(Index, monkeypatch, n, d, b, k, metric, pieces):
     """(pieces "1": the one-query-piece form, DT 9 at 32 slots, which large shards screen with — forced here at every
-    size, RR_SCREEN_I8_PIECES)"""
+    size, option screen_i8_pieces)"""
     rng = np.random.default_rng(n + d + k)
     q = rng.standard_normal((b, d)).astype(np.float32)
     corpus = _spiky_corpus(rng, n, d, q)
-    monkeypatch.setenv("RR_SCREEN_I8_PIECES", pieces)
-    ix = Index(dtype="fp32", metric=metric)
+    ix = Index(dtype="fp32", metric=metric, options={"screen_i8_pieces": int(pieces)})
     ix.load(corpus)
     assert ix.screen_int8()
     got = ix.search(q, k)
@@ -132,14 +131,13 @@ def test_int8_screen_sharded_and_odd_rows(Index):
 
 @pytest.mark.parametrize("ct", ["2", "4"])
 def test_int8_screen_chunk_sizes(Index, monkeypatch, ct):
-    """The int8 screen's dynamic-schedule chunk (2 tiles of 64 rows below 500k rows per shard, else 4; RR_SCREEN_CT8
-    forces either): any chunk size gives the exact kernel's results, on the static schedule too."""
-    monkeypatch.setenv("RR_SCREEN_CT8", ct)
+    """The int8 screen's dynamic-schedule chunk (2 tiles of 64 rows below 500k rows per shard, else 4; option
+    screen_ct8 forces either): any chunk size gives the exact kernel's results, on the static schedule too."""
     rng = np.random.default_rng(int(ct))
     n, d = 150001, 1024
     q = rng.standard_normal((32, d)).astype(np.float32)
     corpus = _spiky_corpus(rng, n, d, q)
-    ix = Index(dtype="fp32", metric="cosine")
+    ix = Index(dtype="fp32", metric="cosine", options={"screen_ct8": int(ct)})
     ix.load(corpus)
     assert ix.screen_int8()
     got = [ix.search(q, 5)]

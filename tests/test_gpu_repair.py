@@ -19,15 +19,13 @@ def Index(hip):
 
 
 def _repair_handle(Index, monkeypatch, metric, i8, devices=None, dist=False):
-    """A handle in repair mode from its load (RR_SCREEN_FULL_LISTS=1), screening the int8 copy (i8, made for small
-    corpora with RR_SCREEN_I8_MIN_ROWS=0) or the f16 copy."""
+    """A handle in repair mode from its load (option screen_full_lists), screening the int8 copy (i8, made for small
+    corpora with screen_i8_min_rows = 0) or the f16 copy."""
     from rag_service_amd import get_unique_id
-    monkeypatch.setenv("RR_SCREEN_FULL_LISTS", "1")
+    opts = {"screen_full_lists": 1}
     if i8:
-        monkeypatch.setenv("RR_SCREEN_I8_MIN_ROWS", "0")
-    ix = Index(devices=devices or [0], dtype="fp32", metric=metric)
-    monkeypatch.delenv("RR_SCREEN_FULL_LISTS")
-    monkeypatch.delenv("RR_SCREEN_I8_MIN_ROWS", raising=False)
+        opts["screen_i8_min_rows"] = 0
+    ix = Index(devices=devices or [0], dtype="fp32", metric=metric, options=opts)
     if dist:
         ix.init_dist(1, 0, get_unique_id())
     return ix

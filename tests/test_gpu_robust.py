@@ -189,19 +189,15 @@ def test_counts_right_after_a_burst_see_every_flag(Index, exchange):
 def test_dist_deadline_fails_loudly(Index, monkeypatch):
     """The multi-process deadline (rr_set_timeout): device work that does not finish in time makes the wait return
     RR_E_TIMEOUT naming the rank, and fails the handle (later calls: RR_E_STATE). The stall is a stand-in kernel
-    holding the exchange stream 1 ms per search block (RR_X_EXCHANGE_DELAY_US), after each block's all-gather, with
+    holding the exchange stream 1 ms per search block (option x_exchange_delay_us), after each block's all-gather, with
     a 2 ms deadline over 24 blocks; the device is left to drain before the handle is destroyed."""
     from rag_service_amd import get_unique_id
     from rag_service_amd._lib import HipRetrievalError, RR_E_STATE, RR_E_TIMEOUT
     corpus = synth.unit_norm_gaussian(71, 8000, 512)
     q = synth.unit_norm_gaussian(72, 32, 512)
-    monkeypatch.setenv("RR_X_EXCHANGE_DELAY_US", "1000")
     # (the exchange issue thread's short host wait for a slot's previous exchange would otherwise pace the 24 blocks
-    # to the stalled lanes, leaving less than the deadline outstanding at the synchronize)
-    monkeypatch.setenv("RR_X_HOST_WAIT_US", "0")
-    ix = Index(dtype="fp32", metric="cosine")
-    monkeypatch.delenv("RR_X_EXCHANGE_DELAY_US")
-    monkeypatch.delenv("RR_X_HOST_WAIT_US")
+    # to the stalled lanes, leaving less than the deadline outstanding at the synchronize: x_host_wait_us = 0)
+    ix = Index(dtype="fp32", metric="cosine", options={"x_exchange_delay_us": 1000, "x_host_wait_us": 0})
     ix.init_dist(1, 0, get_unique_id())
     ix.load(corpus)
     ix.search(q, 5)                                            # warm: no deadline yet (default 120 s)
@@ -228,15 +224,13 @@ def test_dist_deadline_fails_loudly(Index, monkeypatch):
 def test_single_process_deadline_names_shard_and_stream(Index, monkeypatch):
     """Round 3's one hang (a stream that never drained, rr_search never returned) becomes a loud error: within one
     process too, every host wait polls against the handle's deadline (rr_set_timeout). Two shards on one device
-    exchange by peer copies; a stand-in kernel holds the exchange lanes 1 ms per search block (RR_X_EXCHANGE_DELAY_US)
+    exchange by peer copies; a stand-in kernel holds the exchange lanes 1 ms per search block (x_exchange_delay_us)
     under a 2 ms deadline over 24 blocks: the wait returns RR_E_TIMEOUT naming the shard, its device and the stream,
     and the handle is failed (later calls: RR_E_STATE)."""
     from rag_service_amd._lib import HipRetrievalError, RR_E_STATE, RR_E_TIMEOUT
     corpus = synth.unit_norm_gaussian(73, 8000, 512)
     q = synth.unit_norm_gaussian(74, 32, 512)
-    monkeypatch.setenv("RR_X_EXCHANGE_DELAY_US", "1000")
-    ix = Index(devices=[0, 0], dtype="fp32", metric="cosine")
-    monkeypatch.delenv("RR_X_EXCHANGE_DELAY_US")
+    ix = Index(devices=[0, 0], dtype="fp32", metric="cosine", options={"x_exchange_delay_us": 1000})
     ix.load(corpus)
     ix.search(q, 5)                                            # warm, default 120 s deadline
     ix.set_timeout(2)

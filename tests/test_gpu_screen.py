@@ -75,7 +75,7 @@ def test_screen_ties_take_the_exact_pass(Index, monkeypatch, wide, i8):
     """40 copies of one row spread over the corpus, queried with that row: 40 exactly tied top scores, more
     than the screen's global candidate list holds. The verify's wide phase rescores every list entry above the
     largest single-list bound (the copies lie in many workgroups' lists) and proves the top-k; without it
-    (RR_WIDE_VERIFY=0) the bound cannot prove completeness and the search is re-run exactly. Either way the
+    (option wide_verify = 0) the bound cannot prove completeness and the search is re-run exactly. Either way the
     result is the canonical order (equal scores by ascending index), bit-identical to the one-pass exact kernel,
     for cosine and dot."""
     corpus = synth.unit_norm_gaussian(77, 65536, 1024)
@@ -83,9 +83,7 @@ def test_screen_ties_take_the_exact_pass(Index, monkeypatch, wide, i8):
     corpus[dup] = corpus[123]
     q = np.concatenate([corpus[123:124], synth.unit_norm_gaussian(78, 31, 1024)])
     for metric in ("cosine", "dot"):
-        monkeypatch.setenv("RR_WIDE_VERIFY", "1" if wide else "0")
-        ix = Index(dtype="fp32", metric=metric)
-        monkeypatch.delenv("RR_WIDE_VERIFY")
+        ix = Index(dtype="fp32", metric=metric, options={"wide_verify": 1 if wide else 0})
         ix.load(corpus)
         assert ix.screen_int8() and ix.screen_int8(i8) == i8
         got = ix.search(q, 5)

@@ -164,3 +164,42 @@ def test_one_piece_bound_on_unit_norm_bf16_rows():
     slack = u.astype(np.float64) - x.astype(np.float64) @ v.astype(np.float64)
     assert slack.min() >= 0
     assert 0.008 < np.median(slack) < 0.02, float(np.median(slack))
+
+
+def residual_aligned_row(v, b, target=0.5, pieces=1):
+    """A row aligned with query v's quantisation residual r = v - scale (p1 [+ p2 / 64]): x = b r^
+    + beta w (w: v's component orthogonal to r, beta so that x . v = target). Its x . r = b |r| is what the bound's
+    eq |x| term carries — the int8 estimate cannot see it — so a bound fed a row norm of 1 instead of |x| ~ b misses it
+    by ~eq (b - 1). Returns the row in float64."""
+    p1, p2, qsc, _, _, _, w1 = quantize_query(v, pieces)
+    approx = float(qsc) * (w1 * p1.astype(np.float64) + p2.astype(np.float64))
+    r = v.astype(np.float64) - approx
+    rh = r / np.linalg.norm(r)
+    qp = v.astype(np.float64) - (v.astype(np.float64) @ rh) * rh
+    w = qp / np.linalg.norm(qp)
+    beta = (target - b * (v.astype(np.float64) @ rh)) / (w @ v.astype(np.float64))
+    return b * rh + beta * w
+
+
+@pytest.mark.parametrize("pieces", [1, 2])
+def test_int8_bound_holds_on_residual_aligned_rows(pieces):
+    """Rows aligned with the query's residual (the case random rows hide behind Cauchy-Schwarz slack): the bound with
+    the rows' true norms holds at every scale; fed a norm of 1 (what bf16 + dot storage read before r6: its norms were
+    never computed) it falls below the exact score once |x| is a few units — the hole the r6 fix closes."""
+    rng = np.random.default_rng(42 + pieces)
+    d = 1024
+    v = rng.standard_normal(d).astype(F)
+    v /= np.linalg.norm(v)
+    bs = [1.0, 3.0, 10.0, 30.0, 100.0]
+    x = np.stack([residual_aligned_row(v, b, pieces=pieces) for b in bs]).astype(F)
+    if pieces == 1:
+        x = bf16_round(x)
+    xq, sx, e = quantize_rows(x)
+    nd = np.sqrt((x * x).sum(axis=1, dtype=F)).astype(F)
+    qv = quantize_query(v, pieces)
+    exact = x.astype(np.float64) @ v.astype(np.float64)
+    u = bound(xq, sx, e, nd, *qv).astype(np.float64)
+    assert np.all(u >= exact), (u - exact)
+    u1 = bound(xq, sx, e, np.ones_like(nd), *qv).astype(np.float64)
+    if pieces == 1:   # one piece: the residual is ~64x the two-piece one, so the unit-norm bound fails from b ~ 10
+        assert np.all(u1[2:] < exact[2:]), (u1 - exact)
