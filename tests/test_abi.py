@@ -96,12 +96,15 @@ def test_inline_asm_loads_are_hazard_free():
     pkg = _lib.PKG_ROOT
     sys.path.insert(0, os.path.join(os.path.dirname(pkg), "tools"))
     from check_asm_loads import check
-    for unit, pattern, least in (("rr_kernels", r"_ZN2rr18fused_score_kernel\w+", 16),
-                                 ("rr_sk", r"_ZN2rr2sk15sk_score_kernel\w+", 16)):
+    # (the split-K kernel's instantiations live in four units, rr_sk_fam_*.hip)
+    sk = r"_ZN2rr2sk15sk_score_kernel\w+"
+    for unit, pattern, least in (("rr_kernels", r"_ZN2rr18fused_score_kernel\w+", 16), ("rr_sk_fam_exact", sk, 16),
+                                 ("rr_sk_fam_s16", sk, 16), ("rr_sk_fam_s8", sk, 16), ("rr_sk_fam_s9", sk, 16)):
         # the library build keeps the assembly (Makefile: -save-temps=obj); rebuild it when it is older than the code
         s_file = os.path.join(pkg, "build", f"{unit}-hip-amdgcn-amd-amdhsa-gfx950.s")
         src = os.path.join(pkg, "csrc", f"{unit}.hip")
-        deps = [src, os.path.join(pkg, "csrc", "rr_device.h"), os.path.join(pkg, "csrc", "rr_internal.h")]
+        deps = [src, os.path.join(pkg, "csrc", "rr_device.h"), os.path.join(pkg, "csrc", "rr_internal.h"),
+                os.path.join(pkg, "csrc", "rr_sk_kernel.h")]
         if not os.path.exists(s_file) or os.path.getmtime(s_file) < max(map(os.path.getmtime, deps)):
             subprocess.check_call(["make", "-C", pkg, "-j4"], stdout=subprocess.DEVNULL)
         text = open(s_file).read()

@@ -5,6 +5,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I rag-serving-system_amd/csrc \
 //         tools/kbench.hip -o tools/kbench && tools/kbench [n_docs] [rounds]
 #include "../rag-serving-system_amd/csrc/rr_kernels.hip"
+#define RR_SK_ONE_UNIT   // (every split-K instantiation in this unit: rr_sk.hip includes rr_sk_fam_*.hip)
 #include "../rag-serving-system_amd/csrc/rr_sk.hip"
 
 #include <algorithm>

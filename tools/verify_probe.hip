@@ -3,6 +3,7 @@
 //         tools/verify_probe.hip -o tools/verify_probe && tools/verify_probe [n_docs] [int8=1]
 // int8 = 1: the verify of an int8 screen (DT 8 over the int8 copy, wide phase on) — the headline path; 0: the DT 6 screen.
 #include "../rag-serving-system_amd/csrc/rr_kernels.hip"
+#define RR_SK_ONE_UNIT   // (every split-K instantiation in this unit: rr_sk.hip includes rr_sk_fam_*.hip)
 #include "../rag-serving-system_amd/csrc/rr_sk.hip"
 
 #include <algorithm>
