@@ -112,7 +112,7 @@ _lib_lock = threading.Lock()
 def build(force: bool = False) -> str:
     """Compile librag_retrieval.so for gfx950 with hipcc (in-tree)."""
     if force or not os.path.exists(LIB_PATH):
-        subprocess.check_call(["make", "-C", PKG_ROOT, "-j4"])
+        subprocess.check_call(["make", "-C", PKG_ROOT, "-j8"])
     return LIB_PATH
 
 

@@ -106,7 +106,7 @@ def test_inline_asm_loads_are_hazard_free():
         deps = [src, os.path.join(pkg, "csrc", "rr_device.h"), os.path.join(pkg, "csrc", "rr_internal.h"),
                 os.path.join(pkg, "csrc", "rr_sk_kernel.h")]
         if not os.path.exists(s_file) or os.path.getmtime(s_file) < max(map(os.path.getmtime, deps)):
-            subprocess.check_call(["make", "-C", pkg, "-j4"], stdout=subprocess.DEVNULL)
+            subprocess.check_call(["make", "-C", pkg, "-j8"], stdout=subprocess.DEVNULL)
         text = open(s_file).read()
         syms = re.findall(rf"^({pattern}):", text, flags=re.M)
         assert len(syms) >= least, (unit, len(syms))
