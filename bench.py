@@ -53,6 +53,21 @@ def is_score_kernel(name: str) -> bool:
     return len(targs) >= 7 and targs[6].strip() == "0"
 
 
+def stream_priority_range():
+    """(least, greatest) stream priority of the HIP runtime (hipDeviceGetStreamPriorityRange): the library's search
+    streams take the greatest, its staging stream the least — separate hardware-queue pools when they differ from the
+    normal priority (0) RCCL's and torch's streams use."""
+    import ctypes
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        lo, hi = ctypes.c_int(), ctypes.c_int()
+        if hip.hipDeviceGetStreamPriorityRange(ctypes.byref(lo), ctypes.byref(hi)) != 0:
+            return None
+        return [lo.value, hi.value]
+    except OSError:
+        return None
+
+
 def host_cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -123,7 +138,34 @@ def algorithmic_bytes(rows: int, d: int, batch: int, dtype: str, metric: str, sc
     return rows * (d * elem + per_row) + batch * d * 4
 
 
-def timed_steps(ix, k, steps, warmup, dist, cuda_sync, every=1, acct=None):
+def make_stager(ix, q, nb: int, local: int, restage: bool):
+    """A step's queries: with `restage` (the default) every step stages a NEW batch of B queries already resident in HBM
+    (nb distinct batches in one device buffer, batch 0 = q; rr_set_queries_device — the copy into the library's query
+    buffer and the int8 screens' query pieces, on its staging stream), as a serving loop does per batch; without, the
+    batch staged once is searched again (round 5's loop). Returns (stage(i) or None, keep-alive)."""
+    if not restage:
+        return None, None
+    rng = np.random.default_rng(4242)
+    qs = rng.standard_normal((nb,) + q.shape).astype(np.float32)
+    qs /= np.linalg.norm(qs, axis=2, keepdims=True)
+    qs[0] = q
+    try:
+        import torch
+        dev = torch.from_numpy(qs).to(f"cuda:{local}")
+        torch.cuda.synchronize()
+        ptrs = [dev[i].data_ptr() for i in range(nb)]
+        b, d = q.shape
+
+        def stage(i):
+            ix.set_queries_device(ptrs[i % nb], b, d)
+        return stage, dev
+    except Exception:   # (no torch: the pinned host path, rr_set_queries)
+        def stage(i):
+            ix.set_queries(qs[i % nb])
+        return stage, qs
+
+
+def timed_steps(ix, k, steps, warmup, dist, cuda_sync, every=1, acct=None, stage=None):
     """W untimed warmup steps, then exactly K steps between barrier + device sync on both sides.
     HIP events bracket the similarity kernel of every `every`-th step (event markers cost GPU time
     between kernels; sampling keeps the duration measurement inside the timed region).
@@ -138,7 +180,9 @@ def timed_steps(ix, k, steps, warmup, dist, cuda_sync, every=1, acct=None):
     "wide_slots": W} (W: query slots the verify proved in its wide phase, no re-run needed).
     Returns (wall seconds, fused-kernel event ms summed, fused launches timed)."""
     from rag_service_amd.dist import barrier, sum_over_ranks
-    for _ in range(warmup):
+    for i in range(warmup):
+        if stage:
+            stage(i)
         ix.search_staged(k)
     ix.synchronize()
     b0, f0, r0, w0 = ix.screen_counts_all()
@@ -151,6 +195,8 @@ def timed_steps(ix, k, steps, warmup, dist, cuda_sync, every=1, acct=None):
     for i in range(steps):
         if every > 1:
             ix.set_timing(i % every == 0)
+        if stage:
+            stage(warmup + i)
         ix.search_staged(k)
     t_enq = time.perf_counter() - t0           # host time to enqueue the K steps (the device may still be running)
     b1, f1, r1, w1 = ix.screen_counts_all()    # synchronises (and settles the last search)
@@ -292,6 +338,9 @@ def main() -> None:
                          "third of it, at most 120 s) the library's waits on RCCL work; a miss ends the rank with a "
                          "JSON error line naming the rank and stage, and a non-zero exit status")
     ap.add_argument("--dry-run-stall-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--no-restage", action="store_true",
+                    help="search the batch staged once in every step (round 5's loop) instead of staging a new batch, "
+                         "resident in HBM, per step")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="a path setting of the measured handle (rr_set_option: screen_grid, verify_cus, x_slots, "
                          "x_host_wait_us, screen_i8_pieces, ...; results are the same under every value); repeatable")
@@ -376,11 +425,13 @@ def run(args, stage: dict) -> None:
     q = rng.standard_normal((args.batch, args.dim)).astype(np.float32)
     q /= np.linalg.norm(q, axis=1, keepdims=True)
 
-    # ---- throughput: queries resident in HBM, K back-to-back steps --------------------------------
+    # ---- throughput: queries resident in HBM, K back-to-back steps, each a new batch ---------------
     stage["stage"] = "timed steps"
     ix.set_queries(q)
+    stager, _keep = make_stager(ix, q, 16, local, not args.no_restage)
     acct = {}
-    elapsed, kern_ms, launches = timed_steps(ix, args.k, args.steps, args.warmup, dist, cuda_sync, every, acct)
+    elapsed, kern_ms, launches = timed_steps(ix, args.k, args.steps, args.warmup, dist, cuda_sync, every, acct,
+                                             stager)
     elapsed = max_over_ranks(dist, elapsed)
     stage["stage"] = "latency loops"
 
@@ -413,7 +464,7 @@ def run(args, stage: dict) -> None:
     # ---- steady state: the same staged loop again, long after the GPU left idle ---------------------
     stage["stage"] = "steady-state steps"
     st_acct = {}
-    st_el, st_ms, st_n = timed_steps(ix, args.k, args.steady_steps, 0, dist, cuda_sync, 10, st_acct)
+    st_el, st_ms, st_n = timed_steps(ix, args.k, args.steady_steps, 0, dist, cuda_sync, 10, st_acct, stager)
     st_el = max_over_ranks(dist, st_el)
     scr_blocks, scr_fallbacks = ix.screen_stats()
     stage["stage"] = "single-stream and exact-kernel loops"
@@ -446,7 +497,7 @@ def run(args, stage: dict) -> None:
         # the same screen kernel with one compute stream (every CU screening, nothing overlapping): its own launch
         # duration by HIP events on every launch, after the GPU has been busy for the loops above
         ix.compute_streams(1)
-        a_el, a_ms, a_n = timed_steps(ix, args.k, 40, 5, dist, cuda_sync, 1)
+        a_el, a_ms, a_n = timed_steps(ix, args.k, 40, 5, dist, cuda_sync, 1, None, stager)
         ix.compute_streams(2)
         a_kern = a_ms / max(a_n, 1) / 1e3
         alone = {"kernel_avg_us": round(a_kern * 1e6, 2), "frac": round(alg_bytes / a_kern / 1e9 / HBM_PEAK_GBS, 4),
@@ -480,7 +531,7 @@ def run(args, stage: dict) -> None:
         # reference streams (retriever.py:600), and it is what a flagged block's re-run and any corpus the screen
         # cannot prune cost
         ix.set_kernel("exact")
-        e_el, e_ms, e_n = timed_steps(ix, args.k, args.variant_steps, args.warmup, dist, cuda_sync, 10)
+        e_el, e_ms, e_n = timed_steps(ix, args.k, args.variant_steps, args.warmup, dist, cuda_sync, 10, None, stager)
         _, e_idx = ix.search(q, args.k)
         ix.set_kernel("auto")
         e_kern = e_ms / max(e_n, 1) / 1e3
@@ -501,8 +552,10 @@ def run(args, stage: dict) -> None:
             vx = Index(devices=[local], dtype=vd, metric=args.metric)
             vx.fill_synthetic(_lib.RR_SYNTH_UNIT_NORM, 1234, args.docs, args.dim)
             vx.set_queries(q)
+            v_stager, _vkeep = make_stager(vx, q, 16, local, not args.no_restage)
             v_acct = {}
-            v_el, v_ms, v_n = timed_steps(vx, args.k, args.variant_steps, args.warmup, dist, cuda_sync, 10, v_acct)
+            v_el, v_ms, v_n = timed_steps(vx, args.k, args.variant_steps, args.warmup, dist, cuda_sync, 10, v_acct,
+                                          v_stager)
             _, v_idx = vx.search(q, args.k)
             # bf16 storage screens its int8 copy (DT 9, verified by the bf16 pass's own arithmetic): the screen streams
             # that copy, so its bytes are the launch's algorithmic bytes; the screened steps overlap on two streams
@@ -560,6 +613,10 @@ def run(args, stage: dict) -> None:
             "p50_ms": round(p50, 4),
             "p99_ms": round(p99, 4),
             "latency_note": "host-inclusive per batch: H2D queries + pipeline + D2H results, synchronous",
+            "step_queries": ("every step stages a new batch resident in HBM (16 distinct unit-norm batches, "
+                             "rr_set_queries_device: the copy into the library's query buffer and the int8 screens' "
+                             "query pieces, on its staging stream)" if not args.no_restage else
+                             "the batch staged once, searched in every step"),
             "host_pipelined": {"value": round(args.batch * args.latency_steps / host_pipe_s, 2), "unit": "queries/s",
                                "batches": args.latency_steps, "in_flight": 2,
                                "note": "host numpy queries in, host results out: rr_search_async (pinned H2D + "
@@ -581,7 +638,8 @@ def run(args, stage: dict) -> None:
             "library_build": _lib.build_info(),
             "options": args.options,
             "rr_env": {k: v for k, v in sorted(os.environ.items()) if k.startswith("RR_")},
-            "stream_queues_distinct": len(set(queues)),
+            "stream_queues_distinct": len(set(v for v in queues if v)),
+            "stream_priority_range": stream_priority_range(),
             "rccl_ranks": rccl_ranks,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -669,7 +727,8 @@ def pmc_counters(args, kernel_s):
            sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "3", "--warmup", "1",
            "--latency-steps", "1", "--no-cpu-baseline", "--docs", str(args.docs), "--dim", str(args.dim),
            "--batch", str(args.batch), "--k", str(args.k), "--dtype", args.dtype, "--metric", args.metric,
-           "--variants", "", "--kernel", args.kernel] + [a for o in args.opt for a in ("--opt", o)]
+           "--variants", "", "--kernel", args.kernel] + [a for o in args.opt for a in ("--opt", o)] + \
+          (["--no-restage"] if args.no_restage else [])
     try:
         subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
         vals = {}

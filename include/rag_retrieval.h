@@ -318,9 +318,10 @@ const char* rr_build_info(void);
  * above. */
 int rr_set_timeout(rr_handle* h, int32_t ms);
 
-/* Diagnostic: the hardware (AQL) queue each of local shard `i`'s four streams dispatches to — out[0] compute
- * stream 0, out[1] compute stream 1, out[2] exchange lane 0, out[3] exchange lane 1 — as queue addresses (equal
- * addresses = one shared in-order queue). Shards on one device share one set of streams. Synchronises the handle. */
+/* Diagnostic: the hardware (AQL) queue each of local shard `i`'s five streams dispatches to — out[0] compute
+ * stream 0, out[1] compute stream 1, out[2] exchange lane 0, out[3] exchange lane 1, out[4] the staging stream (query
+ * copies and the int8 screens' query pieces, at the runtime's least priority) — as queue addresses (equal addresses =
+ * one shared in-order queue). Shards on one device share one set of streams. Synchronises the handle. */
 int rr_stream_queues(rr_handle* h, int i, uint64_t* out);
 
 /* ---- timing (benchmarks) ----------------------------------------------------------------------- */

@@ -57,6 +57,10 @@ int fail(int code, const char* fmt, ...) {
   } while (0)
 
 constexpr int kXSlots = 4;   // pipelined-exchange buffer sets (Shard::px_keys)
+// Staged query buffers (fp32 rows + the int8 screens' pieces), used in turn by consecutive batches: a batch is staged on
+// the staging stream while earlier batches are searched, and its buffer's previous readers (four batches back) are
+// long done — so the staging never sits in a compute stream's chain (r6; stage_queries)
+constexpr int kQBufs = 4;
 
 // Host-side cost of enqueueing (diagnostics: RR_HOST_PROF=1 prints per-call averages at rr_destroy): [0] whole
 // rr_search_staged, [1] the pipelined exchange's enqueue, [2] the ncclAllGather call alone, [3] the screened block's
@@ -86,39 +90,49 @@ struct Shard {
   int8_t* scr8 = nullptr;
   float* sx8 = nullptr;
   float* e8 = nullptr;
-  int8_t* q8[2] = {nullptr, nullptr};
-  float* q8s[2] = {nullptr, nullptr};
   float* norms = nullptr;                // [round_up(rows, 32) + 32] |row| (pad = 1)
   float* rscale = nullptr;               // [same] split-f16 row scale 2^-e (pad = 1)
-  float* qbuf[2] = {nullptr, nullptr};   // staged queries, double-buffered ([q_cap][d] fp32 each): a new
-                                         // batch is copied into one while verifies may still read the other
+  // staged queries, kQBufs buffers used in turn: [q_cap][d] fp32 each (a new batch is copied into one while searches
+  // read the others), and — on shards that hold an int8 copy — the int8 screens' pieces of the same rows, [2][q8c][d]
+  // (p1, p2) and their scalars [6][q8c] (rr_device.h q8_stage_row; q8c = round_up(q_cap, 64))
+  float* qbuf[kQBufs] = {};
+  int8_t* q8t[kQBufs] = {};
+  float* q8st[kQBufs] = {};
+  int q8c = 0;
   // Two compute streams (rr_set_compute_streams): screened blocks of parity 1 run on cstream2 (stream index 1),
   // so block i + 1's screen starts while block i's screen drains its last chunks and its verify runs. Other work
   // runs on `stream` (index 0). Ordering between the two, by events:
-  //   ev_q[t][i]  the last screened verify on stream i that read query buffer t: a new batch written into buffer t
-  //               on the other stream waits for it; the next verify on the other stream waits for the last one
+  //   ev_q[t][i]  the last screened verify on stream i that read query buffer t: the next staging into buffer t
+  //               (staging stream) waits for it; the next verify on the other stream waits for the last one
   //               (they write the same result rows; a pending async D2H of those rows re-records it);
-  //   ev_stage    the current batch's copy into its query buffer, on the stream of the first block after it: the
-  //               other stream's first block waits for it;
+  //   ev_stage[t] buffer t's staging (sstream, below): every stream's first reader of the batch follows it;
   //   ev_fork     `stream` -> cstream2 after other kinds of search; ev_join cstream2 -> `stream` before them.
   hipStream_t cstream2 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_stage = nullptr;
-  hipEvent_t ev_q[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_q[kQBufs][2] = {};
   // with an exchange step the block's keys-ready event (ev_keys) marks the same point of its stream: ev_q is then not
   // recorded, evq_alias points to that event instead (one marker packet fewer in the compute stream per block;
   // ev_keys[x] is re-recorded kXSlots blocks later, on the same stream — a later point, which only orders more)
-  hipEvent_t evq_alias[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  hipEvent_t evq_alias[kQBufs][2] = {};
   hipEvent_t evq(int t, int i) const { return evq_alias[t][i] ? evq_alias[t][i] : ev_q[t][i]; }
   // rr_screen_counts (a timed window's close) waits on a record at each stream's tail: a later hipStreamSynchronize or
   // hipDeviceSynchronize (torch.cuda.synchronize) returns at once when a stream's last command is a completed record,
   // but enqueues and awaits a marker of its own, 11-16 us per stream, when it is a kernel or a copy
   // (tools/api_cost.hip "sync_after_done")
-  hipEvent_t ev_tail[4] = {};
-  bool q_rd[2][2] = {{false, false}, {false, false}};   // ev_q[t][i] recorded, no writer of buffer t waited on it yet
+  hipEvent_t ev_tail[5] = {};
+  bool q_rd[kQBufs][2] = {};   // ev_q[t][i] recorded, no writer of buffer t waited on it yet
   bool fork_pending = false;   // ev_fork was recorded since cstream2 last waited on it
   bool c2_busy = false;        // cstream2 holds work `stream` has not joined
-  int stage_si = 0;            // stream index that staged the current batch
-  bool stage_pending = false;  // ... and the other stream has not waited on ev_stage yet
+  // Staging (r6): a batch's copy into query buffer t and the int8 screens' pieces of it (ONE fused kernel from a device
+  // source) are made once per batch — not per search block, as the r5 prep kernel was — on the compute stream of the
+  // next block (stage_stream 0, the default), or on a staging stream of their own (options 1-3: measured slower, every
+  // block then follows a cross-stream event). stage_seen[t][i]: compute stream i is ordered after buffer t's
+  // latest staging (the other stream follows ev_stage[t]); ns_rd[t]: a search other than a screened block read buffer t
+  // on `stream` since its staging (a staging stream's next staging into t waits on ev_fork, recorded after each).
+  hipStream_t sstream = nullptr;
+  hipEvent_t ev_stage[kQBufs] = {};
+  bool stage_seen[kQBufs][2] = {};
+  bool ns_rd[kQBufs] = {};
   int last_vsi = -1, last_vq = 0;   // the last screened verify: its stream index and query buffer
   int q_cap = 0;
   uint64_t* cand = nullptr;              // 2 x [grid][64][32] per-workgroup candidates (the screened search
@@ -265,6 +279,8 @@ struct rr_handle {
                                 // a slower all-gather, for measurements and the deadline tests)
   int x_host_wait_us = 500;     // exchange issue thread: host wait for a px slot's previous exchange (x_host_wait_us)
   int x_thread = 1;             // multi-process mode: the exchange issue thread (x_thread; read at rr_init_dist)
+  int stage_mode = 0;           // where batches are staged (stage_stream): 0 = the next block's compute stream, 1 / 2 / 3 =
+                                // a staging stream at normal / greatest / least priority (measured slower: DESIGN §0)
   int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy); bf16: the int8 one
   int screen_i8 = 1;            // ... and an int8 copy, screened first (rr_screen_int8; RR_SCREEN_I8=0 at creation: off)
   int ct8 = 0;                  // the int8 screen's tiles per chunk (0: by shard size; screen_ct8)
@@ -350,6 +366,7 @@ const char* stream_role(const Shard& s, hipStream_t st) {
   if (st == s.cstream2) return "compute stream 1";
   if (st == s.xstream) return "exchange lane 0";
   if (st == s.xstream2) return "exchange lane 1";
+  if (st == s.sstream) return "the staging stream";
   return "a work stream";
 }
 // "shard i (device d), <stream>: <what>" (the rank instead of the shard index in multi-process mode)
@@ -441,7 +458,10 @@ int dmalloc(T** p, size_t bytes) {
 
 int free_shard(Shard& s) {
   hipSetDevice(s.dev);
-  void* ptrs[] = {s.corpus, s.scr16, s.scr8, s.sx8, s.e8, s.q8[0], s.q8[1], s.q8s[0], s.q8s[1], s.norms, s.rscale, s.qbuf[0], s.qbuf[1], s.cand, s.scount, s.ctr, s.shard_keys, s.gathered, s.out_base,
+  for (int t = 0; t < kQBufs; ++t)
+    for (void* p : {(void*)s.qbuf[t], (void*)s.q8t[t], (void*)s.q8st[t]})
+      if (p) hipFree(p);
+  void* ptrs[] = {s.corpus, s.scr16, s.scr8, s.sx8, s.e8, s.norms, s.rscale, s.cand, s.scount, s.ctr, s.shard_keys, s.gathered, s.out_base,
                   s.full_keys, s.sort_temp, s.wcand, s.wfloor, s.wsel, s.rcmax[0], s.rcmax[1], s.rbits[0], s.rbits[1],
                   s.rlist[0], s.rlist[1], s.rcnt[0], s.rcnt[1]};
   for (void* p : ptrs)
@@ -460,27 +480,26 @@ int free_shard(Shard& s) {
   if (s.copies_done) hipEventDestroy(s.copies_done);
   if (s.ev_cdone) hipEventDestroy(s.ev_cdone);
   if (s.ev_rcopy) hipEventDestroy(s.ev_rcopy);
-  for (hipEvent_t e : {s.ev_fork, s.ev_join, s.ev_stage, s.ev_q[0][0], s.ev_q[0][1], s.ev_q[1][0], s.ev_q[1][1],
-                       s.ev_tail[0], s.ev_tail[1], s.ev_tail[2], s.ev_tail[3]})
+  for (hipEvent_t e : {s.ev_fork, s.ev_join, s.ev_tail[0], s.ev_tail[1], s.ev_tail[2], s.ev_tail[3], s.ev_tail[4]})
     if (e) hipEventDestroy(e);
+  for (int t = 0; t < kQBufs; ++t)
+    for (hipEvent_t e : {s.ev_stage[t], s.ev_q[t][0], s.ev_q[t][1]})
+      if (e) hipEventDestroy(e);
   if (s.comm2) ncclCommDestroy(s.comm2);
   if (s.comm) ncclCommDestroy(s.comm);
   if (s.own_streams)
-    for (hipStream_t st : {s.xstream, s.xstream2, s.cstream2, s.stream})
+    for (hipStream_t st : {s.sstream, s.xstream, s.xstream2, s.cstream2, s.stream})
       if (st) hipStreamDestroy(st);
   s = Shard();
   return RR_OK;
 }
 
-// Release the shard's int8 screen copy and its query buffers (current device = s.dev).
+// Release the shard's int8 screen copy (current device = s.dev; the staged query pieces go with the work buffers).
 void free_i8(Shard& s) {
-  for (void* p : {(void*)s.scr8, (void*)s.sx8, (void*)s.e8, (void*)s.q8[0], (void*)s.q8[1], (void*)s.q8s[0],
-                  (void*)s.q8s[1]})
+  for (void* p : {(void*)s.scr8, (void*)s.sx8, (void*)s.e8})
     if (p) hipFree(p);
   s.scr8 = nullptr;
   s.sx8 = s.e8 = nullptr;
-  s.q8[0] = s.q8[1] = nullptr;
-  s.q8s[0] = s.q8s[1] = nullptr;
 }
 
 // Allocate the shard's corpus storage for the current range (and norms when cosine).
@@ -513,11 +532,6 @@ int alloc_corpus(rr_handle* h, Shard& s) {
       bool ok = hipMalloc((void**)&s.scr8, (size_t)r2 * h->d) == hipSuccess;
       ok = ok && hipMalloc((void**)&s.sx8, (size_t)r2 * 4) == hipSuccess;
       ok = ok && hipMalloc((void**)&s.e8, (size_t)r2 * 4) == hipSuccess;
-      for (int i = 0; i < 2 && ok; ++i) {
-        // (two pieces x 32 slots, or DT 9's one piece x 64; scalars [4][64] at most)
-        ok = hipMalloc((void**)&s.q8[i], (size_t)2 * rr::kQSlots * h->d) == hipSuccess;
-        ok = ok && hipMalloc((void**)&s.q8s[i], (size_t)4 * kMaxSlots * 4) == hipSuccess;
-      }
       // the padding row (odd row counts) is read as the second half of the last kernel row: zeros, scale 0
       if (ok && r2 > rows) {
         ok = hipMemset(s.scr8 + (size_t)rows * h->d, 0, h->d) == hipSuccess;
@@ -744,13 +758,23 @@ int check_shape(const rr_handle* h, int64_t n, int32_t d) {
 int drop_work_buffers(rr_handle* h) {
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
-    for (hipStream_t st : {s.stream, s.xstream, s.xstream2, s.cstream2})
-      if (int rc = wait_stream(h, s, st)) return rc;
-    s.c2_busy = s.fork_pending = s.stage_pending = s.rcopy_pending = false;
+    for (hipStream_t st : {s.stream, s.xstream, s.xstream2, s.cstream2, s.sstream})
+      if (st)
+        if (int rc = wait_stream(h, s, st)) return rc;
+    s.c2_busy = s.fork_pending = s.rcopy_pending = false;
     s.last_x = -1;
-    s.q_rd[0][0] = s.q_rd[0][1] = s.q_rd[1][0] = s.q_rd[1][1] = false;
+    for (int t = 0; t < kQBufs; ++t) {
+      s.q_rd[t][0] = s.q_rd[t][1] = false;
+      s.stage_seen[t][0] = s.stage_seen[t][1] = true;   // (nothing staged: nothing to follow)
+      s.ns_rd[t] = false;
+      for (void** p : {(void**)&s.qbuf[t], (void**)&s.q8t[t], (void**)&s.q8st[t]}) {
+        if (*p) HIP_TRY(hipFree(*p));
+        *p = nullptr;
+      }
+    }
+    s.q8c = 0;
     s.last_vsi = -1;
-    void** ptrs[] = {(void**)&s.qbuf[0], (void**)&s.qbuf[1], (void**)&s.cand, (void**)&s.scount, (void**)&s.ctr, (void**)&s.shard_keys, (void**)&s.gathered,
+    void** ptrs[] = {(void**)&s.cand, (void**)&s.scount, (void**)&s.ctr, (void**)&s.shard_keys, (void**)&s.gathered,
                      (void**)&s.out_base, (void**)&s.full_keys, &s.sort_temp,
                      (void**)&s.wcand, (void**)&s.wfloor, (void**)&s.wsel, (void**)&s.rcmax[0], (void**)&s.rcmax[1],
                      (void**)&s.rbits[0], (void**)&s.rbits[1], (void**)&s.rlist[0], (void**)&s.rlist[1],
@@ -819,11 +843,19 @@ int ensure_buffers(rr_handle* h, int b, int k) {
     if (b > s.q_cap || k > s.k_cap) {
       const int qc = std::max(b, s.q_cap), kc = std::max(k, s.k_cap);
       if (b > s.q_cap) {
-        const size_t qb = (size_t)((qc + kMaxSlots - 1) / kMaxSlots * kMaxSlots) * h->d * 4;
-        for (int i = 0; i < 2; ++i) {
+        const int rows = (qc + kMaxSlots - 1) / kMaxSlots * kMaxSlots;
+        const size_t qb = (size_t)rows * h->d * 4;
+        for (int i = 0; i < kQBufs; ++i) {
           if (int rc = dmalloc(&s.qbuf[i], qb)) return rc;
           HIP_TRY(hipMemset(s.qbuf[i], 0, qb));
+          // the int8 screens' pieces of the staged rows (shards with an int8 copy): p1, p2 [rows][d] + 6 scalars per row
+          if (s.scr8) {
+            if (int rc = dmalloc(&s.q8t[i], (size_t)2 * rows * h->d)) return rc;
+            if (int rc = dmalloc(&s.q8st[i], (size_t)rr::kQ8Scalars * rows * 4)) return rc;
+          }
         }
+        s.q8c = s.scr8 ? rows : 0;
+        for (int t = 0; t < kQBufs; ++t) s.stage_seen[t][0] = s.stage_seen[t][1] = true;   // (fresh buffers)
       }
       // scores and indices in one allocation, so a search's results come back in ONE D2H copy. The last search's
       // results (and flag word) move to the new allocation: rr_fetch_results after staging a larger batch still
@@ -1092,9 +1124,10 @@ int join_main(Shard& s) {
   HIP_TRY(hipEventRecord(s.ev_join, s.cstream2));
   HIP_TRY(wait_ev(s.stream, s.ev_join));
   s.c2_busy = false;
+  for (int t = 0; t < kQBufs; ++t) s.stage_seen[t][0] = s.stage_seen[t][0] || s.stage_seen[t][1];
   return RR_OK;
 }
-// Work just enqueued on `stream` (staged queries, another kind of search) that the next cstream2 block follows.
+// Work just enqueued on `stream` (another kind of search) that the next cstream2 block follows.
 int fork_point(Shard& s) {
   HIP_TRY(hipEventRecord(s.ev_fork, s.stream));
   s.fork_pending = true;
@@ -1107,36 +1140,64 @@ int fork_all(rr_handle* h) {
   }
   return RR_OK;
 }
+// cstream2 follows `stream`'s last fork point (current device = s.dev)
+int follow_fork(Shard& s) {
+  if (!s.fork_pending) return RR_OK;
+  HIP_TRY(wait_ev(s.cstream2, s.ev_fork));
+  s.fork_pending = false;
+  for (int t = 0; t < kQBufs; ++t) s.stage_seen[t][1] = s.stage_seen[t][1] || s.stage_seen[t][0];
+  return RR_OK;
+}
+// Compute stream si follows the staging of query buffer t (the copy and the int8 pieces, on the staging stream) before
+// its first kernel that reads them: one barrier packet per stream and staging, already satisfied when the staging ran
+// beside earlier searches.
+hipError_t follow_stage(Shard& s, int t, int si) {
+  if (s.stage_seen[t][si]) return hipSuccess;
+  s.stage_seen[t][si] = true;
+  return wait_ev(stream_of(s, si), s.ev_stage[t]);
+}
 
-// Copy a batch of queries into every shard's query buffer t, on the stream of the next screened block: from pinned
-// host memory (src_dev < 0) or device memory on src_dev. pin_ev: record each shard's pin_q_free after its copy.
-int stage_queries(rr_handle* h, int t, const void* src, size_t bytes, int src_dev, bool pin_ev) {
+// Stage a batch of queries into every shard's query buffer t, on the staging stream: from pinned host memory (src_dev <
+// 0) or device memory on src_dev; then (shards with an int8 copy) the int8 screens' pieces of the batch — the device copy
+// fused into the same kernel when the source is on the shard's own device. The buffer's previous readers (kQBufs
+// batches back: screened verifies on either compute stream, other kinds of search on `stream`) are waited for on the
+// staging stream. pin_ev: record each shard's pin_q_free after its copy.
+int stage_queries(rr_handle* h, int t, const void* src, int b, int src_dev, bool pin_ev) {
+  const size_t bytes = (size_t)b * h->d * 4;
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
-    const bool two = two_streams(h, s);
-    const int x = block_si(h, s, h->parity);
-    const hipStream_t xs = stream_of(s, x);
-    if (two) {
-      if (s.q_rd[t][x ^ 1]) HIP_TRY(wait_ev(xs, s.evq(t, x ^ 1)));   // its last readers there
-      s.q_rd[t][x ^ 1] = false;
-      if (x == 1) {   // after other kinds of search on `stream` (they read query buffers too)
-        if (s.fork_pending) HIP_TRY(wait_ev(xs, s.ev_fork));
-        s.fork_pending = false;
-        s.c2_busy = true;
-      }
+    // where: the staging stream, or (stage_stream 0) the compute stream of the next block, in its chain
+    const int x = h->stage_mode == 0 ? block_si(h, s, h->parity) : -1;
+    const hipStream_t ss = x >= 0 ? stream_of(s, x) : s.sstream;
+    if (x == 1) {   // cstream2 after other kinds of search on `stream` (they read query buffers too)
+      if (int rc = follow_fork(s)) return rc;
+      s.c2_busy = true;
     }
-    if (src_dev < 0)
-      HIP_TRY(hipMemcpyAsync(s.qbuf[t], src, bytes, hipMemcpyHostToDevice, xs));
-    else if (s.dev == src_dev)
-      HIP_TRY(hipMemcpyAsync(s.qbuf[t], src, bytes, hipMemcpyDeviceToDevice, xs));
-    else
-      HIP_TRY(hipMemcpyPeerAsync(s.qbuf[t], s.dev, src, src_dev, bytes, xs));
-    if (pin_ev) HIP_TRY(hipEventRecord(s.pin_q_free, xs));
-    if (two) {
-      HIP_TRY(hipEventRecord(s.ev_stage, xs));
-      s.stage_si = x;
-      s.stage_pending = true;
+    for (int i = 0; i < 2; ++i) {
+      if (s.q_rd[t][i] && i != x) HIP_TRY(wait_ev(ss, s.evq(t, i)));
+      s.q_rd[t][i] = false;
     }
+    if (s.ns_rd[t] && x < 0) HIP_TRY(wait_ev(ss, s.ev_fork));   // (recorded after every such search)
+    s.ns_rd[t] = false;
+    const bool pieces = s.q8t[t] && s.scr8 && s.rows() > 0;
+    if (src_dev < 0) {
+      HIP_TRY(hipMemcpyAsync(s.qbuf[t], src, bytes, hipMemcpyHostToDevice, ss));
+    } else if (s.dev == src_dev) {
+      if (!pieces) HIP_TRY(hipMemcpyAsync(s.qbuf[t], src, bytes, hipMemcpyDeviceToDevice, ss));
+    } else {
+      HIP_TRY(hipMemcpyPeerAsync(s.qbuf[t], s.dev, src, src_dev, bytes, ss));
+    }
+    if (pin_ev) HIP_TRY(hipEventRecord(s.pin_q_free, ss));
+    if (pieces) {   // (from the caller's device buffer directly, copying it on the way, when it is on this device)
+      const bool fused = src_dev >= 0 && s.dev == src_dev;
+      rr::set_launch_events(nullptr, s.ev_stage[t]);   // (ev_stage on the launch packet: no separate record)
+      HIP_TRY(rr::launch_q8_stage(fused ? (const float*)src : s.qbuf[t], b, h->d, s.q8t[t], s.q8c, s.q8st[t],
+                                  fused ? s.qbuf[t] : nullptr, ss));
+    } else {
+      HIP_TRY(hipEventRecord(s.ev_stage[t], ss));
+    }
+    s.stage_seen[t][0] = s.stage_seen[t][1] = false;
+    if (x >= 0) s.stage_seen[t][x] = true;
   }
   return RR_OK;
 }
@@ -1472,15 +1533,11 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       const bool two = two_streams(h, s);
       const int bsi = block_si(h, s, p), t = h->qpar;
       const hipStream_t cs = stream_of(s, bsi), vs = cs;
-      if (two) {
-        if (s.stage_pending && bsi != s.stage_si) HIP_TRY(wait_ev(cs, s.ev_stage));
-        if (bsi != s.stage_si) s.stage_pending = false;
-        if (bsi == 1) {
-          if (s.fork_pending) HIP_TRY(wait_ev(cs, s.ev_fork));
-          s.fork_pending = false;
-          s.c2_busy = true;
-        }
+      if (two && bsi == 1) {   // after other kinds of search on `stream`
+        if (int rc = follow_fork(s)) return rc;
+        s.c2_busy = true;
       }
+      HIP_TRY(follow_stage(s, t, bsi));   // the batch's rows and int8 pieces (staging stream)
       if (multi) {
         // px_keys[x]'s last reader is the exchange of the block kXSlots back. A stream wait on it is a barrier packet in
         // this compute stream's chain (prep, screen, verify): ~10-16 us of device latency per block even when the
@@ -1543,20 +1600,14 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         a.eps_a = s16 ? kScreen16EpsA : kScreenEpsA;
         a.eps_b = s16 ? kScreen16EpsB : kScreenEpsB;
         if (s16) a.corpus = (const char*)s.scr16;
-        if (s8) {   // the queries' int8 pieces on this stream first (the previous block's screen here is done with them)
-          const int64_t tq = h->host_prof ? now_ns() : 0;
-          if (timed) rr::set_launch_events(e0, nullptr);
-          HIP_TRY(one_piece ? rr::launch_q8_prep(qb, bb, d, s.q8[bsi], s.q8s[bsi], cs, 1, slots)
-                     : rr::launch_q8_prep(qb, bb, d, s.q8[bsi], s.q8s[bsi], cs));
-          if (h->host_prof) {
-            h->hp.ns[8] += now_ns() - tq;
-            ++h->hp.n[8];
-          }
+        if (s8) {   // the queries' int8 pieces: made when the batch was staged (stage_queries), rows q0 .. q0 + slots
           a.corpus = (const char*)s.scr8;
           a.n = (s.rows() + 1) / 2;
           a.rows8 = s.rows();
-          a.q8 = s.q8[bsi];
-          a.q8s = s.q8s[bsi];
+          a.q8 = s.q8t[t] + (size_t)q0 * d;
+          a.q8p2 = s.q8t[t] + ((size_t)s.q8c + q0) * d;
+          a.q8s = s.q8st[t] + q0;
+          a.q8s_stride = s.q8c;
           a.sx8 = s.sx8;
           a.e8 = s.e8;
           a.ct8 = ct8;
@@ -1564,7 +1615,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
           a.eps_b = kScreen8EpsB;
         }
         const int64_t tsc = h->host_prof ? now_ns() : 0;
-        if (timed) rr::set_launch_events(s8 ? nullptr : e0, e1);
+        if (timed) rr::set_launch_events(e0, e1);
         HIP_TRY(rr::launch_sk_args(sdt, h->metric, kt, 0, sgrid, slots, a, cs));
         if (h->host_prof) {
           h->hp.ns[9] += now_ns() - tsc;
@@ -1645,6 +1696,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
     } else if (kt) {
       int grid = fused_grid(s);
       HIP_TRY(wait_px(-1, s.stream));   // no screened verify still reads cand or writes the results
+      HIP_TRY(follow_stage(s, h->qpar, 0));
+      s.ns_rd[h->qpar] = true;
       const bool ev_packet = s.rows() > 0 && use_sk(h);   // (timed: events on the launch packet, as above)
       if (timed && !ev_packet) HIP_TRY(hipEventRecord(e0, s.stream));
       if (s.rows() > 0) {
@@ -1676,6 +1729,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       // floors: unproven -> the block's flag word (the host re-runs the search with the full sort).
       HIP_TRY(wait_px(-1, s.stream));
       HIP_TRY(wait_copies());
+      HIP_TRY(follow_stage(s, h->qpar, 0));
+      s.ns_rd[h->qpar] = true;
       if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
       uint64_t* flagw = multi ? s.shard_keys + (size_t)rr::kQSlots * k : (uint64_t*)s.out_base;
       // the exchanged flag word sits after this k's keys: clear it (earlier searches with a larger k left keys
@@ -1742,6 +1797,8 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
       HIP_TRY(wait_px(-1, s.stream));   // no pipelined exchange or screened verify still uses the buffers
       HIP_TRY(wait_copies());
+      HIP_TRY(follow_stage(s, h->qpar, 0));
+      s.ns_rd[h->qpar] = true;
       HIP_TRY(hipMemsetAsync(s.shard_keys, 0, (size_t)rr::kQSlots * k * 8, s.stream));
       if (rows > 0) {
         if (use_sk(h)) {   // the split-K kernel's arithmetic, as every other path of this handle
@@ -1853,7 +1910,7 @@ int enqueue_block(rr_handle* h, int q0, int bb, int k, int slots) {
 // only while its buffer is intact, so it is settled first when its buffer is the one about to be rewritten
 // (two batches staged, no search).
 int begin_stage(rr_handle* h, int* nq) {
-  const int t = h->qpar ^ 1;
+  const int t = (h->qpar + 1) % kQBufs;
   if (h->last_screened && !h->last_settled && h->last_qpar == t)
     if (int rc = rr_synchronize(h)) return rc;
 
@@ -1865,6 +1922,27 @@ int begin_stage(rr_handle* h, int* nq) {
 // Every option picks HOW a search runs — grid sizes, list widths, query pieces, the exchange's buffering — never its
 // results: each path is exact by construction and the GPU tests check them against the exact kernel. Defaults are the
 // measured best; the options exist for measurements and for tests that reach a path on small inputs.
+// (Re)create every device's staging stream at the priority of stage_stream mode (1 normal, 2 greatest, 3 least).
+int make_stage_streams(rr_handle* h, int mode) {
+  int least = 0, greatest = 0;
+  HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  const int prio = mode == 2 ? greatest : mode == 3 ? least : 0;
+  for (Shard& s : h->shards) {
+    if (!s.own_streams) continue;
+    HIP_TRY(hipSetDevice(s.dev));
+    if (s.sstream) HIP_TRY(hipStreamDestroy(s.sstream));
+    s.sstream = nullptr;
+    HIP_TRY(hipStreamCreateWithPriority(&s.sstream, hipStreamNonBlocking, prio));
+  }
+  for (Shard& s : h->shards)   // shards on one device share the first one's
+    for (const Shard& o : h->shards)
+      if (o.own_streams && o.dev == s.dev) {
+        s.sstream = o.sstream;
+        break;
+      }
+  return RR_OK;
+}
+
 struct OptionDesc {
   const char* name;
   int64_t lo, hi;
@@ -1883,6 +1961,8 @@ const OptionDesc kOptions[] = {
     {"screen_guided", 0, 1},            // 2-tile chunks at the end of a screen launch
     {"screen_full_lists", 0, 1},        // repair mode from the start (and from every load on)
     {"screen_i8_min_rows", 0, INT64_MAX / 2},   // the int8 copy for shards of at least this many rows (next load)
+    {"stage_stream", 0, 3},             // batches staged on: 0 the next block's compute stream, 1 / 2 / 3 the staging
+                                        // stream at normal / greatest / least priority
 };
 
 int64_t* option_field64(rr_handle* h, const std::string& n) { return n == "screen_i8_min_rows" ? &h->i8_min_rows : nullptr; }
@@ -1897,6 +1977,7 @@ int* option_field(rr_handle* h, const std::string& n) {
   if (n == "screen_ct8") return &h->ct8;
   if (n == "screen_i8_pieces") return &h->i8_pieces;
   if (n == "screen_guided") return &h->guided;
+  if (n == "stage_stream") return &h->stage_mode;
   return nullptr;
 }
 int set_option(rr_handle* h, const OptionDesc& o, int64_t v) {
@@ -1910,6 +1991,9 @@ int set_option(rr_handle* h, const OptionDesc& o, int64_t v) {
     h->full_lists = v != 0;
     h->win_nb = h->win_nf = 0;
     return RR_OK;
+  }
+  if (n == "stage_stream" && v != h->stage_mode && v > 0) {   // (the caller synchronised: the stream is idle)
+    if (int rc = make_stage_streams(h, (int)v)) return rc;
   }
   if (int64_t* f = option_field64(h, n)) *f = v;
   else *option_field(h, n) = (int)v;
@@ -1981,13 +2065,15 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
       s.cstream2 = owner->cstream2;
       s.xstream = owner->xstream;
       s.xstream2 = owner->xstream2;
+      s.sstream = owner->sstream;
     } else {
       int least = 0, greatest = 0;
-      if (e == hipSuccess && h->stream_prio) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+      if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
       const int prio = h->stream_prio ? greatest : least;
       // creation order = the order the hardware queues are handed out in (least used first)
       for (hipStream_t* st : {&s.stream, &s.xstream, &s.xstream2, &s.cstream2})
         if (e == hipSuccess) e = hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio);
+      // (no staging stream by default: stage_stream 0 stages on the compute streams; rr_set_option makes one)
     }
     if (e != hipSuccess) {
       for (int j = i + 1; j < n_dev; ++j) h->shards[j].own_streams = false;
@@ -2003,9 +2089,12 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
       e = hipEventCreateWithFlags(&s.ev_keys[x], hipEventDisableTiming);
       if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev_xdone[x], hipEventDisableTiming);
     }
-    for (hipEvent_t* ev : {&s.ev_cdone, &s.ev_rcopy, &s.ev_fork, &s.ev_join, &s.ev_stage, &s.ev_q[0][0], &s.ev_q[0][1],
-                           &s.ev_q[1][0], &s.ev_q[1][1], &s.ev_tail[0], &s.ev_tail[1], &s.ev_tail[2], &s.ev_tail[3]})
+    for (hipEvent_t* ev : {&s.ev_cdone, &s.ev_rcopy, &s.ev_fork, &s.ev_join, &s.ev_tail[0], &s.ev_tail[1], &s.ev_tail[2],
+                           &s.ev_tail[3], &s.ev_tail[4]})
       if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    for (int t = 0; t < kQBufs; ++t)
+      for (hipEvent_t* ev : {&s.ev_stage[t], &s.ev_q[t][0], &s.ev_q[t][1]})
+        if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e != hipSuccess) {
       rr_destroy(h);
       return fail(RR_E_HIP, "event setup failed: %s", hipGetErrorString(e));
@@ -2352,7 +2441,7 @@ int rr_set_queries(rr_handle* h, const float* host_q, int32_t b, int32_t d) {
   memcpy(h->pin_q, host_q, qbytes);
   int nq = 0;
   if (int rc = begin_stage(h, &nq)) return rc;
-  if (int rc = stage_queries(h, nq, h->pin_q, qbytes, -1, true)) return rc;
+  if (int rc = stage_queries(h, nq, h->pin_q, b, -1, true)) return rc;
   h->qpar = nq;
   h->cur_b = b;
   return RR_OK;
@@ -2368,7 +2457,7 @@ int rr_set_queries_device(rr_handle* h, const float* dev_q, int32_t b, int32_t d
   const int src_dev = h->shards[0].dev;
   int nq = 0;
   if (int rc = begin_stage(h, &nq)) return rc;
-  if (int rc = stage_queries(h, nq, dev_q, (size_t)b * d * 4, src_dev, false)) return rc;
+  if (int rc = stage_queries(h, nq, dev_q, b, src_dev, false)) return rc;
   h->qpar = nq;
   h->cur_b = b;
   return RR_OK;
@@ -2432,8 +2521,9 @@ namespace {
 int sync_streams(rr_handle* h) {
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
-    for (hipStream_t st : {s.stream, s.xstream, s.xstream2, s.cstream2})
-      if (int rc = wait_stream(h, s, st)) return rc;
+    for (hipStream_t st : {s.stream, s.xstream, s.xstream2, s.cstream2, s.sstream})
+      if (st)
+        if (int rc = wait_stream(h, s, st)) return rc;
     s.c2_busy = false;
     s.rcopy_pending = false;
   }
@@ -2458,12 +2548,13 @@ int sync_streams_tail(rr_handle* h, bool flag) {
     if (int rc = xw_drain(h)) return rc;
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
-    const hipStream_t others[3] = {s.xstream, s.xstream2, s.cstream2};
-    for (int i = 1; i < 4; ++i) HIP_TRY(hipEventRecord(s.ev_tail[i], others[i - 1]));
+    const hipStream_t others[4] = {s.xstream, s.xstream2, s.cstream2, s.sstream};
+    for (int i = 1; i < 5; ++i)
+      if (others[i - 1]) HIP_TRY(hipEventRecord(s.ev_tail[i], others[i - 1]));
   }
   for (Shard& s : h->shards) {
     HIP_TRY(hipSetDevice(s.dev));
-    for (int i = 1; i < 4; ++i)
+    for (int i = 1; i < (s.sstream ? 5 : 4); ++i)
       if (int rc = wait_event(h, s, s.ev_tail[i], "device work (stream tails)")) return rc;
     HIP_TRY(queue_count_copies(h, s, flag));
     HIP_TRY(hipEventRecord(s.ev_tail[0], s.stream));
@@ -2605,7 +2696,7 @@ int rr_search_async(rr_handle* h, const float* host_q, int32_t b, int32_t d, int
   memcpy(a.pin, host_q, qbytes);
   int nq = 0;
   if (int rc = begin_stage(h, &nq)) return rc;
-  if (int rc = stage_queries(h, nq, a.pin, qbytes, -1, false)) return rc;
+  if (int rc = stage_queries(h, nq, a.pin, b, -1, false)) return rc;
   h->qpar = nq;
   h->cur_b = b;
   if (int rc = rr_search_staged(h, k)) return rc;
@@ -2681,7 +2772,7 @@ int rr_wait(rr_handle* h, int32_t ticket, float* out_scores, int64_t* out_idx) {
     const int saved_qpar = h->qpar, saved_b = h->cur_b;
     int nq = 0;
     if (int rc = begin_stage(h, &nq)) return rc;
-    if (int rc = stage_queries(h, nq, a.pin, qbytes, -1, false)) return rc;
+    if (int rc = stage_queries(h, nq, a.pin, a.b, -1, false)) return rc;
     h->qpar = nq;
     h->cur_b = a.b;
     const int saved = h->kernel;
@@ -2766,13 +2857,16 @@ int rr_stream_queues(rr_handle* h, int i, uint64_t* out) {
   Shard& s = h->shards[i];
   HIP_TRY(hipSetDevice(s.dev));
   uint64_t* dq = nullptr;
-  HIP_TRY(hipMalloc((void**)&dq, 4 * sizeof(uint64_t)));
-  const hipStream_t st[4] = {s.stream, s.cstream2, s.xstream, s.xstream2};
+  HIP_TRY(hipMalloc((void**)&dq, 5 * sizeof(uint64_t)));
+  const hipStream_t st[5] = {s.stream, s.cstream2, s.xstream, s.xstream2, s.sstream};
   hipError_t e = hipSuccess;
-  for (int j = 0; j < 4 && e == hipSuccess; ++j) e = rr::launch_queue_probe(dq + j, st[j]);
+  for (int j = 0; j < 5 && e == hipSuccess; ++j)
+    if (st[j]) e = rr::launch_queue_probe(dq + j, st[j]);
   int rc = RR_OK;
   if (e == hipSuccess) rc = sync_streams(h);
-  if (e == hipSuccess && rc == RR_OK) e = hipMemcpy(out, dq, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && rc == RR_OK) e = hipMemcpy(out, dq, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost);
+  for (int j = 0; j < 5; ++j)
+    if (!st[j]) out[j] = 0;   // (no staging stream: stage_stream 0)
   if (!h->failed) hipFree(dq);
   if (rc) return rc;
   if (e != hipSuccess) return fail(RR_E_HIP, "queue probe failed: %s", hipGetErrorString(e));

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <type_traits>
+#include "rr_internal.h"
 
 namespace rr {
 
@@ -135,31 +136,33 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// The int8 screen's query pieces, one wave per query slot: s = max|q| / 127, t = q / s, p1 = clamp(rint(t)), p2 =
-// clamp(rint((t - p1) * 64)) — q ~ s (p1 + p2 / 64), the MFMAs' sum being x8 . (64 p1 + p2) — and eq >= the
-// residual's norm (real arithmetic), in the scale's units as f32_to_i8_kernel: t - p1 - p2 / 64 is exact (each step
-// by Sterbenz), so |q - s (p1 + p2 / 64)|_2 <= s |t - p1 - p2/64|_2 (x 1 + 2^-12) + 2^-21 sqrt(d) max|q| + 2^-140.
-// |q| and sum|q| in fp32 (the bound bumps for their summation order). One wave (64 lanes) per query slot `slot`;
-// slots >= b get zero pieces and scalars. Run by q8_prep_kernel / q9_prep_kernel (rr_kernels.hip) in front of the
-// screen on its stream. (Quantising in every screen workgroup instead — each redoing all 32 queries,
-// two L2 passes — measured 8-13 us longer per launch: profiles/r04/ab/int8/.)
-// PIECES = 1 (the bf16-storage screen, DT 9: q ~ s p1, pieces [QS][d], scalars [4][QS] with the scale s itself; up to 64
-// slots) or 2 (DT 8: q ~ s (p1 + p2 / 64), pieces [2][32][d], scale s / 64).
-template <int PIECES = 2, int kQS = 32>
-__device__ __forceinline__ void q8_prep_slot(const float* __restrict__ q, int b, int d, int8_t* __restrict__ q8,
-                                             float* __restrict__ q8s, int slot, int lane) {
-  int8_t* p1 = q8 + (size_t)slot * d;
-  int8_t* p2 = q8 + (size_t)(kQS + slot) * d;
-  if (slot >= b) {
+// The int8 screens' query pieces of ONE query row (one wave), made when a batch is staged (rr_api.cpp stage_queries, on
+// the staging stream — off the compute streams' chain; r6, VERDICT r5 #4: the per-block prep kernel was 6.5 % of GPU
+// time at 1M and ~6 us of every compute stream's chain at 125k): s = max|q| / 127, t = q / s, p1 = clamp(rint(t)),
+// p2 = clamp(rint((t - p1) * 64)), so q ~ s (p1 + p2 / 64) with two pieces (DT 8: the MFMAs sum x8 . (64 p1 + p2)) or
+// q ~ s p1 with one (DT 9), and both residual norms, eq2 / eq1 >= |q - s (p1 + p2 / 64)| / |q - s p1| (real
+// arithmetic), in the scale's units as f32_to_i8_kernel: t - p1 - p2 / 64 is exact (each step by Sterbenz), so
+// |residual|_2 <= s |t - p1 - p2/64|_2 (x 1 + 2^-12) + 2^-21 sqrt(d) max|q| + 2^-140. |q| and sum|q| in fp32 (the bound
+// bumps for their summation order).
+// Layout (per query buffer): pieces p1 [QC][d] then p2 [QC][d] (int8, natural element order), scalars [6][QC]:
+// |q|, sum|q| (x 1 + 2^-18), s / 64, eq2, s, eq1 — DT 8 reads rows 0-3, DT 9 rows 0, 1, 4, 5 (kQ8Scalar). Query rows >= b
+// get zero pieces and scalars (the padding slots of the last block). qcopy (optional): the row's fp32 values are also
+// written there (the device-to-device staging copy, fused).
+__device__ __forceinline__ void q8_stage_row(const float* __restrict__ q, int b, int d, int8_t* __restrict__ p1base,
+                                             int8_t* __restrict__ p2base, float* __restrict__ q8s, int qc,
+                                             float* __restrict__ qcopy, int row, int lane) {
+  int8_t* p1 = p1base + (size_t)row * d;
+  int8_t* p2 = p2base + (size_t)row * d;
+  if (row >= b) {
     for (int e = 4 * lane; e < d; e += 256) {
       *(uint32_t*)(p1 + e) = 0;
-      if constexpr (PIECES == 2) *(uint32_t*)(p2 + e) = 0;
+      *(uint32_t*)(p2 + e) = 0;
     }
-    if (lane < 4) q8s[lane * kQS + slot] = 0.f;
+    if (lane < kQ8Scalars) q8s[lane * qc + row] = 0.f;
     return;
   }
-  (void)p2;
-  const f32x4* src = (const f32x4*)(q + (size_t)slot * d);
+  const f32x4* src = (const f32x4*)(q + (size_t)row * d);
+  f32x4* dst = qcopy ? (f32x4*)(qcopy + (size_t)row * d) : nullptr;
   // d <= 1024 (every d the int8 copy serves): the lane's <= 4 float4 loaded once, all issued before the first use —
   // one memory latency for both passes instead of one per float4 per pass (the same values in the same order)
   constexpr int kRegC = 4;
@@ -171,6 +174,10 @@ __device__ __forceinline__ void q8_prep_slot(const float* __restrict__ q, int b,
       const int c = lane + 64 * i;
       vr[i] = c < (d >> 2) ? src[c] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    if (dst)
+#pragma unroll
+      for (int i = 0; i < kRegC; ++i)
+        if (lane + 64 * i < (d >> 2)) dst[lane + 64 * i] = vr[i];
   }
   float m = 0.f, s2 = 0.f, s1 = 0.f;
   auto pass1 = [&](const f32x4 v) {
@@ -186,7 +193,11 @@ __device__ __forceinline__ void q8_prep_slot(const float* __restrict__ q, int b,
     for (int i = 0; i < kRegC; ++i)
       if (lane + 64 * i < (d >> 2)) pass1(vr[i]);
   } else {
-    for (int c = lane; c < (d >> 2); c += 64) pass1(src[c]);
+    for (int c = lane; c < (d >> 2); c += 64) {
+      const f32x4 v = src[c];
+      if (dst) dst[c] = v;
+      pass1(v);
+    }
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
@@ -195,29 +206,26 @@ __device__ __forceinline__ void q8_prep_slot(const float* __restrict__ q, int b,
     s1 += __shfl_xor(s1, off, 64);
   }
   const float s = m > 0.f ? m / 127.0f : 0.f;
-  float se = 0.f;
+  float se1 = 0.f, se2 = 0.f;
   auto pass2 = [&](const f32x4 v, int c) {
     uint32_t w1 = 0, w2 = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float a = 0.f, cc = 0.f, r = 0.f;
+      float a = 0.f, cc = 0.f, r1 = 0.f, r2 = 0.f;
       if (s > 0.f) {
         const float t = v[j] / s;
         a = fminf(fmaxf(rintf(t), -127.0f), 127.0f);
-        const float ta = t - a;   // exact
-        if constexpr (PIECES == 2) {
-          cc = fminf(fmaxf(rintf(ta * 64.0f), -127.0f), 127.0f);
-          r = ta - cc * 0x1p-6f;    // exact
-        } else {
-          r = ta;
-        }
+        r1 = t - a;   // exact
+        cc = fminf(fmaxf(rintf(r1 * 64.0f), -127.0f), 127.0f);
+        r2 = r1 - cc * 0x1p-6f;    // exact
       }
       w1 |= ((uint32_t)(int)a & 0xFFu) << (8 * j);
       w2 |= ((uint32_t)(int)cc & 0xFFu) << (8 * j);
-      se = fmaf(r, r, se);
+      se1 = fmaf(r1, r1, se1);
+      se2 = fmaf(r2, r2, se2);
     }
     *(uint32_t*)(p1 + 4 * c) = w1;
-    if constexpr (PIECES == 2) *(uint32_t*)(p2 + 4 * c) = w2;
+    *(uint32_t*)(p2 + 4 * c) = w2;
   };
   if (in_regs) {
 #pragma unroll
@@ -227,12 +235,18 @@ __device__ __forceinline__ void q8_prep_slot(const float* __restrict__ q, int b,
     for (int c = lane; c < (d >> 2); c += 64) pass2(src[c], c);
   }
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) se += __shfl_xor(se, off, 64);
+  for (int off = 32; off >= 1; off >>= 1) {
+    se1 += __shfl_xor(se1, off, 64);
+    se2 += __shfl_xor(se2, off, 64);
+  }
   if (lane == 0) {
-    q8s[slot] = sqrtf(s2);
-    q8s[kQS + slot] = s1 * (1.0f + 0x1p-18f);
-    q8s[2 * kQS + slot] = PIECES == 2 ? s * 0x1p-6f : s;
-    q8s[3 * kQS + slot] = fmaf(s * sqrtf(se), 1.0f + 0x1p-12f, fmaf(m, sqrtf((float)d) * 0x1p-21f, 0x1p-140f));
+    const float abs_term = fmaf(m, sqrtf((float)d) * 0x1p-21f, 0x1p-140f);
+    q8s[row] = sqrtf(s2);
+    q8s[qc + row] = s1 * (1.0f + 0x1p-18f);
+    q8s[2 * qc + row] = s * 0x1p-6f;
+    q8s[3 * qc + row] = fmaf(s * sqrtf(se2), 1.0f + 0x1p-12f, abs_term);
+    q8s[4 * qc + row] = s;
+    q8s[5 * qc + row] = fmaf(s * sqrtf(se1), 1.0f + 0x1p-12f, abs_term);
   }
 }
 

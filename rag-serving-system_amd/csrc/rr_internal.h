@@ -114,11 +114,13 @@ struct SkArgs {
   uint64_t* floors;
   // MODE 0, KT 32, 32 slots: every key instead of lists, all_keys[q * n + row] for q < b (full-sort path)
   uint64_t* all_keys;
-  // int8 screen (KDT_SCREEN8): corpus = the int8 copy, read as n = ceil(rows8 / 2) kernel rows of two corpus rows each;
-  // sx8 / e8 [rows8] the rows' scales and error norms; q8 [2][32][d] the queries' int8 pieces and q8s [4][32] their
-  // scalars (launch_q8_prep)
+  // int8 screen (KDT_SCREEN8 / 9): corpus = the int8 copy, read as n = ceil(rows8 / 2) kernel rows of two corpus rows
+  // each; sx8 / e8 [rows8] the rows' scales and error norms; the block's query pieces p1 at q8 and p2 at q8p2 ([slots][d]
+  // each) and their scalars q8s [6][q8s_stride] (launch_q8_stage's layout, offset to the block's first query)
   const int8_t* q8;
+  const int8_t* q8p2;
   const float* q8s;
+  int q8s_stride;
   const float* sx8;
   const float* e8;
   int64_t rows8;
@@ -146,8 +148,8 @@ struct SkArgs {
 // Events recorded by the NEXT kernel launch of the calling thread through its launch packet (hipExtLaunchKernelGGL:
 // start / stop), instead of hipEventRecord after it: a record is a separate barrier packet that holds the stream's
 // next kernel ~3 us on the device (tools/api_cost.hip: kernel -> record -> kernel 4.5 us, kernel with its stop event
-// -> kernel 1.4 us, as with nothing between). Taken (and cleared) by launch_sk / launch_sk_args, launch_merge and
-// launch_q8_prep; set it right before the launch it is meant for.
+// -> kernel 1.4 us, as with nothing between). Taken (and cleared) by launch_sk / launch_sk_args and launch_merge; set
+// it right before the launch it is meant for.
 struct LaunchEvents {
   hipEvent_t start = nullptr, stop = nullptr;
 };
@@ -252,11 +254,11 @@ hipError_t launch_f32_to_f16(const float* in, uint16_t* out, int64_t nrows, int 
 // (bf16 = 1: the rows' bf16 roundings, for bf16 storage's int8 copy)
 hipError_t launch_f32_to_i8(const float* in, int64_t nrows, int d, int8_t* out, float* sx, float* e, hipStream_t s,
                             int bf16 = 0);
-// The int8 screen's query pieces for a block of b <= 32 queries (slots b..31 zeroed): q8 [2][32][d], q8s [4][32] =
-// |q|, sum|q|, the pieces' scale / 64, an upper bound of |q - scale * (p1 + p2 / 64)|
-// pieces = 1 (the bf16 screen, DT 9): q ~ s p1, q8 [64][d], q8s [4][64] (scale s), for `slots` (32 or 64) slots.
-hipError_t launch_q8_prep(const float* q, int b, int d, int8_t* q8, float* q8s, hipStream_t s, int pieces = 2,
-                          int slots = 32);
+// The int8 screens' query pieces of a staged batch of b queries (rr_device.h q8_stage_row): q8 = p1 [qc][d] then p2
+// [qc][d], q8s [6][qc] (|q|, sum|q|, scale / 64, two-piece residual norm, scale, one-piece residual norm), rows b ..
+// 31 (b <= 32) or round_up(b, 64) - 1 zeroed (qc >= that). qcopy (may be null): the fp32 rows are also copied there (fused staging copy).
+constexpr int kQ8Scalars = 6;
+hipError_t launch_q8_stage(const float* q, int b, int d, int8_t* q8, int qc, float* q8s, float* qcopy, hipStream_t s);
 hipError_t launch_row_norms(int dtype, const void* corpus, int64_t n, int d, float* norms, hipStream_t s);
 hipError_t launch_synth(int kind, uint64_t seed, int64_t row_begin, int64_t n_rows, int d, float* out,
                         hipStream_t s);

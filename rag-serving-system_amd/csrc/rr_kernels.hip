@@ -853,16 +853,11 @@ __global__ __launch_bounds__(256) void f32_to_i8_kernel(const float* __restrict_
   }
 }
 
-// The int8 screen's query pieces: one 64-lane workgroup per query slot (rr_device.h q8_prep_slot), launched in front of
-// a screen when the screen launch does not prep them itself (rr_sk.hip: its joiner workgroups do when they run).
-__global__ __launch_bounds__(64) void q8_prep_kernel(const float* __restrict__ q, int b, int d,
-                                                     int8_t* __restrict__ q8, float* __restrict__ q8s) {
-  q8_prep_slot<2, 32>(q, b, d, q8, q8s, (int)blockIdx.x, (int)threadIdx.x);
-}
-// ... one piece per query, up to 64 slots (the bf16-storage screen, rr_sk.hip DT 9)
-__global__ __launch_bounds__(64) void q9_prep_kernel(const float* __restrict__ q, int b, int d,
-                                                     int8_t* __restrict__ q8, float* __restrict__ q8s) {
-  q8_prep_slot<1, 64>(q, b, d, q8, q8s, (int)blockIdx.x, (int)threadIdx.x);
+// The int8 screens' query pieces of a staged batch: one 64-lane workgroup per query row (rr_device.h q8_stage_row) over
+// every row a block reads (the rows past b zeroed: any block's padding slots read zeros), where the batch is staged.
+__global__ __launch_bounds__(64) void q8_stage_kernel(const float* __restrict__ q, int b, int d, int8_t* __restrict__ q8,
+                                                      int qc, float* __restrict__ q8s, float* __restrict__ qcopy) {
+  q8_stage_row(q, b, d, q8, q8 + (size_t)qc * d, q8s, qc, qcopy, (int)blockIdx.x, (int)threadIdx.x);
 }
 
 // Repair pass (rr_sk.hip "Repair"): the set bits of `bits` -> their indices in ascending order (list) and their count,
@@ -1151,16 +1146,11 @@ hipError_t launch_f32_to_i8(const float* in, int64_t nrows, int d, int8_t* out, 
   return hipGetLastError();
 }
 
-hipError_t launch_q8_prep(const float* q, int b, int d, int8_t* q8, float* q8s, hipStream_t s, int pieces,
-                          int slots) {
-  if (b < 1 || d < 1 || d % 4 != 0) return hipErrorInvalidValue;
-  if (pieces == 2) {
-    if (b > kQSlots || slots != kQSlots) return hipErrorInvalidValue;
-    RR_LAUNCH(q8_prep_kernel, dim3(kQSlots), dim3(64), 0, s, q, b, d, q8, q8s);
-  } else {   // one piece: [64][d] pieces and [4][64] scalars, `slots` of them written (32 or 64)
-    if (pieces != 1 || b > slots || (slots != 32 && slots != 64)) return hipErrorInvalidValue;
-    RR_LAUNCH(q9_prep_kernel, dim3(slots), dim3(64), 0, s, q, b, d, q8, q8s);
-  }
+hipError_t launch_q8_stage(const float* q, int b, int d, int8_t* q8, int qc, float* q8s, float* qcopy, hipStream_t s) {
+  // the rows any block reads: 32-slot blocks for b <= 32, else round_up(b, 64) (64-slot blocks, or 32-slot pairs)
+  const int rows = b <= 32 ? 32 : (b + 63) / 64 * 64;
+  if (b < 1 || d < 1 || d % 4 != 0 || rows > qc) return hipErrorInvalidValue;
+  RR_LAUNCH(q8_stage_kernel, dim3(rows), dim3(64), 0, s, q, b, d, q8, qc, q8s, qcopy);
   return hipGetLastError();
 }
 

@@ -59,7 +59,8 @@ hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int q
   }
   if (sdt == KDT_SCREEN8 || sdt == KDT_SCREEN9) {   // the int8 screens (a.corpus = the int8 copy, a.n = ceil(rows8 / 2))
     const int ns8 = sk_slabs(sdt, a.d);
-    if (!ns8 || !a.q8 || !a.q8s || !a.sx8 || !a.e8 || a.n != (a.rows8 + 1) / 2) return hipErrorInvalidValue;
+    if (!ns8 || !a.q8 || !a.q8s || !a.sx8 || !a.e8 || a.n != (a.rows8 + 1) / 2 || (sdt == KDT_SCREEN8 && !a.q8p2))
+      return hipErrorInvalidValue;
     if (sdt == KDT_SCREEN8) {
       if (qslots != 32) return hipErrorInvalidValue;
       return sk::fam_screen8(metric, ns8, kt, grid, a, s);

@@ -713,7 +713,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
           // two-row kernel row is elements (w % 4) KS .. + KS of its corpus row; K-step t, lane half h: 16 elements
           // at 32 t + 16 h of slab j — the 16-byte column 2t + h of the LDS image, as DT 7
           const int8_t* p1 = a.q8 + (size_t)rq * d;
-          const int8_t* p2 = a.q8 + (size_t)(QS + rq) * d;
+          const int8_t* p2 = a.q8p2 + (size_t)rq * d;
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             const int e0 = (w & (kWaves / 2 - 1)) * KS + j * kSlabRowBytes + 32 * t + 16 * h;
@@ -721,7 +721,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
             qf.c2[j][t] = *(const i32x4*)(p2 + e0);
           }
         } else if constexpr (DT == 9) {
-          // one piece per query, [64][d] (slot rq = r + 32 qh), the same element mapping as DT 8
+          // one piece per query (slot rq = r + 32 qh), the same element mapping as DT 8
           const int8_t* p1 = a.q8 + (size_t)rq * d;
 #pragma unroll
           for (int t = 0; t < 4; ++t)
@@ -819,11 +819,12 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // the int8 screen's per-query scalars of this lane's epilogue query (qe below), loaded with the fragments: one
   // latency before the first barrier instead of a second one after it
   float q8pre[4] = {0.f, 0.f, 0.f, 0.f};
-  if constexpr (I8) {   // (scalars [4][32], or DT 9's [4][64])
-    constexpr int QSS = DT == 9 ? 64 : 32;
+  if constexpr (I8) {   // (the staged scalars [6][stride]: |q|, sum|q|, then DT 8's scale / 64 and two-piece residual
+                        // norm, or DT 9's scale and one-piece residual norm — rr_device.h q8_stage_row)
     const int qe0 = 4 * QH * w + lane / (16 / QH);
+    const size_t st = (size_t)a.q8s_stride;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) q8pre[i] = a.q8s[i * QSS + qe0];
+    for (int i = 0; i < 4; ++i) q8pre[i] = a.q8s[(i < 2 || DT == 8 ? i : i + 2) * st + qe0];
   }
   if constexpr (MODE == 0) SK_PROBE(6);   // (diagnostic builds: prologue issued, before the fragments)
   if constexpr (DT != 2) {

@@ -420,9 +420,9 @@ class Index:
         _check(self._lib.rr_set_timeout(self._h, int(ms)))
 
     def stream_queues(self, shard: int = 0) -> list:
-        """Hardware-queue addresses of local shard `shard`'s four streams (compute 0, compute 1, exchange
-        lanes 0 and 1); equal addresses share one in-order queue (diagnostic)."""
-        out = (ctypes.c_uint64 * 4)()
+        """Hardware-queue addresses of local shard `shard`'s five streams (compute 0, compute 1, exchange
+        lanes 0 and 1, staging); equal addresses share one in-order queue (diagnostic)."""
+        out = (ctypes.c_uint64 * 5)()
         _check(self._lib.rr_stream_queues(self._h, int(shard), out))
         return list(out)
 

@@ -33,7 +33,9 @@ def test_stream_queues_distinct_and_shared_per_device(Index):
     """Hardware-queue placement (rr_stream_queues: each stream's AQL queue address, read by a probe kernel). A handle's
     four streams dispatch to four distinct hardware queues at the box's own GPU_MAX_HW_QUEUES (they take the
     high-priority pool, which nothing else of the process uses), also with a 1-rank RCCL communicator whose internal
-    streams are created after them; shards on one device share one set of streams (no cross-shard stream waits)."""
+    streams are created after them; shards on one device share one set of streams (no cross-shard stream waits).
+    out[4] is the optional staging stream (rr_set_option stage_stream >= 1): none by default; made at the least
+    priority (its own pool) it is distinct too."""
     import gc
     from rag_service_amd import get_unique_id
     gc.collect()                                               # handles of earlier tests released
@@ -41,12 +43,15 @@ def test_stream_queues_distinct_and_shared_per_device(Index):
     one = Index(dtype="fp32", metric="cosine")
     one.load(corpus)
     qs = one.stream_queues(0)
-    assert len(set(qs)) == 4 and all(qs), [hex(v) for v in qs]
+    assert len(set(qs[:4])) == 4 and all(qs[:4]) and qs[4] == 0, [hex(v) for v in qs]
+    one.set_option("stage_stream", 3)
+    qs = one.stream_queues(0)
+    assert len(set(qs)) == 5 and all(qs), [hex(v) for v in qs]
     one.close()
     many = Index(devices=[0, 0, 0], dtype="fp32", metric="cosine")
     many.load(corpus)
     q0 = many.stream_queues(0)
-    assert len(set(q0)) == 4, [hex(v) for v in q0]
+    assert len(set(q0[:4])) == 4, [hex(v) for v in q0]
     assert many.stream_queues(1) == q0 and many.stream_queues(2) == q0
     many.close()
     rx = Index(dtype="fp32", metric="cosine")
@@ -55,7 +60,7 @@ def test_stream_queues_distinct_and_shared_per_device(Index):
     q = synth.unit_norm_gaussian(76, 32, 512)
     rx.search(q, 5)                                            # the communicators' streams are in use
     qr = rx.stream_queues(0)
-    assert len(set(qr)) == 4, [hex(v) for v in qr]
+    assert len(set(qr[:4])) == 4, [hex(v) for v in qr]
     rx.close()
 
 

@@ -48,8 +48,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&e8, (size_t)r2 * 4));
   CK(hipMalloc(&norms, (size_t)(n + 64) * 4));
   CK(hipMalloc(&q, (size_t)b * d * 4));
-  CK(hipMalloc(&q8, (size_t)2 * 32 * d));
-  CK(hipMalloc(&q8s, (size_t)4 * 32 * 4));
+  CK(hipMalloc(&q8, (size_t)2 * 64 * d));   // (launch_q8_stage: p1 [64][d], p2 [64][d])
+  CK(hipMalloc(&q8s, (size_t)kQ8Scalars * 64 * 4));
   CK(hipMalloc(&cand, (size_t)(grid + 64) * 64 * 32 * 8));
   CK(hipMalloc(&ctr, 512));
   CK(hipMemset(ctr, 0, 512));
@@ -61,7 +61,7 @@ int main(int argc, char** argv) {
   CK(launch_synth(1, 99, 0, b, d, q, s));
   CK(launch_row_norms(0, c32, n, d, norms, s));
   CK(launch_f32_to_i8(c32, n, d, c8, sx, e8, s));
-  CK(launch_q8_prep(q, b, d, q8, q8s, s));
+  CK(launch_q8_stage(q, b, d, q8, 64, q8s, nullptr, s));
   CK(hipStreamSynchronize(s));
   SkArgs a{};
   a.corpus = (const char*)c8;
@@ -78,7 +78,9 @@ int main(int argc, char** argv) {
   a.eps_a = 6e-5f;
   a.eps_b = 4e-8f;
   a.q8 = q8;
+  a.q8p2 = q8 + (size_t)64 * d;
   a.q8s = q8s;
+  a.q8s_stride = 64;
   a.sx8 = sx;
   a.e8 = e8;
   a.ct8 = ct8;

@@ -56,8 +56,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&c8, (size_t)r2 * d));
   CK(hipMalloc(&sx, (size_t)r2 * 4));
   CK(hipMalloc(&e8, (size_t)r2 * 4));
-  CK(hipMalloc(&q8, (size_t)2 * 32 * d));
-  CK(hipMalloc(&q8s, (size_t)4 * 64 * 4));
+  CK(hipMalloc(&q8, (size_t)2 * 64 * d));   // (launch_q8_stage: p1 [64][d], p2 [64][d])
+  CK(hipMalloc(&q8s, (size_t)kQ8Scalars * 64 * 4));
   CK(hipMalloc(&ctr, 512));
   CK(hipMalloc(&wcount, 64));
   CK(hipMemset(ctr, 0, 512));
@@ -66,7 +66,7 @@ int main(int argc, char** argv) {
   CK(hipMemset(sx + n, 0, (size_t)(r2 - n) * 4));
   CK(hipMemset(e8 + n, 0, (size_t)(r2 - n) * 4));
   CK(launch_f32_to_i8(tmp, n, d, c8, sx, e8, s));
-  CK(launch_q8_prep(q, b, d, q8, q8s, s));
+  CK(launch_q8_stage(q, b, d, q8, 64, q8s, nullptr, s));
   CK(hipStreamSynchronize(s));
   SkArgs a{};
   a.corpus = (const char*)c32; a.norms = norms; a.queries = q; a.n = n; a.d = d; a.b = b; a.out = cand;
@@ -76,7 +76,7 @@ int main(int argc, char** argv) {
   v.wide_verify = 1;
   v.wide_count = wcount;
   if (i8) {
-    a.corpus = (const char*)c8; a.n = (n + 1) / 2; a.rows8 = n; a.q8 = q8; a.q8s = q8s; a.sx8 = sx; a.e8 = e8; a.ct8 = 2;
+    a.corpus = (const char*)c8; a.n = (n + 1) / 2; a.rows8 = n; a.q8 = q8; a.q8p2 = q8 + (size_t)64 * d; a.q8s = q8s; a.q8s_stride = 64; a.sx8 = sx; a.e8 = e8; a.ct8 = 2;
     a.eps_a = 6.0e-5f; a.eps_b = 4.0e-8f; a.sqrt_d = 32.0f * (1.0f + 0x1p-20f); a.ctr = ctr; a.dyn = 1;
   }
   hipEvent_t e0, e1;
