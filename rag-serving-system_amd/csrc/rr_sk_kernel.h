@@ -273,8 +273,15 @@ template <int NS>
 struct QFrag<9, NS> { i32x4 c1[NS][4]; };   // the bf16 storage's int8 screen: one int8 piece (64 slots fit)
 
 
-// LDS byte offset (within a slot) of 16-byte column position cp of tile row r (swizzled image)
-__device__ __forceinline__ int slab_off(int r, int cp) { return (r >> 3) * 1024 + (r & 7) * 128 + ((cp ^ (r & 7)) << 4); }
+// LDS byte offset (within a slot) of 16-byte column position cp of tile row r (swizzled image): column cp of row r sits
+// at position cp ^ (r & 7) ^ ((r >> 3) & 1). A ds_read_b128 serves 16 lanes per pass — rows r .. r + 15 of one column
+// position here — which must cover all 64 banks: the (r & 7) term spreads rows r .. r + 7 over 32 of them, the
+// (r >> 3) & 1 term moves rows r + 8 .. r + 15 to the other 32. (r6: without it rows r and r + 8 shared their banks —
+// 4 conflict cycles per fragment read, every SQ_LDS_BANK_CONFLICT cycle of the streaming kernels; profiles/r06/sq/.
+// Round 4 had attributed them to the LDS-DMA landing.)
+__device__ __forceinline__ int slab_off(int r, int cp) {
+  return (r >> 3) * 1024 + (r & 7) * 128 + ((cp ^ (r & 7) ^ ((r >> 3) & 1)) << 4);
+}
 
 // Verify stage (MODE 1): the screen's [QS][nlists][KT] upper-bound lists -> this query's global top-NC by u
 // in akeys[] (LDS, descending; NC = 32 >= KT: one whole MFMA tile of rows), by rank selection instead of NC rounds of
@@ -563,15 +570,18 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   };
 
   // LDS-DMA lane mapping: instruction i of a slab covers tile rows 8i + lane/8, 16-byte column
-  // (lane % 8) ^ (lane / 8) of the slab — so the image holds column c of row r at c ^ (r & 7)
+  // (lane % 8) ^ (lane / 8) ^ (i & 1) of the slab — so the image holds column c of row r at c ^ (r & 7) ^ ((r >> 3) & 1)
+  // (slab_off)
   const int rl = lane >> 3, cl = lane & 7;
   const unsigned ring_lds = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(smem + (size_t)w * RS * kSlabBytes));
   const unsigned trow_lds = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)trow);
   const char* ring = smem + (size_t)w * RS * kSlabBytes;
-  const char* lane_src = corpus + (size_t)w * KS + ((cl ^ rl) << 4);
+  const char* lane_src = corpus + (size_t)w * KS + ((cl ^ rl) << 4);        // row groups 0, 16 (instructions 0, 2)
+  const char* lane_srcx = corpus + (size_t)w * KS + ((cl ^ rl ^ 1) << 4);   // row groups 8, 24 (instructions 1, 3)
 
   // per-lane part of a slab address: row rl of each 8-row group, swizzled 16-byte column (< 8 rows: 32-bit)
   const unsigned lane_off = (unsigned)(rl * row_bytes + ((cl ^ rl) << 4));
+  const unsigned lane_offx = (unsigned)(rl * row_bytes + ((cl ^ rl ^ 1) << 4));
   const unsigned row8 = (unsigned)(8 * row_bytes);   // (row groups 8, 16, 24 of a tile: offsets < 2^32)
   const char* wave_src = corpus + (size_t)w * KS;
   auto issue = [&](int64_t base, int j, int slot) {   // slab j (this wave's K-slice) of the tile at row base
@@ -582,12 +592,12 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #define RR_SK_SLAB_ASM 1   // one inline-asm statement per slab; A/B (r4, profiles/r04/ab_slab.txt): window +1.5 %, steady +0.8 %
 #endif
       if constexpr (RR_SK_SLAB_ASM) {
-        glds16s_slab(wave_src + sb * row_bytes + j * kSlabRowBytes, lane_off, lane_off + row8, lane_off + 2 * row8,
-                     lane_off + 3 * row8, ring_lds + slot * kSlabBytes);
+        glds16s_slab(wave_src + sb * row_bytes + j * kSlabRowBytes, lane_off, lane_offx + row8, lane_off + 2 * row8,
+                     lane_offx + 3 * row8, ring_lds + slot * kSlabBytes);
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          glds16s(wave_src + (sb + 8 * i) * row_bytes + j * kSlabRowBytes, lane_off,
+          glds16s(wave_src + (sb + 8 * i) * row_bytes + j * kSlabRowBytes, (i & 1) ? lane_offx : lane_off,
                   ring_lds + slot * kSlabBytes + i * 1024);
       }
     } else {
@@ -595,7 +605,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       for (int i = 0; i < 4; ++i) {
         int64_t row = base + 8 * i + rl;
         row = row < n ? row : n - 1;                    // partial last tile: re-read a valid row
-        glds16(lane_src + row * row_bytes + j * kSlabRowBytes, ring_lds + slot * kSlabBytes + i * 1024);
+        glds16(((i & 1) ? lane_srcx : lane_src) + row * row_bytes + j * kSlabRowBytes, ring_lds + slot * kSlabBytes + i * 1024);
       }
     }
   };
@@ -1453,8 +1463,14 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
         }
       } else if constexpr (DT == 9) {   // bf16 storage's int8 screen: one piece per query, both query halves
         i32x4 av[4];
+#if defined(RR_SK_DIAG) && (RR_SK_DIAG & 8)
+        // diagnostic builds only (profiles/r06/sq): no slab fragment reads (the LDS-DMA still lands)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) av[t] = (i32x4){lane, t, j, (int)tcount};
+#else
 #pragma unroll
         for (int t = 0; t < 4; ++t) av[t] = *(const i32x4*)(sl + slab_off(r, 2 * t + h));
+#endif
         if constexpr (MODE == 0 && LA == 2) issue_ahead(jc);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -1518,9 +1534,12 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
 #if defined(RR_SK_DIAG) && (RR_SK_DIAG & 2)
     if (MODE == 0) {   // diagnostic builds only: no K-partial exchange (the barrier stays), this wave's own partials
       lds_barrier();
-      float sv[DPL];
+      float sv[DPO];
 #pragma unroll
-      for (int e = 0; e < DPL; ++e) sv[e] = accs[e % QH][e];
+      for (int e = 0; e < DPO; ++e) {
+        if constexpr (I8) sv[e] = (float)iacc[e % NIA][e];
+        else sv[e] = accs[e % QH][e];
+      }
       epilogue(sv, base, ts);
       ++tcount;
       ts = (ts + 1) & 3;

@@ -15,7 +15,7 @@ def main():
     out = {}
     for d in args:
         per = collections.defaultdict(lambda: collections.defaultdict(list))
-        for f in glob.glob(f"{d}/p*/**/*counter_collection.csv", recursive=True):
+        for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
             for r in csv.DictReader(open(f)):
                 n = r["Kernel_Name"]
                 if "sk_score_kernel" in n or "fused_score_kernel" in n:
