@@ -1,6 +1,8 @@
 #!/bin/bash
 # A/B of bench arms interleaved on one GPU box (run inside gpurun). An arm is name:dir:ENV=VAL[,ENV=VAL]
 # (dir holds the bench.py + package to run; "." = the working tree). Arms alternate REPS times per workload.
+# (r6: the product library reads path options through rr_set_option only — set them with EXTRA="--opt name=value",
+# or give an arm a library built with tools/ab/build_rev.sh ... -DRR_AB_ENV=1, which reads RR_<NAME> variables.)
 #   bash tools/ab/ab2.sh gpurun_out/<file> "<docs> <batch> <k> <dtype>" arm1 arm2 ...
 set -o pipefail
 R=$GRAFT_REPO_ROOT
