@@ -143,6 +143,10 @@ struct SkArgs {
   const int* rcount;
   ChunkGeo rs;
   int rs_rows;
+  // MODE 0: the launch's own chunk geometry, computed by launch_sk_args on the host (geo_set = 1): the kernel then
+  // starts issuing its first slabs without the ~500 scalar instructions of chunk_geo's 64-bit divisions (r6)
+  ChunkGeo geo;
+  int geo_set;
 };
 
 // Events recorded by the NEXT kernel launch of the calling thread through its launch packet (hipExtLaunchKernelGGL:

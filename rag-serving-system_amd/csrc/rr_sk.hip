@@ -41,10 +41,15 @@ int sk_slabs(int sdt, int d) {
 }
 
 #ifndef RR_SK_NO_DISPATCH   // (diagnostic tools that instantiate one kernel directly: tools/probe_screen.hip)
-hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int qslots, const SkArgs& a,
+hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int qslots, const SkArgs& a_in,
                           hipStream_t s, int ring) {
-  const int ns = sk_slabs(sdt == KDT_SCREEN ? KDT_F32_X3 : sdt, a.d);
-  if (!ns || a.b < 1 || a.b > qslots || a.n < 1 || (qslots != 32 && qslots != 64)) return hipErrorInvalidValue;
+  const int ns = sk_slabs(sdt == KDT_SCREEN ? KDT_F32_X3 : sdt, a_in.d);
+  if (!ns || a_in.b < 1 || a_in.b > qslots || a_in.n < 1 || (qslots != 32 && qslots != 64)) return hipErrorInvalidValue;
+  SkArgs a = a_in;
+  // the kernel's chunk geometry (its CT: sk_chunk_tiles), here instead of in every workgroup (MODE 1 does not use it,
+  // but would compute it)
+  a.geo = chunk_geo((a.n + 31) / 32, sk_chunk_tiles(sdt, a.d, a.ct8), grid, !a.no_guided);
+  a.geo_set = 1;
   if (ring == 0) ring = kSkRing;
   if (ring != 2) return hipErrorInvalidValue;
   if (mode == 1) {   // verify, one workgroup per query slot: exact fp32 arithmetic (32 slots) or bf16's (32 or 64)

@@ -543,7 +543,7 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
   // The repair pass (a.rlist: MODE 0 over the fp32 rows, static schedule) instead walks the screen chunks listed in
   // rlist: chunk j = the corpus rows of screen chunk rlist[j] (rs: the screen's geometry, rs_rows rows per screen tile).
   const bool REP = MODE == 0 && !SCR && SCHED == 0 && a.rlist != nullptr;
-  const ChunkGeo geo = chunk_geo((n + 31) / 32, CT, G, !a.no_guided);
+  const ChunkGeo geo = a.geo_set ? a.geo : chunk_geo((n + 31) / 32, CT, G, !a.no_guided);   // (host-computed: launch_sk_args)
   const int64_t T = geo.T;
   const int64_t C = REP ? (int64_t)*a.rcount : geo.C;
   auto rep_rows = [&](int64_t j, int64_t* r0, int64_t* r1) {

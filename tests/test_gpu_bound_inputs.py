@@ -211,3 +211,32 @@ def test_options_reject_unknown_and_out_of_range(Index):
     ix.set_option("screen_grid", 128)
     assert ix.get_option("screen_grid") == 128
     ix.close()
+
+
+def test_update_rows_rejects_collectively(Index):
+    """rr_update_rows under rr_init_dist is a collective: a rank whose arguments are invalid still reaches
+    the ranks' agreement and fails with RR_E_INVALID (with a world of one, here, its own message); the handle stays
+    usable — a valid update and a search follow, equal to the exact kernel on the updated corpus."""
+    from rag_service_amd import get_unique_id
+    from rag_service_amd._lib import HipRetrievalError, RR_E_INVALID
+    corpus = synth.unit_norm_gaussian(93, 70000, 1024)
+    q = synth.unit_norm_gaussian(94, 32, 1024)
+    ix = Index(dtype="fp32", metric="cosine")
+    ix.init_dist(1, 0, get_unique_id())
+    ix.load(corpus)
+    with pytest.raises(HipRetrievalError) as e:
+        ix.update_rows(q[:2], np.array([5, 70000]))            # index out of range
+    assert e.value.code == RR_E_INVALID and "outside" in str(e.value)
+    with pytest.raises(HipRetrievalError) as e:
+        ix.update_rows(q[:2, :512], np.array([5, 6]))          # wrong dimension
+    assert e.value.code == RR_E_INVALID
+    ix.update_rows(q[:2], np.array([5, 6]))
+    corpus[[5, 6]] = q[:2]
+    got = ix.search(q, 5)
+    assert np.all(got[1][:2, 0] == [5, 6])
+    ex = Index(dtype="fp32", metric="cosine")
+    ex.load(corpus)
+    ex.set_kernel("exact")
+    _same(got, ex.search(q, 5))
+    ex.close()
+    ix.close()

@@ -129,6 +129,29 @@ def test_config5_bf16_b64_through_rccl(Index, golden_configs, config5):
     ix.close()
 
 
+@pytest.mark.parametrize("metric,flavour", [("dot", "simple"), ("cosine", "cupy")])
+def test_config5_golden_in_32_query_blocks(Index, golden_configs, config5, metric, flavour):
+    """The reference's own config-5 results (golden, 1M bf16-rounded rows, k = 10) through bf16 storage's 32-slot
+    screened blocks (r6): the 64 queries as two batches of 32 — each one screened block over the int8 copy, verified
+    by the bf16 pass's arithmetic — give the golden indices, and equal the exact kernel's results bit for bit."""
+    corpus, q, k = config5
+    ix = Index(dtype="bf16", metric=metric)
+    ix.load(corpus)
+    assert ix.screen_int8()
+    got = [ix.search(q[:32], k), ix.search(q[32:], k)]
+    assert ix.screen_counts_all()[0] == 2
+    scores = np.concatenate([g[0] for g in got])
+    idx = np.concatenate([g[1] for g in got])
+    _, near = check_topk(idx, scores, golden_configs[f"c5_{flavour}_idx"], corpus, q, metric, near_tie=1e-5)
+    if float(golden_configs[f"c5_{flavour}_gap"]) > 1e-5:
+        assert near == 0
+    ix.set_kernel("exact")
+    for g, qq in zip(got, (q[:32], q[32:])):
+        want = ix.search(qq, k)
+        assert np.array_equal(g[1], want[1]) and np.array_equal(g[0], want[0])
+    ix.close()
+
+
 N5 = 50_000_000
 
 
