@@ -1,7 +1,8 @@
 // hbm_ceiling.hip — the streaming-read ceilings the split-K kernels are judged against: how fast MI355X
 // reads an fp32 corpus of 1M x 1024 (4.1 GB) with (a) plain float4 loads, (b) non-temporal float4 loads, (c) the
 // product kernels' own movement — 4-KiB slabs of 32 rows x 128 contiguous bytes per wave by `global_load_lds_dwordx4
-// ... nt` into an LDS ring, two slabs in flight per wave, one 512-thread workgroup per CU — with no arithmetic, and
+// ... nt` into an LDS ring, one slab in flight per wave beside the one read (two slots; also three and four slots),
+// one 512-thread workgroup per CU — with no arithmetic, and
 // (d) a float4 copy (read + write, the number MI355X_MICROARCH.md quotes). Development tool, not part of the product.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/hbm_ceiling.hip -o tools/hbm_ceiling && tools/hbm_ceiling [rows] [reps]
@@ -65,17 +66,23 @@ __device__ __forceinline__ void glds16_nt(const void* src, unsigned lds) {
       : "v"(src), "s"(lds)
       : "memory");
 }
+template <int SLOTS>
 __global__ __launch_bounds__(512) void lds_dma_stream(const char* __restrict__ c, int64_t rows, int row_bytes,
                                                       unsigned* out) {
+  // SLOTS slab slots per wave, SLOTS - 1 slabs in flight while one is read (the product kernels: 2 slots, the next
+  // slab issued into the other before waiting; here also 3 and 4)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int KS = row_bytes / 8, NS = KS / 128;
   const int64_t per = (rows + gridDim.x - 1) / gridDim.x;
   const int64_t r0 = (int64_t)blockIdx.x * per, r1 = r0 + per < rows ? r0 + per : rows;
-  const unsigned ring = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(smem + (size_t)w * 2 * 4096));
+  const unsigned ring = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(smem + (size_t)w * SLOTS * 4096));
   const int rl = lane >> 3, cl = lane & 7;
   const char* src0 = c + (size_t)w * KS + ((cl ^ rl) << 4);
-  auto issue = [&](int64_t base, int j, int slot) {
+  const int64_t nslabs = (r1 - r0 + 31) / 32 * NS;   // slab s: tile s / NS, K-part s % NS
+  auto issue = [&](int64_t sidx, int slot) {
+    const int64_t base = r0 + sidx / NS * 32;
+    const int j = (int)(sidx % NS);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       int64_t row = base + 8 * i + rl;
@@ -84,17 +91,19 @@ __global__ __launch_bounds__(512) void lds_dma_stream(const char* __restrict__ c
     }
   };
   unsigned acc = 0;
-  int slot = 0;
-  if (r0 < r1) issue(r0, 0, 0);
-  for (int64_t base = r0; base < r1; base += 32) {
-    for (int j = 0; j < NS; ++j) {
-      const bool more = j + 1 < NS || base + 32 < r1;
-      if (more) issue(j + 1 < NS ? base : base + 32, j + 1 < NS ? j + 1 : 0, slot ^ 1);
-      if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      acc ^= *(const unsigned*)(smem + (size_t)w * 2 * 4096 + slot * 4096 + lane * 64);   // one word per lane read
-      slot ^= 1;
-    }
+  for (int p = 0; p < SLOTS - 1; ++p)
+    if (p < nslabs) issue(p, p);
+  for (int64_t sidx = 0; sidx < nslabs; ++sidx) {
+    const int slot = (int)(sidx % SLOTS);
+    const int64_t nx = sidx + SLOTS - 1;
+    if (nx < nslabs) issue(nx, (int)(nx % SLOTS));
+    // in flight after this slab: min(SLOTS - 1, slabs left after it), 4 instructions each
+    const int64_t after = nslabs - 1 - sidx < SLOTS - 1 ? nslabs - 1 - sidx : SLOTS - 1;
+    if (after >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (after == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    acc ^= *(const unsigned*)(smem + (size_t)w * SLOTS * 4096 + slot * 4096 + lane * 64);   // one word per lane read
   }
   out[(size_t)blockIdx.x * 512 + threadIdx.x] = acc;
 }
@@ -134,10 +143,15 @@ int main(int argc, char** argv) {
   const int grid = cus * 8;   // 8 workgroups of 512 per CU for the register loads
   const float t_plain = time_it([&] { hipLaunchKernelGGL(read_f4<false>, dim3(grid), dim3(512), 0, 0, (const u32x4*)c, n16, out); });
   const float t_nt = time_it([&] { hipLaunchKernelGGL(read_f4<true>, dim3(grid), dim3(512), 0, 0, (const u32x4*)c, n16, out); });
-  CK(hipFuncSetAttribute((const void*)lds_dma_stream, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
-  const float t_dma = time_it([&] {
-    hipLaunchKernelGGL(lds_dma_stream, dim3(cus), dim3(512), 64 * 1024, 0, (const char*)c, rows, row_bytes, out);
-  });
+  float t_dma[3];
+  auto dma = [&](auto kern, int slots, float* t) {
+    const int lds = 8 * slots * 4096;
+    CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    *t = time_it([&] { hipLaunchKernelGGL(kern, dim3(cus), dim3(512), lds, 0, (const char*)c, rows, row_bytes, out); });
+  };
+  dma(lds_dma_stream<2>, 2, &t_dma[0]);
+  dma(lds_dma_stream<3>, 3, &t_dma[1]);
+  dma(lds_dma_stream<4>, 4, &t_dma[2]);
   const float t_copy = time_it([&] { hipLaunchKernelGGL(copy_f4, dim3(grid), dim3(512), 0, 0, (const u32x4*)c, (u32x4*)o, n16); });
   CK(hipGetLastError());
   auto gbs = [&](float ms, double b) { return b / (ms * 1e-3) / 1e9; };
@@ -145,9 +159,13 @@ int main(int argc, char** argv) {
          "\"read_plain_float4\": {\"us\": %.1f, \"GBps\": %.0f, \"frac_8TBps\": %.4f}, "
          "\"read_nt_float4\": {\"us\": %.1f, \"GBps\": %.0f, \"frac_8TBps\": %.4f}, "
          "\"lds_dma_nt_slabs_one_wg_per_cu\": {\"us\": %.1f, \"GBps\": %.0f, \"frac_8TBps\": %.4f}, "
+         "\"lds_dma_3_slots\": {\"us\": %.1f, \"GBps\": %.0f, \"frac_8TBps\": %.4f}, "
+         "\"lds_dma_4_slots\": {\"us\": %.1f, \"GBps\": %.0f, \"frac_8TBps\": %.4f}, "
          "\"copy_float4_read_plus_write\": {\"us\": %.1f, \"GBps\": %.0f, \"frac_8TBps\": %.4f}}\n",
          (long long)rows, bytes, cus, reps, t_plain * 1e3, gbs(t_plain, bytes), gbs(t_plain, bytes) / 8000.0,
-         t_nt * 1e3, gbs(t_nt, bytes), gbs(t_nt, bytes) / 8000.0, t_dma * 1e3, gbs(t_dma, bytes), gbs(t_dma, bytes) / 8000.0,
+         t_nt * 1e3, gbs(t_nt, bytes), gbs(t_nt, bytes) / 8000.0, t_dma[0] * 1e3, gbs(t_dma[0], bytes),
+         gbs(t_dma[0], bytes) / 8000.0, t_dma[1] * 1e3, gbs(t_dma[1], bytes), gbs(t_dma[1], bytes) / 8000.0,
+         t_dma[2] * 1e3, gbs(t_dma[2], bytes), gbs(t_dma[2], bytes) / 8000.0,
          t_copy * 1e3, gbs(t_copy, 2.0 * bytes), gbs(t_copy, 2.0 * bytes) / 8000.0);
   return 0;
 }
