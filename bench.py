@@ -10,9 +10,12 @@ rank; started plainly (`python bench.py --gpus N`), it launches `python -m torch
 with its status (no exec).
 
 A step = one batch of B queries through the whole device pipeline (fused MFMA similarity + top-k over
-the rank's corpus shard, per-shard merge, RCCL all-gather of candidates when N > 1, final merge), with
-the queries already resident in HBM. The corpus (N_DOCS x d, fixed total: strong scaling) is generated
-on device. Rank 0 prints ONE JSON line.
+the rank's corpus shard, per-shard merge, RCCL all-gather of candidates over the rank's shard group, final
+merge), with the queries already resident in HBM. The corpus (N_DOCS x d) is generated on device. N > 1:
+the ranks form R replica groups of S ranks (`--shard-group`, auto: the fewest ranks whose row shards keep
+>= 500k rows — 1M docs: S = 2); each group holds the whole corpus as S row shards and searches its own
+batches, and `value` counts every group's batches. With R > 1 the same loop over all N ranks as one
+row-sharded group is measured too (`row_shard_all`). Rank 0 prints ONE JSON line.
 
 Also reported: host-inclusive latency (H2D of the queries + pipeline + D2H of results) p50/p99 over
 synchronous batches, and the CPU baseline = the oracle's restatement of the reference SimpleRetriever
@@ -138,14 +141,14 @@ def algorithmic_bytes(rows: int, d: int, batch: int, dtype: str, metric: str, sc
     return rows * (d * elem + per_row) + batch * d * 4
 
 
-def make_stager(ix, q, nb: int, local: int, restage: bool):
+def make_stager(ix, q, nb: int, local: int, restage: bool, seed: int = 4242):
     """A step's queries: with `restage` (the default) every step stages a NEW batch of B queries already resident in HBM
     (nb distinct batches in one device buffer, batch 0 = q; rr_set_queries_device — the copy into the library's query
     buffer and the int8 screens' query pieces, on its staging stream), as a serving loop does per batch; without, the
     batch staged once is searched again (round 5's loop). Returns (stage(i) or None, keep-alive)."""
     if not restage:
         return None, None
-    rng = np.random.default_rng(4242)
+    rng = np.random.default_rng(seed)
     qs = rng.standard_normal((nb,) + q.shape).astype(np.float32)
     qs /= np.linalg.norm(qs, axis=2, keepdims=True)
     qs[0] = q
@@ -341,6 +344,13 @@ def main() -> None:
     ap.add_argument("--no-restage", action="store_true",
                     help="search the batch staged once in every step (round 5's loop) instead of staging a new batch, "
                          "resident in HBM, per step")
+    ap.add_argument("--shard-group", type=int, default=0,
+                    help="N>1: ranks per shard group S (the corpus as S row shards with one RCCL all-gather per block, "
+                         "groups searching their own batches; R = N / S replica groups); 0 = auto: the fewest ranks "
+                         "whose shards keep >= 500k rows (rag_service_amd.dist.placement); N = pure row shards")
+    ap.add_argument("--no-row-shard-all", action="store_true",
+                    help="with R > 1 replica groups, skip the second measurement over all N ranks as row shards")
+    ap.add_argument("--same-device", action="store_true", help=argparse.SUPPRESS)   # (test hook: every rank on cuda:0)
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="a path setting of the measured handle (rr_set_option: screen_grid, verify_cus, x_slots, "
                          "x_host_wait_us, screen_i8_pieces, ...; results are the same under every value); repeatable")
@@ -375,10 +385,16 @@ def run(args, stage: dict) -> None:
 
     from rag_service_amd import Index, get_unique_id
     from rag_service_amd import _lib
-    from rag_service_amd.dist import (barrier, broadcast_bytes, env_rank_world, init_control_plane,
-                                      max_over_ranks)
+    from rag_service_amd.dist import (all_gather_bytes, barrier, broadcast_bytes, env_rank_world,
+                                      init_control_plane, max_over_ranks, placement, sum_over_ranks)
 
     rank, world, local = env_rank_world()
+    if args.same_device:
+        local = 0
+    # placement: R replica groups of S ranks; group g holds the whole corpus as S row shards (its own RCCL
+    # communicator) and searches its own batches
+    S, R = placement(args.docs, world, args.shard_group)
+    grp, grank = rank // S, rank % S
     stage["stage"] = "control-plane init"
     dist = init_control_plane(world, rank, timeout_s=max(1, int(args.dist_timeout_s)))
     if args.dry_run:
@@ -387,10 +403,15 @@ def run(args, stage: dict) -> None:
         stage["stage"] = "dry-run barrier"
         barrier(dist)
         ranks_seen = max_over_ranks(dist, float(rank)) + 1
+        # the groups' communicator ids as the real run exchanges them (stand-in ids: no GPU call)
+        ids = all_gather_bytes(dist, f"group-{grp}".encode() if grank == 0 else None)
+        ids_ok = sum_over_ranks(dist, float(ids[grp * S] == f"group-{grp}".encode()))
         if rank == 0:
             print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": int(ranks_seen),
                               "launched_by": "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ
-                              else "plain"}), flush=True)
+                              else "plain",
+                              "placement": {"shard_group": S, "replica_groups": R,
+                                            "ranks_with_their_group_id": int(ids_ok)}}), flush=True)
         barrier(dist)
         return
 
@@ -405,14 +426,14 @@ def run(args, stage: dict) -> None:
     stage["stage"] = "handle + RCCL communicator"
     ix = Index(devices=[local], dtype=args.dtype, metric=args.metric, options=args.options)
     rccl_ranks = 0
-    if world > 1:
-        uid = broadcast_bytes(dist, get_unique_id() if rank == 0 else None)
-        ix.init_dist(world, rank, uid)
+    if S > 1:   # the group's communicator: its first rank's id, exchanged over the control plane
+        uids = all_gather_bytes(dist, get_unique_id() if grank == 0 else None)
+        ix.init_dist(S, grank, uids[grp * S])
         rccl_ranks = ix.dist_info()[0]
     elif args.exchange_1rank:
         ix.init_dist(1, 0, get_unique_id())
         rccl_ranks = ix.dist_info()[0]
-    if world > 1:   # the library's waits on RCCL work: a third of the control-plane deadline, at most 120 s
+    if S > 1:   # the library's waits on RCCL work: a third of the control-plane deadline, at most 120 s
         ix.set_timeout(int(min(120.0, args.dist_timeout_s / 3) * 1000))
     # the hardware queues the handle's four streams dispatch to (distinct = none shares an in-order queue)
     queues = ix.stream_queues(0)
@@ -421,14 +442,14 @@ def run(args, stage: dict) -> None:
     if args.kernel != "auto":
         ix.set_kernel(args.kernel)
     sb, se = ix.shard_range(0)
-    rng = np.random.default_rng(5678)
+    rng = np.random.default_rng(5678 + grp)   # (each replica group searches batches of its own)
     q = rng.standard_normal((args.batch, args.dim)).astype(np.float32)
     q /= np.linalg.norm(q, axis=1, keepdims=True)
 
     # ---- throughput: queries resident in HBM, K back-to-back steps, each a new batch ---------------
     stage["stage"] = "timed steps"
     ix.set_queries(q)
-    stager, _keep = make_stager(ix, q, 16, local, not args.no_restage)
+    stager, _keep = make_stager(ix, q, 16, local, not args.no_restage, 4242 + grp)
     acct = {}
     elapsed, kern_ms, launches = timed_steps(ix, args.k, args.steps, args.warmup, dist, cuda_sync, every, acct,
                                              stager)
@@ -507,6 +528,35 @@ def run(args, stage: dict) -> None:
     if args.pmc_child:            # only the fused-kernel launches matter to the parent's PMC parse
         ix.close()
         return
+
+    # ---- replica groups (R > 1): the same workload with all N ranks as ONE row-sharded group (the north star's
+    # layout, one RCCL all-gather over all N per block), reported beside value ----------------------------------
+    row_all = None
+    if R > 1 and not args.no_row_shard_all:
+        stage["stage"] = "all ranks as one row-sharded group"
+        ix.close()
+        ax = Index(devices=[local], dtype=args.dtype, metric=args.metric, options=args.options)
+        ax.init_dist(world, rank, broadcast_bytes(dist, get_unique_id() if rank == 0 else None))
+        ax.set_timeout(int(min(120.0, args.dist_timeout_s / 3) * 1000))
+        ax.fill_synthetic(_lib.RR_SYNTH_UNIT_NORM, 1234, args.docs, args.dim)
+        q0 = np.random.default_rng(5678).standard_normal((args.batch, args.dim)).astype(np.float32)
+        q0 /= np.linalg.norm(q0, axis=1, keepdims=True)
+        ax.set_queries(q0)
+        a_stager, _akeep = make_stager(ax, q0, 16, local, not args.no_restage)
+        a_acct, a_st = {}, {}
+        aw_el, _, _ = timed_steps(ax, args.k, args.steps, args.warmup, dist, cuda_sync, every, a_acct, a_stager)
+        aw_el = max_over_ranks(dist, aw_el)
+        as_el, _, _ = timed_steps(ax, args.k, args.steady_steps, 0, dist, cuda_sync, 10, a_st, a_stager)
+        as_el = max_over_ranks(dist, as_el)
+        row_all = {"value": round(args.batch * args.steps / aw_el, 2), "unit": "queries/s",
+                   "ms_per_step": round(aw_el / args.steps * 1e3, 4),
+                   "steady_value": round(args.batch * args.steady_steps / as_el, 2),
+                   "steady_ms_per_step": round(as_el / args.steady_steps * 1e3, 4),
+                   "parallelism": f"row-shard x{world}", "rccl_ranks": ax.dist_info()[0],
+                   "screen_fallbacks_timed": a_acct.get("flagged"), "reruns_paid": a_acct.get("reruns_paid"),
+                   "note": "the same K / W staged loop and steady loop with all N ranks as one group: every rank "
+                           "searches every batch over its 1/N row shard, one RCCL all-gather over all N per block"}
+        ax.close()
 
     # ---- the other corpus dtypes on the same workload (1 GPU only; reported beside, never `value`) --
     # ---- corpus ingest (main.py:20-23 + retriever.py:582): host fp32 numpy -> HBM storage, N=1 only ------
@@ -592,7 +642,7 @@ def run(args, stage: dict) -> None:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:   # rank 0 at N=1 only
             cpu = cpu_baseline(args.docs, args.dim, args.batch, args.k, args.cpu_budget)
-        value = args.batch * args.steps / elapsed
+        value = args.batch * args.steps * R / elapsed   # (R replica groups, each its own batches)
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -602,14 +652,22 @@ def run(args, stage: dict) -> None:
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "strong" if R == 1 else "weak",
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (device-generated unit-norm approx-Gaussian rows, seed 1234; unit-norm queries)",
             "config": {"workload": f"{args.docs} synthetic docs d={args.dim}, batch={args.batch}, top-k={args.k}, "
                                    f"{args.metric} (CupyRetriever semantics)",
                        "docs": args.docs, "d": args.dim, "batch": args.batch, "k": args.k,
-                       "metric": args.metric, "corpus_dtype": args.dtype, "parallelism": f"row-shard x{world}"},
+                       "metric": args.metric, "corpus_dtype": args.dtype,
+                       "parallelism": f"row-shard x{S}" + (f", replica groups x{R}" if R > 1 else "")},
+            "placement": {"shard_group": S, "replica_groups": R, "rule": (
+                "auto: the fewest ranks whose row shards keep >= 500k rows each (rag_service_amd.dist.placement)"
+                if args.shard_group == 0 else f"--shard-group {args.shard_group}"),
+                "note": "each group holds the whole corpus as S contiguous row shards and searches its own batches "
+                        "(one RCCL all-gather over its S ranks per block); value = the R groups' batches together "
+                        "over the max-over-ranks time"},
+            "row_shard_all": row_all,
             "p50_ms": round(p50, 4),
             "p99_ms": round(p99, 4),
             "latency_note": "host-inclusive per batch: H2D queries + pipeline + D2H results, synchronous",
@@ -617,7 +675,8 @@ def run(args, stage: dict) -> None:
                              "rr_set_queries_device: the copy into the library's query buffer and the int8 screens' "
                              "query pieces, on its staging stream)" if not args.no_restage else
                              "the batch staged once, searched in every step"),
-            "host_pipelined": {"value": round(args.batch * args.latency_steps / host_pipe_s, 2), "unit": "queries/s",
+            "host_pipelined": {"value": round(args.batch * args.latency_steps * R / host_pipe_s, 2),
+                               "unit": "queries/s",
                                "batches": args.latency_steps, "in_flight": 2,
                                "note": "host numpy queries in, host results out: rr_search_async (pinned H2D + "
                                        "search + D2H enqueued) / rr_wait, two batches in flight"},
@@ -625,7 +684,7 @@ def run(args, stage: dict) -> None:
                                          "steady": st_acct.get("host_enqueue_ms_per_step"),
                                          "note": "host time to enqueue one search step (rr_search_staged) in the timed "
                                                  "loops: below ms_per_step, the device and not the host sets the rate"},
-            "steady_state": {"value": round(args.batch * args.steady_steps / st_el, 2), "unit": "queries/s",
+            "steady_state": {"value": round(args.batch * args.steady_steps * R / st_el, 2), "unit": "queries/s",
                              "steps": args.steady_steps,
                              "ms_per_step": round(st_el / args.steady_steps * 1e3, 4),
                              "kernel_avg_us": round(st_ms / max(st_n, 1) * 1e3, 2),
@@ -633,7 +692,7 @@ def run(args, stage: dict) -> None:
                              "note": "the same staged loop after the latency loops (GPU long out of idle); "
                                      "value above is the first K steps after W warm-up steps from idle"},
             "exchange": ("rccl ncclAllGather of per-shard top-k keys, device merge on every rank"
-                         if world > 1 or rccl_ranks else "none (one shard)"),
+                         if S > 1 or rccl_ranks else "none (one shard)"),
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "runtime default (4)"),
             "library_build": _lib.build_info(),
             "options": args.options,

@@ -65,8 +65,8 @@ constexpr int kQBufs = 4;
 // Host-side cost of enqueueing (diagnostics: RR_HOST_PROF=1 prints per-call averages at rr_destroy): [0] whole
 // rr_search_staged, [1] the pipelined exchange's enqueue, [2] the ncclAllGather call alone, [3] the screened block's
 // screen + verify launches; nanoseconds and calls.
-struct HostProf {
-  int64_t ns[10] = {}, n[10] = {};
+struct HostProf {   // (atomics: the exchange issue thread adds to its slots while the caller adds to others)
+  std::atomic<int64_t> ns[10] = {}, n[10] = {};
 };
 inline int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
@@ -1243,6 +1243,8 @@ struct XWorker {
   std::condition_variable cv;
   std::atomic<int64_t> posted{0}, done{0};
   std::atomic<bool> stop{false}, sleeping{false};
+  std::condition_variable done_cv;      // the caller's wait for issued exchanges, past its short spin (xw_wait)
+  std::atomic<bool> waiter{false};
   std::atomic<int> err{0};
   std::string errmsg;   // written by the worker before err (release), read by the caller after it (acquire)
   XJob ring[kRing];
@@ -1273,7 +1275,11 @@ void xw_main(rr_handle* h, XWorker* w) {
           w->err.store(rc, std::memory_order_release);
         }
       }
-      w->done.store(d + 1, std::memory_order_release);
+      w->done.store(d + 1, std::memory_order_seq_cst);
+      if (w->waiter.load(std::memory_order_seq_cst)) {   // the caller blocked in xw_wait (past its short spin)
+        std::lock_guard<std::mutex> lk(w->mu);
+        w->done_cv.notify_all();
+      }
       idle_since = now_ns();
       continue;
     }
@@ -1305,8 +1311,20 @@ int xw_wait(rr_handle* h, int64_t lag) {
   if (!w) return RR_OK;
   const auto t0 = std::chrono::steady_clock::now();
   const int64_t limit_ms = std::max<int64_t>(30000, h->timeout_ms);
-  while (w->posted.load(std::memory_order_relaxed) - w->done.load(std::memory_order_acquire) > lag) {
-    std::this_thread::yield();
+  auto pending = [&]() {
+    return w->posted.load(std::memory_order_relaxed) - w->done.load(std::memory_order_seq_cst) > lag;
+  };
+  // a short spin (the worker issues a posted exchange within tens of microseconds), then a blocking wait the worker
+  // wakes after each exchange it issues (bounded 1 ms waits: a missed wake-up costs at most that)
+  while (pending()) {
+    if (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200)) {
+      std::this_thread::yield();
+    } else {
+      std::unique_lock<std::mutex> lk(w->mu);
+      w->waiter.store(true, std::memory_order_seq_cst);
+      if (pending()) w->done_cv.wait_for(lk, std::chrono::milliseconds(1));
+      w->waiter.store(false, std::memory_order_relaxed);
+    }
     if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(limit_ms)) {
       h->failed = true;
       return fail(RR_E_TIMEOUT, "rank %d of %d: the exchange issue thread did not issue its posted exchanges within "

@@ -44,6 +44,31 @@ def broadcast_bytes(dist, payload: Optional[bytes], src: int = 0) -> bytes:
     return obj[0]
 
 
+def all_gather_bytes(dist, payload: Optional[bytes]) -> list:
+    """Every rank's payload, in rank order (world == 1: [payload])."""
+    if dist is None:
+        return [payload]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, payload)
+    return out
+
+
+def placement(n_docs: int, world: int, shard_group: int = 0, min_shard_rows: int = 500_000) -> Tuple[int, int]:
+    """(S, R): the ranks are split into R replica groups of S consecutive ranks; each group holds the whole corpus as S
+    contiguous row shards (one RCCL communicator per group: the per-block all-gather of candidates and the device
+    merge) and searches its own batches. shard_group > 0 fixes S; 0 (auto) takes the fewest ranks whose
+    shards still have >= min_shard_rows rows each — below that a shard's per-block fixed cost (screen start-up and
+    tail, the verify and staging chain: DESIGN §5 "Placement") outweighs the bytes it streams — and S is rounded up
+    to a divisor of world."""
+    if world <= 1:
+        return 1, 1
+    s = shard_group if shard_group > 0 else max(1, -(-n_docs // max(1, min_shard_rows)))
+    s = min(max(1, s), world)
+    while world % s:
+        s += 1
+    return s, world // s
+
+
 def max_over_ranks(dist, x: float) -> float:
     if dist is None:
         return x

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Staged-loop timeline of one shard (run under rocprofv3 --kernel-trace inside gpurun, then analyse here).
 
-    rocprofv3 --kernel-trace --output-format csv -d <dir> -o t -- python3 tools/step_timeline.py run [--docs N] [--x]
+    rocprofv3 --kernel-trace --output-format csv -d <dir> -o t -- python3 tools/step_timeline.py run [--docs N] [--x] [--restage]
     python3 tools/step_timeline.py analyse <dir>
 
 `run`: a 1-GPU handle on N synthetic unit-norm rows (optionally with a 1-rank RCCL communicator: --x, the multi-GPU
@@ -32,17 +32,28 @@ def run(argv):
     q = rng.standard_normal((32, 1024)).astype(np.float32)
     q /= np.linalg.norm(q, axis=1, keepdims=True)
     ix.set_queries(q)
-    for _ in range(50):
+    stage = lambda i: None
+    if "--restage" in argv:   # a new batch resident in HBM staged every step, as bench.py's timed loop
+        import torch
+        qs = rng.standard_normal((16, 32, 1024)).astype(np.float32)
+        qs /= np.linalg.norm(qs, axis=2, keepdims=True)
+        dev = torch.from_numpy(qs).to("cuda:0")
+        torch.cuda.synchronize()
+        ptrs = [dev[i].data_ptr() for i in range(16)]
+        stage = lambda i: ix.set_queries_device(ptrs[i % 16], 32, 1024)
+    for i in range(50):
+        stage(i)
         ix.search_staged(5)
     ix.synchronize()
     ix.stream_queues()            # marker: queue_probe_kernel launches separate warm-up and timed steps
     ix.synchronize()
     t = time.perf_counter()
-    for _ in range(300):
+    for i in range(300):
+        stage(i)
         ix.search_staged(5)
     ix.synchronize()
     el = time.perf_counter() - t
-    print({"docs": docs, "exchange": "--x" in argv, "qps": round(32 * 300 / el, 1), "ms_per_step": round(el / 300 * 1e3, 4)})
+    print({"docs": docs, "exchange": "--x" in argv, "restage": "--restage" in argv, "qps": round(32 * 300 / el, 1), "ms_per_step": round(el / 300 * 1e3, 4)})
     ix.close()
 
 
@@ -84,6 +95,10 @@ def analyse(d):
         fams.setdefault(f, []).append((b - a) / 1e3)
     for f, v in sorted(fams.items(), key=lambda x: -sum(x[1])):
         print(f"  {f:28s} n={len(v):4d} mean {statistics.mean(v):7.2f} us  sum/step {sum(v) / 300:7.2f} us")
+    scr = [r for r in win if r[2].endswith("screen")]
+    if len(scr) > 2:
+        st = [(scr[i + 1][0] - scr[i][0]) / 1e3 for i in range(len(scr) - 1)]
+        print(f"screen start-to-start median {statistics.median(st):.2f} us, mean {statistics.mean(st):.2f} us")
     for s in sorted({s for *_, s in win}):
         ks = [r for r in win if r[3] == s]
         if len(ks) < 50:
