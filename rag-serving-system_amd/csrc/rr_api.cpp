@@ -131,6 +131,10 @@ struct Shard {
   // on `stream` since its staging (a staging stream's next staging into t waits on ev_fork, recorded after each).
   hipStream_t sstream = nullptr;
   hipEvent_t ev_stage[kQBufs] = {};
+  // option stage_wait_value: each staging also writes its sequence number into stage_word[t] (a stream write-value
+  // packet after it), and a compute stream follows it by a wait-value packet instead of an event barrier
+  uint32_t* stage_word = nullptr;
+  uint32_t stage_seq[kQBufs] = {};
   bool stage_seen[kQBufs][2] = {};
   bool ns_rd[kQBufs] = {};
   int last_vsi = -1, last_vq = 0;   // the last screened verify: its stream index and query buffer
@@ -279,6 +283,7 @@ struct rr_handle {
                                 // a slower all-gather, for measurements and the deadline tests)
   int x_host_wait_us = 500;     // exchange issue thread: host wait for a px slot's previous exchange (x_host_wait_us)
   int x_thread = 1;             // multi-process mode: the exchange issue thread (x_thread; read at rr_init_dist)
+  int stage_wv = 0;             // option stage_wait_value (Shard::stage_word)
   int stage_mode = 0;           // where batches are staged (stage_stream): 0 = the next block's compute stream, 1 / 2 / 3 =
                                 // a staging stream at normal / greatest / least priority (measured slower: DESIGN §0)
   int screen_copy = 1;          // fp32 storage: keep an f16 copy for the screened search (rr_screen_copy); bf16: the int8 one
@@ -461,7 +466,7 @@ int free_shard(Shard& s) {
   for (int t = 0; t < kQBufs; ++t)
     for (void* p : {(void*)s.qbuf[t], (void*)s.q8t[t], (void*)s.q8st[t]})
       if (p) hipFree(p);
-  void* ptrs[] = {s.corpus, s.scr16, s.scr8, s.sx8, s.e8, s.norms, s.rscale, s.cand, s.scount, s.ctr, s.shard_keys, s.gathered, s.out_base,
+  void* ptrs[] = {s.corpus, s.scr16, s.scr8, s.sx8, s.e8, s.norms, s.rscale, s.cand, s.scount, s.ctr, s.stage_word, s.shard_keys, s.gathered, s.out_base,
                   s.full_keys, s.sort_temp, s.wcand, s.wfloor, s.wsel, s.rcmax[0], s.rcmax[1], s.rbits[0], s.rbits[1],
                   s.rlist[0], s.rlist[1], s.rcnt[0], s.rcnt[1]};
   for (void* p : ptrs)
@@ -895,6 +900,9 @@ int ensure_buffers(rr_handle* h, int b, int k) {
       for (int i = 0; i < 8; ++i) ((volatile int*)s.pin_scount)[i] = 0;
       if (int rc = dmalloc(&s.ctr, 4 * kCtrStride * sizeof(uint32_t))) return rc;
       HIP_TRY(hipMemset(s.ctr, 0, 4 * kCtrStride * sizeof(uint32_t)));
+      if (int rc = dmalloc(&s.stage_word, 64)) return rc;
+      HIP_TRY(hipMemset(s.stage_word, 0, 64));
+      for (int t = 0; t < kQBufs; ++t) s.stage_seq[t] = 0;
     }
     if ((h->world > 1 || h->dist) && !s.px_keys[0]) {
       for (int p = 0; p < kXSlots; ++p) {
@@ -1151,9 +1159,11 @@ int follow_fork(Shard& s) {
 // Compute stream si follows the staging of query buffer t (the copy and the int8 pieces, on the staging stream) before
 // its first kernel that reads them: one barrier packet per stream and staging, already satisfied when the staging ran
 // beside earlier searches.
-hipError_t follow_stage(Shard& s, int t, int si) {
+hipError_t follow_stage(const rr_handle* h, Shard& s, int t, int si) {
   if (s.stage_seen[t][si]) return hipSuccess;
   s.stage_seen[t][si] = true;
+  if (h->stage_wv && s.stage_word)   // (uint32 sequence: wraps after 2^32 stagings of one buffer)
+    return hipStreamWaitValue32(stream_of(s, si), s.stage_word + t, s.stage_seq[t], hipStreamWaitValueGte, 0xFFFFFFFFu);
   return wait_ev(stream_of(s, si), s.ev_stage[t]);
 }
 
@@ -1196,6 +1206,7 @@ int stage_queries(rr_handle* h, int t, const void* src, int b, int src_dev, bool
     } else {
       HIP_TRY(hipEventRecord(s.ev_stage[t], ss));
     }
+    if (h->stage_wv && s.stage_word) HIP_TRY(hipStreamWriteValue32(ss, s.stage_word + t, ++s.stage_seq[t], 0));
     s.stage_seen[t][0] = s.stage_seen[t][1] = false;
     if (x >= 0) s.stage_seen[t][x] = true;
   }
@@ -1555,7 +1566,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
         if (int rc = follow_fork(s)) return rc;
         s.c2_busy = true;
       }
-      HIP_TRY(follow_stage(s, t, bsi));   // the batch's rows and int8 pieces (staging stream)
+      HIP_TRY(follow_stage(h, s, t, bsi));   // the batch's rows and int8 pieces (staging stream)
       if (multi) {
         // px_keys[x]'s last reader is the exchange of the block kXSlots back. A stream wait on it is a barrier packet in
         // this compute stream's chain (prep, screen, verify): ~10-16 us of device latency per block even when the
@@ -1714,7 +1725,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
     } else if (kt) {
       int grid = fused_grid(s);
       HIP_TRY(wait_px(-1, s.stream));   // no screened verify still reads cand or writes the results
-      HIP_TRY(follow_stage(s, h->qpar, 0));
+      HIP_TRY(follow_stage(h, s, h->qpar, 0));
       s.ns_rd[h->qpar] = true;
       const bool ev_packet = s.rows() > 0 && use_sk(h);   // (timed: events on the launch packet, as above)
       if (timed && !ev_packet) HIP_TRY(hipEventRecord(e0, s.stream));
@@ -1747,7 +1758,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       // floors: unproven -> the block's flag word (the host re-runs the search with the full sort).
       HIP_TRY(wait_px(-1, s.stream));
       HIP_TRY(wait_copies());
-      HIP_TRY(follow_stage(s, h->qpar, 0));
+      HIP_TRY(follow_stage(h, s, h->qpar, 0));
       s.ns_rd[h->qpar] = true;
       if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
       uint64_t* flagw = multi ? s.shard_keys + (size_t)rr::kQSlots * k : (uint64_t*)s.out_base;
@@ -1815,7 +1826,7 @@ int enqueue_block_body(rr_handle* h, int q0, int bb, int k, int slots) {
       if (timed) HIP_TRY(hipEventRecord(e0, s.stream));
       HIP_TRY(wait_px(-1, s.stream));   // no pipelined exchange or screened verify still uses the buffers
       HIP_TRY(wait_copies());
-      HIP_TRY(follow_stage(s, h->qpar, 0));
+      HIP_TRY(follow_stage(h, s, h->qpar, 0));
       s.ns_rd[h->qpar] = true;
       HIP_TRY(hipMemsetAsync(s.shard_keys, 0, (size_t)rr::kQSlots * k * 8, s.stream));
       if (rows > 0) {
@@ -1981,6 +1992,7 @@ const OptionDesc kOptions[] = {
     {"screen_i8_min_rows", 0, INT64_MAX / 2},   // the int8 copy for shards of at least this many rows (next load)
     {"stage_stream", 0, 3},             // batches staged on: 0 the next block's compute stream, 1 / 2 / 3 the staging
                                         // stream at normal / greatest / least priority
+    {"stage_wait_value", 0, 1},         // a compute stream follows a staging by a stream wait-value packet, not an event
 };
 
 int64_t* option_field64(rr_handle* h, const std::string& n) { return n == "screen_i8_min_rows" ? &h->i8_min_rows : nullptr; }
@@ -1996,6 +2008,7 @@ int* option_field(rr_handle* h, const std::string& n) {
   if (n == "screen_i8_pieces") return &h->i8_pieces;
   if (n == "screen_guided") return &h->guided;
   if (n == "stage_stream") return &h->stage_mode;
+  if (n == "stage_wait_value") return &h->stage_wv;
   return nullptr;
 }
 int set_option(rr_handle* h, const OptionDesc& o, int64_t v) {

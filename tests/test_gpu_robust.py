@@ -255,3 +255,32 @@ def test_single_process_deadline_names_shard_and_stream(Index, monkeypatch):
     time.sleep(1.0)                                            # 24 ms of stand-in delay: the queues drain
     ix.close()
 
+
+
+@pytest.mark.parametrize("x", [False, True], ids=["local", "rccl1"])
+@pytest.mark.parametrize("mode,wv", [(0, 1), (1, 0), (1, 1), (2, 1)])
+def test_staging_placements_equal_the_exact_kernel(Index, mode, wv, x):
+    """Where a batch is staged (option stage_stream: the next block's compute stream, or a staging stream of its own
+    at normal / greatest priority) and how the compute streams follow it (stage_wait_value: an event barrier, or a
+    wait-value packet on the staging's sequence word): runs of 1..8 batches staged from HBM back to back with no host
+    wait in between, so each staging overlaps earlier searches; the last batch's results equal the exact kernel's.
+    Also through the 1-rank RCCL exchange path."""
+    torch = pytest.importorskip("torch")
+    from rag_service_amd import get_unique_id
+    corpus = synth.unit_norm_gaussian(91, 70000, 1024)          # >= 65536 rows: the int8 copy, its staged pieces
+    qs = np.stack([synth.unit_norm_gaussian(92 + i, 32, 1024) for i in range(8)])
+    dq = torch.from_numpy(qs).to("cuda:0")
+    torch.cuda.synchronize()
+    ex = _exact(Index, corpus)
+    want = [ex.search(qs[i], 5) for i in range(8)]
+    ex.close()
+    ix = Index(dtype="fp32", metric="cosine", options={"stage_stream": mode, "stage_wait_value": wv})
+    if x:
+        ix.init_dist(1, 0, get_unique_id())
+    ix.load(corpus)
+    for n in range(1, 9):
+        for i in range(n):
+            ix.set_queries_device(dq[i].data_ptr(), 32, 1024)
+            ix.search_staged(5)
+        assert _same(ix.fetch(), want[n - 1]), (mode, wv, x, n)
+    ix.close()
