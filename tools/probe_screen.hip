@@ -5,7 +5,9 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DRR_SK_PROBE -DRR_SK_NO_DISPATCH -I include \
 //         -I rag-serving-system_amd/csrc tools/probe_screen.hip -o tools/probe_screen
-//   tools/probe_screen [rows=125000] [grid=256] [ct8=2] [unused=0] [guided=1] [streams_test=0]
+//   tools/probe_screen [rows=125000] [grid=256] [ct8=2] [unused=0] [guided=1] [streams_test=0] [pieces=2]
+// (pieces: 2 = DT 8, the two-piece int8 screen; 1 = DT 9, one piece. The chunk geometry is computed on the host, as
+// launch_sk_args does since r6.)
 // (argument 4 was the rejected joiner prep, removed from the product kernel in r5; kept as a placeholder)
 // Phases per workgroup: start -> (1) prologue + query fragments -> (2) first tile -> (3) second tile -> (4) the rest of
 // its tiles -> (5) list merge and write. Printed: min / median / max over the workgroups, and the launch span.
@@ -84,14 +86,18 @@ int main(int argc, char** argv) {
   a.sx8 = sx;
   a.e8 = e8;
   a.ct8 = ct8;
-  auto kern = sk::sk_score_kernel<8, 2, 16, true, 2, 1, 0, 1, 0>;
-  const size_t lds = sk_lds_bytes(KDT_SCREEN8, true, 2, 32);
+  const int pieces = argc > 7 ? atoi(argv[7]) : 2;
+  auto kern = pieces == 1 ? sk::sk_score_kernel<9, 2, 16, true, 2, 1, 0, 1, 0> : sk::sk_score_kernel<8, 2, 16, true, 2, 1, 0, 1, 0>;
+  const int sdt = pieces == 1 ? KDT_SCREEN9 : KDT_SCREEN8;
+  const size_t lds = sk_lds_bytes(sdt, true, 2, 32);
   CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   std::vector<unsigned long long> h((size_t)grid * 8);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   a.no_guided = !guided;
+  a.geo = chunk_geo((a.n + 31) / 32, sk_chunk_tiles(sdt, a.d, a.ct8), grid, !a.no_guided);
+  a.geo_set = 1;
   for (int rep = 0; rep < 30; ++rep) {
     CK(hipEventRecord(e0, s));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads + 64), lds, s, a);
@@ -145,8 +151,8 @@ int main(int argc, char** argv) {
   }
   unsigned long long hf = 0;
   CK(hipMemcpy(&hf, flag, 8, hipMemcpyDeviceToHost));
-  printf("{\"guided\": %d, \"prep\": %d, \"flag\": %llu, \"rows\": %lld, \"grid\": %d, \"ct8\": %d, \"event_us\": %.2f, \"start_spread_us\": %.2f, \"span_us\": %.2f",
-         guided, prep, hf, (long long)n, grid, ct8, ms * 1e3, (t0max - t0min) / 100.0, (t5max - t0min) / 100.0);
+  printf("{\"pieces\": %d, \"guided\": %d, \"prep\": %d, \"flag\": %llu, \"rows\": %lld, \"grid\": %d, \"ct8\": %d, \"event_us\": %.2f, \"start_spread_us\": %.2f, \"span_us\": %.2f",
+         pieces, guided, prep, hf, (long long)n, grid, ct8, ms * 1e3, (t0max - t0min) / 100.0, (t5max - t0min) / 100.0);
   const char* ph[] = {"prologue", "tile0", "tile1", "rest", "merge"};
   for (int i = 1; i <= 5; ++i) {
     std::vector<double> v;
