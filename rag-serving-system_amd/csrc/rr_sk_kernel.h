@@ -1755,20 +1755,26 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
     // ---- wide phase: R = every list entry whose bound reaches R's bar (wide_bar; every key left out of the lists is
     // at most vtail, below the bar), rescored with exactly the arithmetic of the first tile (same K split, MFMA order,
     // wave order, epilogue), 32 rows a tile; complete when the exact k-th key is above vtail. Lists are disjoint (each
-    // workgroup its own rows).
+    // workgroup its own rows). The first tile's rows — akeys, the 32 largest list entries when no list was folded
+    // (nlists <= kThreads) — are not rescored (r6): their exact keys (the first tile's top-KT, xk) go back into the
+    // owner lanes' lists, and R's other entries follow. The top-k of exact keys over that superset of R is the same.
     int* wl = (int*)(smem + kWideListOff);
     const uint32_t tb_ord = (uint32_t)(*vtail >> 32);
     const uint32_t rbar = (uint32_t)vstate[4];
+    // list entries at or above done_from were the first tile's rows (keys are unique; akeys[31] = 0: every entry was)
+    const uint64_t done_from = a.nlists <= kThreads ? (akeys[31] ? akeys[31] : 1ull) : ~0ull;
     if (tid == 0) vstate[1] = 0;
     __syncthreads();
     for (int l = tid; l < a.nlists; l += kThreads) {
       const uint64_t* src = a.vin + ((size_t)vq * a.nlists + l) * (KT + 1);
       int c = 0;
       while (c < KT && (uint32_t)(src[c] >> 32) >= rbar) ++c;   // a prefix of the sorted list
-      if (c) {
-        const int pos = atomicAdd(&vstate[1], c);
-        for (int i = 0; i < c; ++i)
-          if (pos + i < kWideCap) wl[pos + i] = (int)((int64_t)(0xFFFFFFFFu - (uint32_t)src[i]) - idx_base);
+      int c0 = 0;
+      while (c0 < c && src[c0] >= done_from) ++c0;              // ... whose first c0 entries were scored already
+      if (c > c0) {
+        const int pos = atomicAdd(&vstate[1], c - c0);
+        for (int i = c0; i < c; ++i)
+          if (pos + i - c0 < kWideCap) wl[pos + i - c0] = (int)((int64_t)(0xFFFFFFFFu - (uint32_t)src[i]) - idx_base);
       }
     }
     __syncthreads();
@@ -1783,6 +1789,11 @@ __global__ __launch_bounds__(SCHED ? 576 : 512, 1) void sk_score_kernel(const Sk
       return;
     }
     tk.init();
+    if (done_from != ~0ull && owner && qe == vql) {   // the first tile's exact top-KT, spread over the query's LPQ lanes
+#pragma unroll
+      for (int i = 0; i < KT; ++i)
+        if (i % LPQ == lane % LPQ && xk[i] != 0) tk.insert(xk[i]);
+    }
     const int ntiles = (nr + 31) / 32;
     for (int t = 0; t < ntiles; ++t) {
       // this lane's MFMA row (r) and its epilogue rows (er + e)
