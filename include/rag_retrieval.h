@@ -296,7 +296,10 @@ int rr_screen_state(rr_handle* h, int32_t* full_lists, int64_t* pause_left, int6
  *   screen_i8_pieces     fp32 storage's int8 screen: query pieces, 0 (by shard size), 1 or 2
  *   screen_guided        2-tile chunks at the end of a screen launch (1)
  *   screen_full_lists    repair mode from the start and from every load on (0)
- *   screen_i8_min_rows   the int8 copy is made for shards of at least this many rows (65536; the next load) */
+ *   screen_i8_min_rows   the int8 copy is made for shards of at least this many rows (65536; the next load)
+ *   stage_stream         where a staged batch's copy and int8 pieces are made: 0 the next block's compute stream (0),
+ *                        1 / 2 / 3 a staging stream of its own at normal / greatest / least priority (measured slower)
+ *   stage_wait_value     a compute stream follows a staging by a stream wait-value packet instead of an event (0) */
 int rr_set_option(rr_handle* h, const char* name, int64_t value);
 int rr_get_option(const rr_handle* h, const char* name, int64_t* value);
 
