@@ -779,7 +779,8 @@ int drop_work_buffers(rr_handle* h) {
     }
     s.q8c = 0;
     s.last_vsi = -1;
-    void** ptrs[] = {(void**)&s.cand, (void**)&s.scount, (void**)&s.ctr, (void**)&s.shard_keys, (void**)&s.gathered,
+    void** ptrs[] = {(void**)&s.cand, (void**)&s.scount, (void**)&s.ctr, (void**)&s.stage_word, (void**)&s.shard_keys,
+                     (void**)&s.gathered,
                      (void**)&s.out_base, (void**)&s.full_keys, &s.sort_temp,
                      (void**)&s.wcand, (void**)&s.wfloor, (void**)&s.wsel, (void**)&s.rcmax[0], (void**)&s.rcmax[1],
                      (void**)&s.rbits[0], (void**)&s.rbits[1], (void**)&s.rlist[0], (void**)&s.rlist[1],
