@@ -350,6 +350,9 @@ def main() -> None:
                          "whose shards keep >= 500k rows (rag_service_amd.dist.placement); N = pure row shards")
     ap.add_argument("--no-row-shard-all", action="store_true",
                     help="with R > 1 replica groups, skip the second measurement over all N ranks as row shards")
+    ap.add_argument("--idle-start", action="store_true",
+                    help="prepare the step batches on the host after the corpus build (the round-5 order): the GPU idles "
+                         "for that preparation right before the warm-up steps")
     ap.add_argument("--same-device", action="store_true", help=argparse.SUPPRESS)   # (test hook: every rank on cuda:0)
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="a path setting of the measured handle (rr_set_option: screen_grid, verify_cus, x_slots, "
@@ -437,19 +440,25 @@ def run(args, stage: dict) -> None:
         ix.set_timeout(int(min(120.0, args.dist_timeout_s / 3) * 1000))
     # the hardware queues the handle's four streams dispatch to (distinct = none shares an in-order queue)
     queues = ix.stream_queues(0)
+    rng = np.random.default_rng(5678 + grp)   # (each replica group searches batches of its own)
+    q = rng.standard_normal((args.batch, args.dim)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    # The host-side preparation of the step batches (NumPy, torch's first device copy) comes BEFORE the corpus build
+    # unless --idle-start: the W warm-up and K timed steps then follow the build without the GPU idling for the ~5-10
+    # ms that preparation takes (measured both ways: DESIGN §4, profiles/r06/idle_start/). No GPU work is added.
+    if not args.idle_start:
+        stager, _keep = make_stager(ix, q, 16, local, not args.no_restage, 4242 + grp)
     stage["stage"] = "corpus fill"
     ix.fill_synthetic(_lib.RR_SYNTH_UNIT_NORM, 1234, args.docs, args.dim)
     if args.kernel != "auto":
         ix.set_kernel(args.kernel)
     sb, se = ix.shard_range(0)
-    rng = np.random.default_rng(5678 + grp)   # (each replica group searches batches of its own)
-    q = rng.standard_normal((args.batch, args.dim)).astype(np.float32)
-    q /= np.linalg.norm(q, axis=1, keepdims=True)
 
     # ---- throughput: queries resident in HBM, K back-to-back steps, each a new batch ---------------
     stage["stage"] = "timed steps"
     ix.set_queries(q)
-    stager, _keep = make_stager(ix, q, 16, local, not args.no_restage, 4242 + grp)
+    if args.idle_start:
+        stager, _keep = make_stager(ix, q, 16, local, not args.no_restage, 4242 + grp)
     acct = {}
     elapsed, kern_ms, launches = timed_steps(ix, args.k, args.steps, args.warmup, dist, cuda_sync, every, acct,
                                              stager)
@@ -671,6 +680,11 @@ def run(args, stage: dict) -> None:
             "p50_ms": round(p50, 4),
             "p99_ms": round(p99, 4),
             "latency_note": "host-inclusive per batch: H2D queries + pipeline + D2H results, synchronous",
+            "setup_order": ("--idle-start: the step batches prepared on the host after the corpus build (the GPU idle "
+                            "for that right before the W warm-up steps)" if args.idle_start else
+                            "the step batches prepared on the host before the corpus build, so the W warm-up and K timed "
+                            "steps follow the build without an idle gap (no GPU work added; --idle-start gives the other "
+                            "order: profiles/r06/idle_start/)"),
             "step_queries": ("every step stages a new batch resident in HBM (16 distinct unit-norm batches, "
                              "rr_set_queries_device: the copy into the library's query buffer and the int8 screens' "
                              "query pieces, on its staging stream)" if not args.no_restage else

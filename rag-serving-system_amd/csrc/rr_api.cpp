@@ -2113,6 +2113,17 @@ int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** 
       return fail(RR_E_HIP, "device %d setup failed: %s", devices[i], hipGetErrorString(e));
     }
   }
+  for (Shard& s : h->shards) {   // every kernel unit loaded on each device now, not inside the first search
+    if (!s.own_streams) continue;
+    if (hipError_t e = hipSetDevice(s.dev)) {
+      rr_destroy(h);
+      return fail(RR_E_HIP, "device %d: %s", s.dev, hipGetErrorString(e));
+    }
+    if (hipError_t e = rr::preload_kernels()) {
+      rr_destroy(h);
+      return fail(RR_E_HIP, "device %d: loading the kernels failed: %s", s.dev, hipGetErrorString(e));
+    }
+  }
   for (Shard& s : h->shards) {   // single-process exchange events (unused with one shard)
     hipError_t e = hipSetDevice(s.dev);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.keys_ready, hipEventDisableTiming);

@@ -263,6 +263,10 @@ hipError_t launch_f32_to_i8(const float* in, int64_t nrows, int d, int8_t* out, 
 // 31 (b <= 32) or round_up(b, 64) - 1 zeroed (qc >= that). qcopy (may be null): the fp32 rows are also copied there (fused staging copy).
 constexpr int kQ8Scalars = 6;
 hipError_t launch_q8_stage(const float* q, int b, int d, int8_t* q8, int qc, float* q8s, float* qcopy, hipStream_t s);
+// Load every kernel unit's code object on the current device (rr_create), and the units' own parts of it
+hipError_t preload_kernels();
+hipError_t preload_sk();
+hipError_t preload_topk();
 hipError_t launch_row_norms(int dtype, const void* corpus, int64_t n, int d, float* norms, hipStream_t s);
 hipError_t launch_synth(int kind, uint64_t seed, int64_t row_begin, int64_t n_rows, int d, float* out,
                         hipStream_t s);

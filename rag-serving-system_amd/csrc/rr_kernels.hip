@@ -1146,6 +1146,15 @@ hipError_t launch_f32_to_i8(const float* in, int64_t nrows, int d, int8_t* out, 
   return hipGetLastError();
 }
 
+// Every kernel unit's code object on the current device (rr_create): deferred loading otherwise loads a unit at the first
+// launch of one of its kernels — inside the first search (~8 ms for a split-K unit, profiles/r06/preload/).
+hipError_t preload_kernels() {
+  hipFuncAttributes fa;
+  if (hipError_t e = hipFuncGetAttributes(&fa, (const void*)q8_stage_kernel)) return e;
+  if (hipError_t e = preload_topk()) return e;
+  return preload_sk();
+}
+
 hipError_t launch_q8_stage(const float* q, int b, int d, int8_t* q8, int qc, float* q8s, float* qcopy, hipStream_t s) {
   // the rows any block reads: 32-slot blocks for b <= 32, else round_up(b, 64) (64-slot blocks, or 32-slot pairs)
   const int rows = b <= 32 ? 32 : (b + 63) / 64 * 64;

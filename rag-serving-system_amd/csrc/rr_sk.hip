@@ -13,6 +13,10 @@ hipError_t fam_exact(int sdt, int metric, int ns, int kt, int mode, int grid, in
 hipError_t fam_screen16(int sdt, int metric, int ns, int kt, int grid, const SkArgs& a, hipStream_t s);
 hipError_t fam_screen8(int metric, int ns, int kt, int grid, const SkArgs& a, hipStream_t s);
 hipError_t fam_screen9(int metric, int ns, int kt, int grid, int qslots, const SkArgs& a, hipStream_t s);
+hipError_t preload_fam_exact();
+hipError_t preload_fam_screen16();
+hipError_t preload_fam_screen8();
+hipError_t preload_fam_screen9();
 }  // namespace sk
 
 size_t sk_lds_bytes(int sdt, bool cos, int ring, int qslots) {
@@ -41,6 +45,12 @@ int sk_slabs(int sdt, int d) {
 }
 
 #ifndef RR_SK_NO_DISPATCH   // (diagnostic tools that instantiate one kernel directly: tools/probe_screen.hip)
+hipError_t preload_sk() {   // every split-K unit's code object on the current device
+  for (hipError_t (*f)() : {sk::preload_fam_exact, sk::preload_fam_screen16, sk::preload_fam_screen8, sk::preload_fam_screen9})
+    if (hipError_t e = f()) return e;
+  return hipSuccess;
+}
+
 hipError_t launch_sk_args(int sdt, int metric, int kt, int mode, int grid, int qslots, const SkArgs& a_in,
                           hipStream_t s, int ring) {
   const int ns = sk_slabs(sdt == KDT_SCREEN ? KDT_F32_X3 : sdt, a_in.d);

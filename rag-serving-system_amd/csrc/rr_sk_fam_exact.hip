@@ -25,5 +25,12 @@ hipError_t fam_exact(int sdt, int metric, int ns, int kt, int mode, int grid, in
     default: return hipErrorInvalidValue;
   }
 }
+// Load this unit's code object on the current device now (rr_create, rr_preload_kernels): with the runtime's deferred
+// loading the first launch of any of its kernels otherwise pays it — ~8 ms for a unit of split-K instantiations, inside
+// the first search (measured: the first verify 8 ms after its screen, profiles/r06/preload/).
+hipError_t preload_fam_exact() {
+  hipFuncAttributes fa;
+  return hipFuncGetAttributes(&fa, (const void*)sk_score_kernel<3, 4, 16, true, 2, 1, 1, 0, 0>);
+}
 }  // namespace sk
 }  // namespace rr

@@ -21,5 +21,12 @@ hipError_t screen16(int metric, int ns, int kt, int grid, const SkArgs& a, hipSt
 hipError_t fam_screen16(int sdt, int metric, int ns, int kt, int grid, const SkArgs& a, hipStream_t s) {
   return sdt == KDT_SCREEN16 ? screen16<7>(metric, ns, kt, grid, a, s) : screen16<6>(metric, ns, kt, grid, a, s);
 }
+// Load this unit's code object on the current device now (rr_create, rr_preload_kernels): with the runtime's deferred
+// loading the first launch of any of its kernels otherwise pays it — ~8 ms for a unit of split-K instantiations, inside
+// the first search (measured: the first verify 8 ms after its screen, profiles/r06/preload/).
+hipError_t preload_fam_screen16() {
+  hipFuncAttributes fa;
+  return hipFuncGetAttributes(&fa, (const void*)sk_score_kernel<7, 2, 16, true, 2, 1, 0, 1, 0>);
+}
 }  // namespace sk
 }  // namespace rr

@@ -20,5 +20,12 @@ hipError_t fam_screen9(int metric, int ns, int kt, int grid, int qslots, const S
                : launch_metric<9, 2, 1, 0, 0, 1>(metric, ns, kt, grid, a, s);
   return dyn ? launch_metric<9, 2, 1, 0, 1>(metric, ns, kt, grid, a, s) : launch_metric<9, 2, 1>(metric, ns, kt, grid, a, s);
 }
+// Load this unit's code object on the current device now (rr_create, rr_preload_kernels): with the runtime's deferred
+// loading the first launch of any of its kernels otherwise pays it — ~8 ms for a unit of split-K instantiations, inside
+// the first search (measured: the first verify 8 ms after its screen, profiles/r06/preload/).
+hipError_t preload_fam_screen9() {
+  hipFuncAttributes fa;
+  return hipFuncGetAttributes(&fa, (const void*)sk_score_kernel<9, 2, 16, true, 2, 1, 0, 1, 0>);
+}
 }  // namespace sk
 }  // namespace rr

@@ -182,6 +182,11 @@ size_t topk_scratch_bytes(int b, int64_t k) {
   return ((size_t)b * sizeof(TkState) + 255) / 256 * 256 + (size_t)b * 256 * 4 + 256 + (size_t)b * k * 8;
 }
 
+hipError_t preload_topk() {   // (rr_kernels.hip preload_kernels)
+  hipFuncAttributes fa;
+  return hipFuncGetAttributes(&fa, (const void*)tk_init_kernel);
+}
+
 hipError_t launch_topk_sorted(const uint64_t* in, int b, int64_t seg, int64_t k, uint64_t* out, void* scratch,
                               hipStream_t s) {
   if (b < 1 || seg < 1 || k < 1 || !in || !out || !scratch) return hipErrorInvalidValue;
