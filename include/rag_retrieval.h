@@ -86,7 +86,8 @@ typedef struct rr_handle rr_handle;
 /* ---- lifecycle ---------------------------------------------------------------------------------- */
 
 /* Create a handle over n_dev local shards on the given devices (HIP ordinals, repeats allowed).
- * devices == NULL means {0}.
+ * devices == NULL means {0}. Loads every kernel unit's code object on each device (tens of ms the first time in a
+ * process), so no search pays the runtime's deferred loading.
  * Replaces CupyRetriever.__init__'s device setup (retriever.py:580-586). */
 int rr_create(const int* devices, int n_dev, int dtype, int metric, rr_handle** out);
 
