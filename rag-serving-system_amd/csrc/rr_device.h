@@ -124,6 +124,23 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   v = dpp_max_u32<0x143, 0xC>(v);                   // row_bcast:31 into rows 2, 3: lane 63 has the max
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
+// fp32 sum over the 64 lanes with DPP, in lane 63's order, returned in every lane (the staging kernel's norms: one VALU per
+// step instead of an LDS round trip per __shfl_xor level)
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dpp_add_f32(float v) {
+  const int t = ROW_MASK == 0xF ? __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true)
+                                : __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xF, false);
+  return v + __builtin_bit_cast(float, t);
+}
+__device__ __forceinline__ float wave_sum_f32(float v) {
+  v = dpp_add_f32<0xB1>(v);        // quad_perm [1,0,3,2]
+  v = dpp_add_f32<0x4E>(v);        // quad_perm [2,3,0,1]
+  v = dpp_add_f32<0x141>(v);       // row_half_mirror: the other quad of the half-row
+  v = dpp_add_f32<0x140>(v);       // row_mirror: the other half of the row
+  v = dpp_add_f32<0x142, 0xA>(v);  // row_bcast:15 into rows 1, 3 (rows 0, 2 add 0)
+  v = dpp_add_f32<0x143, 0xC>(v);  // row_bcast:31 into rows 2, 3: lane 63 holds the sum
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
 template <int G>
 __device__ __forceinline__ uint64_t group_max_u64(uint64_t x) {
   const uint32_t hi = group_max_u32<G>((uint32_t)(x >> 32));
@@ -200,11 +217,10 @@ __device__ __forceinline__ void q8_stage_row(const float* __restrict__ q, int b,
     }
   }
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    m = fmaxf(m, __shfl_xor(m, off, 64));
-    s2 += __shfl_xor(s2, off, 64);
-    s1 += __shfl_xor(s1, off, 64);
-  }
+  for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));   // (fmaxf: a NaN element is dropped)
+  // (the sums' order is a DPP tree's: |q| and sum|q| carry relative bumps for any order, q8s below)
+  s2 = wave_sum_f32(s2);
+  s1 = wave_sum_f32(s1);
   const float s = m > 0.f ? m / 127.0f : 0.f;
   float se1 = 0.f, se2 = 0.f;
   auto pass2 = [&](const f32x4 v, int c) {
@@ -234,11 +250,8 @@ __device__ __forceinline__ void q8_stage_row(const float* __restrict__ q, int b,
   } else {
     for (int c = lane; c < (d >> 2); c += 64) pass2(src[c], c);
   }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    se1 += __shfl_xor(se1, off, 64);
-    se2 += __shfl_xor(se2, off, 64);
-  }
+  se1 = wave_sum_f32(se1);
+  se2 = wave_sum_f32(se2);
   if (lane == 0) {
     const float abs_term = fmaf(m, sqrtf((float)d) * 0x1p-21f, 0x1p-140f);
     q8s[row] = sqrtf(s2);

@@ -25,9 +25,9 @@ def quantize_rows(x):
 
 
 def quantize_query(v, pieces=2):
-    """q8_prep_kernel: t = q / s, p1 = clamp(rint(t)), p2 = clamp(rint((t - p1) 64)); eq from the exact scaled
-    residual t - p1 - p2 / 64. pieces = 1 (q9_prep_kernel, rr_device.h q8_prep_slot<1>): p2 = 0, the residual t - p1,
-    the scale s itself."""
+    """The staged pieces (rr_device.h q8_stage_row, once per staged batch): t = q / s, p1 = clamp(rint(t)),
+    p2 = clamp(rint((t - p1) 64)); eq from the exact scaled residual t - p1 - p2 / 64. pieces = 1 (DT 9 reads p1 and
+    the one-piece scalars of the same staging): p2 = 0, the residual t - p1, the scale s itself."""
     m = F(np.abs(v).max())
     s = F(m / F(127)) if m > 0 else F(0)
     with np.errstate(under="ignore"):
