@@ -31,3 +31,25 @@ def test_bench_line(hip, exchange):
     assert r["kernel_alone"] and r["kernel_alone"]["launches"] == 40
     assert rec["rccl_ranks"] == (1 if exchange else 0)
     assert rec["exchange"].startswith("rccl") == exchange
+
+
+def test_bench_replica_groups_on_one_gpu(hip):
+    """The N > 1 placement path (R replica groups) end to end: two ranks launched the driver's way (`--gpus 2` spawns
+    torch.distributed.run), both on cuda:0 (test hook --same-device), each a whole-corpus replica with a 1-rank RCCL
+    exchange searching its own batches; rank 0's line counts both groups' batches (parallelism and scaling say so).
+    The groups' 2-rank communicators need distinct GPUs and are not reachable on a one-GPU box."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--same-device", "--shard-group", "1",
+           "--exchange-1rank", "--no-row-shard-all", "--docs", "70000", "--steps", "12", "--warmup", "3",
+           "--latency-steps", "4", "--steady-steps", "12", "--no-cpu-baseline", "--variants", "", "--ingest-rows", "0",
+           "--no-pmc"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=150, cwd=REPO, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    recs = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(recs) == 1, out.stdout[-2000:]
+    rec = recs[0]
+    assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["scaling"] == "weak"
+    assert rec["placement"]["shard_group"] == 1 and rec["placement"]["replica_groups"] == 2
+    assert rec["config"]["parallelism"] == "row-shard x1, replica groups x2"
+    assert rec["rccl_ranks"] == 1 and rec["row_shard_all"] is None
+    assert rec["roofline"]["screen_fallbacks"] == 0
